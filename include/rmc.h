@@ -1,0 +1,200 @@
+/*
+ * rmc.h — C ABI of librmc.so, the MI355X-native breadth-first model checker
+ * for raft.tla (the hot path of TLC's `tlc2.TLC -config MCraft.cfg MCraft.tla`).
+ *
+ * The reference path has no FFI of its own: it sits behind TLC's CLI and file
+ * formats.  Each entry point below replaces one piece of that
+ * path; the reference interface it replaces is cited next to it.  A Java
+ * driver binds these through Panama FFM; the C++ CLI
+ * (`bin/rmc-tlc`) and the Python ctypes harness (tests, bench) bind the same
+ * symbols.
+ *
+ * Conventions: plain C types only; return 0 on success and a negative code
+ * otherwise (RMC_E_*); the message is available from rmc_last_error(ctx).
+ * No C++ exception crosses the ABI.  A ctx owns all device memory; output
+ * buffers are caller-owned.  Calls on one ctx are not reentrant.
+ */
+#ifndef RMC_H_
+#define RMC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMC_ABI_VERSION 1
+
+/* Capacity of the packed encoding (DESIGN.md "Packed state"). */
+#define RMC_MAX_SERVERS 5
+#define RMC_MAX_VALUES 2
+#define RMC_MAX_LOG 3      /* MaxLogLen bound <= 3 */
+#define RMC_MAX_MSGS 8     /* |DOMAIN messages| bound <= 8 */
+#define RMC_MAX_TERM 14    /* MaxTerm bound <= 14 */
+#define RMC_MAX_DUP 3      /* per-message count bound <= 3 */
+
+/* Error codes. */
+#define RMC_OK 0
+#define RMC_E_INVAL (-22)      /* config validation failed (TLC: semantic error) */
+#define RMC_E_NOMEM (-12)      /* device allocation failed */
+#define RMC_E_HIP (-5)         /* HIP runtime error */
+#define RMC_E_CAPACITY (-28)   /* fingerprint set / state store full (TLC spills to disk; we stop) */
+#define RMC_E_NOGPU (-19)      /* no usable gfx950 device */
+#define RMC_E_PARSE (-74)      /* .cfg / .tla front-end could not recognise the model */
+#define RMC_E_STATE (-71)      /* call out of order (e.g. rmc_trace before a violation) */
+
+/* rmc_config.flags */
+#define RMC_FLAG_SYMMETRY (1u << 0)        /* SYMMETRY Permutations(Server)            */
+#define RMC_FLAG_CHECK_DEADLOCK (1u << 1)  /* CHECK_DEADLOCK TRUE (TLC default)         */
+#define RMC_FLAG_BUG_QUORUM (1u << 2)      /* BecomeLeader guard raft.tla:197 weakened  */
+                                           /* to votesGranted[i] /= {} (config 5)       */
+
+/* rmc_config.invariants — the INVARIANT names the engine knows (fused checks). */
+#define RMC_INV_TYPEOK (1u << 0)           /* raft.tla:482-492                          */
+#define RMC_INV_ONE_LEADER (1u << 1)       /* ElectionSafety restated (raft.tla:1124)   */
+#define RMC_INV_LOG_MATCHING (1u << 2)     /* raft.tla:1132-1136                        */
+
+/* A bounded model: constants of the MC module + the CONSTRAINT bounds.
+ * Replaces the CONSTANTS / CONSTRAINT / INVARIANT / SYMMETRY / CHECK_DEADLOCK
+ * sections of a TLC .cfg (MCraft.cfg:1-39, Smokeraft.cfg:43-48). */
+typedef struct rmc_config {
+    int32_t n_servers;        /* |Server|  (MCraft.tla:20-21: {r1,r2,r3})        */
+    int32_t n_values;         /* |Value|   (MCraft.tla:15-16: {v1,v2})           */
+    int32_t max_term;         /* CONSTRAINT \A i: currentTerm[i] <= max_term      */
+    int32_t max_log_len;      /* CONSTRAINT \A i: Len(log[i]) <= max_log_len      */
+    int32_t max_msgs;         /* CONSTRAINT Cardinality(DOMAIN messages) <= ..    */
+    int32_t max_dup;          /* CONSTRAINT \A m: messages[m] <= max_dup          */
+    uint32_t flags;           /* RMC_FLAG_*                                       */
+    uint32_t invariants;      /* RMC_INV_*                                        */
+    int32_t device;           /* HIP device ordinal                               */
+    int32_t max_depth;        /* 0 = unbounded; else stop after this many levels  */
+    uint64_t state_capacity;  /* distinct states this GPU may store; 0 = auto     */
+    uint64_t seed;            /* simulation seed (unused by BFS)                  */
+} rmc_config;
+
+/* End-of-run summary.  Replaces TLC's stdout summary lines:
+ * "N states generated, M distinct states found, Q states left on queue." and
+ * "The depth of the complete state graph search is D." */
+typedef struct rmc_result {
+    uint64_t generated;        /* init states + every successor of every expanded state */
+    uint64_t distinct;         /* distinct (canonical) states found                     */
+    uint64_t left_on_queue;    /* frontier states not expanded at stop                  */
+    int32_t depth;             /* BFS levels (init = level 1)                           */
+    int32_t violated_inv;      /* RMC_INV_* bit of the violated invariant, or 0         */
+    int32_t violation_depth;   /* level of the violating state, or 0                    */
+    int32_t deadlock;          /* 1 if a state without successors was found             */
+    double collision_probability; /* fingerprint collision estimate (TLC prints one too) */
+    double seconds;            /* wall time of rmc_run_bfs                              */
+    double expand_kernel_seconds; /* device time of the expansion kernels, HIP events on */
+                                  /* the ctx stream (sum over levels)                    */
+    uint64_t expand_launches;  /* levels expanded (one timed launch group per level)    */
+} rmc_result;
+
+/* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */
+typedef struct rmc_level_stats {
+    int32_t level;             /* level just completed (its successors were generated)  */
+    int32_t pad;
+    uint64_t generated;        /* cumulative generated                                  */
+    uint64_t distinct;         /* cumulative distinct                                   */
+    uint64_t new_states;       /* distinct states found at level+1                      */
+    double seconds;            /* wall time since rmc_run_bfs started                   */
+} rmc_level_stats;
+
+/* Return non-zero to stop the search early. */
+typedef int (*rmc_progress_fn)(const rmc_level_stats* stats, void* user);
+
+/* A decoded state in neutral form, for traces and tests.  Field meanings are
+ * the TLA+ variables of raft.tla:31-67; Nil = -1; roles 0/1/2 =
+ * Follower/Candidate/Leader; mtype 0..3 = RequestVoteRequest,
+ * RequestVoteResponse, AppendEntriesRequest, AppendEntriesResponse.
+ * Fields that do not apply to a message type are 0. */
+typedef struct rmc_entry { int32_t term, value; } rmc_entry;
+typedef struct rmc_msg_view {
+    int32_t mtype, mterm, msource, mdest;
+    int32_t mlastLogTerm, mlastLogIndex;                      /* RequestVoteRequest    */
+    int32_t mvoteGranted, mlog_len;                           /* RequestVoteResponse   */
+    rmc_entry mlog[RMC_MAX_LOG];
+    int32_t mprevLogIndex, mprevLogTerm, mentries_len;        /* AppendEntriesRequest  */
+    rmc_entry mentries[1];
+    int32_t mcommitIndex;
+    int32_t msuccess, mmatchIndex;                            /* AppendEntriesResponse */
+    int32_t count;                                            /* bag multiplicity >= 1 */
+} rmc_msg_view;
+typedef struct rmc_state_view {
+    int32_t n_servers, n_msgs;
+    int32_t currentTerm[RMC_MAX_SERVERS];
+    int32_t state[RMC_MAX_SERVERS];
+    int32_t votedFor[RMC_MAX_SERVERS];
+    int32_t commitIndex[RMC_MAX_SERVERS];
+    int32_t log_len[RMC_MAX_SERVERS];
+    rmc_entry log[RMC_MAX_SERVERS][RMC_MAX_LOG];
+    uint32_t votesResponded[RMC_MAX_SERVERS];   /* bitmask over server ids */
+    uint32_t votesGranted[RMC_MAX_SERVERS];
+    int32_t nextIndex[RMC_MAX_SERVERS][RMC_MAX_SERVERS];
+    int32_t matchIndex[RMC_MAX_SERVERS][RMC_MAX_SERVERS];
+    rmc_msg_view msgs[RMC_MAX_MSGS];
+} rmc_state_view;
+
+/* One successor produced by rmc_expand (differential tests). */
+typedef struct rmc_succ_view {
+    uint64_t parent;           /* index into the input array                       */
+    int32_t family;            /* 0..9 = Restart .. DropMessage (raft.tla:421-430)  */
+    int32_t instance;          /* lane id within the state (DESIGN.md lane table)   */
+    int32_t in_constraint;     /* 1 if the successor satisfies the CONSTRAINT       */
+    int32_t pad;
+    uint64_t fingerprint;
+    rmc_state_view state;      /* valid when in_constraint                          */
+} rmc_succ_view;
+
+typedef struct rmc_ctx rmc_ctx;
+
+/* ---- lifecycle ----------------------------------------------------------
+ * rmc_create replaces TLC's model setup: cfg binding, ASSUME checks
+ * (raft.tla:494-503, trivially true for model values), and FPSet/queue
+ * allocation.  It validates the config and allocates the device state store,
+ * fingerprint table and parent array on `cfg->device`. */
+int rmc_create(const rmc_config* cfg, rmc_ctx** out);
+void rmc_destroy(rmc_ctx* ctx);
+const char* rmc_last_error(const rmc_ctx* ctx);   /* never NULL */
+const char* rmc_version(void);                    /* "rmc <abi> gfx950 ..."           */
+
+/* ---- breadth-first search ----------------------------------------------
+ * Replaces TLC's BFS worker loop (ModelChecker: dequeue, getNextStates over
+ * Next raft.tla:421-430, CONSTRAINT filter, FP64 + FPSet.put, invariant check,
+ * enqueue).  Blocks until fixpoint, first violation, deadlock (when checked),
+ * max_depth, or the callback asks to stop. */
+int rmc_run_bfs(rmc_ctx* ctx, rmc_progress_fn cb, void* user);
+int rmc_get_result(const rmc_ctx* ctx, rmc_result* out);
+
+/* Counterexample: the states from an initial state to the violating (or
+ * deadlocked) state, in order, with the action family and lane of the step
+ * into each state (-1 for the initial state).  Replaces TLC's trace
+ * reconstruction from the states/ trace file ("State 1: ... State d").
+ * *len receives the trace length even if it exceeds cap. */
+int rmc_trace(rmc_ctx* ctx, rmc_state_view* states, int32_t* families, int32_t* instances,
+              size_t cap, size_t* len);
+
+/* ---- codec and successor enumeration (tests, Java driver printing) -------
+ * rmc_state_bytes: bytes of one packed state for this config.
+ * rmc_expand: run the SAME device successor code as the BFS on n caller
+ * states (no dedup) and return every enabled lane's successor.  *n_out
+ * receives the number of successors even if it exceeds cap. */
+size_t rmc_state_bytes(const rmc_config* cfg);
+int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_view* out,
+               size_t cap, size_t* n_out);
+
+/* ---- front-end -----------------------------------------------------------
+ * Reads a TLC model (.tla root module + .cfg) of raft.tla and fills *cfg.
+ * Recognises: CONSTANTS (model values, `X <- def`, `Name = n` for bounds),
+ * SPECIFICATION / INIT / NEXT, INVARIANT(S), CONSTRAINT(S), SYMMETRY,
+ * CHECK_DEADLOCK, and `BecomeLeader <- Def` overrides whose body weakens the
+ * quorum guard.  `tla_path` may be NULL (the module next to cfg_path with the
+ * same stem is used).  Errors name the unsupported construct in err. */
+int rmc_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* cfg,
+                          char* err, size_t err_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RMC_H_ */

@@ -1,0 +1,522 @@
+// raft_packed.h — bit-packed raft.tla state and the per-lane successor logic.
+//
+// One state = S 64-bit server words + K 32-bit bag slots (DESIGN.md "Packed
+// state").  Every action of Next (raft.tla:421-430) changes at most ONE server
+// word plus at most one bag add and one bag remove, so a lane computes a
+// successor as a *delta* against its parent (server index + new word, slot to
+// decrement, message to add) and its fingerprint incrementally from the
+// parent's.  Only successors that turn out to be new are materialised.
+//
+// This header is compiled for the host (codec, tests) and for gfx950 (the
+// expansion kernels); nothing in it allocates or loops unboundedly.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define RMC_HD __host__ __device__ __forceinline__
+#else
+#define RMC_HD inline
+#endif
+
+namespace rmc {
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+// ---- server word (raft.tla:37-67, one per server) ---------------------------
+//  bits  0-3  currentTerm          bits 11-12 Len(log)
+//  bits  4-5  state (F/C/L)        bits 13-27 log[1..3], 5 bits each: term(4) | value(1)<<4
+//  bits  6-8  votedFor (7 = Nil)   bits 28..  votesResponded (S), votesGranted (S),
+//  bits  9-10 commitIndex                     nextIndex-1 (2 bits x S), matchIndex (2 bits x S)
+constexpr int CT_SH = 0, ST_SH = 4, VF_SH = 6, CI_SH = 9, LEN_SH = 11, LOG_SH = 13;
+constexpr int ENT_W = 5, LOG_CAP = 3;
+constexpr int VR_SH = LOG_SH + LOG_CAP * ENT_W;  // 28
+constexpr u32 NILV = 7;
+enum : u32 { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
+enum : u32 { RVQ = 0, RVP = 1, AEQ = 2, AEP = 3 };  // raft.tla:23-24
+// Fields kept by Restart (raft.tla:136-143): currentTerm, votedFor, log.
+constexpr u64 RESTART_KEEP = 0xFull | (0x7ull << VF_SH) | (0x1FFFFull << LEN_SH);
+
+template <int S>
+struct SL {
+    static constexpr int VR = VR_SH, VG = VR_SH + S, NI = VR_SH + 2 * S, MI = VR_SH + 4 * S;
+    static constexpr int END = VR_SH + 6 * S;
+    static_assert(END <= 59, "server word overflow");
+    static constexpr u32 SMASK = (1u << S) - 1;
+};
+
+RMC_HD u32 bits(u64 w, int sh, int n) { return (u32)((w >> sh) & ((1ull << n) - 1)); }
+RMC_HD u64 setbits(u64 w, int sh, int n, u64 v) {
+    const u64 m = ((1ull << n) - 1) << sh;
+    return (w & ~m) | ((v << sh) & m);
+}
+RMC_HD u32 w_ct(u64 w) { return bits(w, CT_SH, 4); }
+RMC_HD u32 w_st(u64 w) { return bits(w, ST_SH, 2); }
+RMC_HD u32 w_vf(u64 w) { return bits(w, VF_SH, 3); }
+RMC_HD u32 w_ci(u64 w) { return bits(w, CI_SH, 2); }
+RMC_HD u32 w_len(u64 w) { return bits(w, LEN_SH, 2); }
+RMC_HD u32 w_ent(u64 w, u32 k) { return bits(w, LOG_SH + ENT_W * (int)k, ENT_W); }  // k 0-based
+RMC_HD u32 ent_term(u32 e) { return e & 15u; }
+RMC_HD u32 w_last_term(u64 w) {  // LastTerm raft.tla:84
+    const u32 n = w_len(w);
+    return n ? ent_term(w_ent(w, n - 1)) : 0u;
+}
+template <int S> RMC_HD u32 w_vr(u64 w) { return bits(w, SL<S>::VR, S); }
+template <int S> RMC_HD u32 w_vg(u64 w) { return bits(w, SL<S>::VG, S); }
+template <int S> RMC_HD u32 w_ni(u64 w, u32 j) { return bits(w, SL<S>::NI + 2 * (int)j, 2) + 1u; }
+template <int S> RMC_HD u32 w_mi(u64 w, u32 j) { return bits(w, SL<S>::MI + 2 * (int)j, 2); }
+
+// ---- bag slot (raft.tla:31, messages) -----------------------------------------
+//  bits 0-1 mtype, 2-4 msource, 5-7 mdest, 8-11 mterm, 12-29 body, 30-31 count (1..3)
+//  RVQ body: mlastLogTerm 12-15, mlastLogIndex 16-17
+//  RVP body: mvoteGranted 12, mlog 13-29 (= server-word bits 11-27: len + entries)
+//  AEQ body: mprevLogIndex 12-13, mprevLogTerm 14-17, Len(mentries) 18, entry 19-23, mcommitIndex 24-25
+//  AEP body: msuccess 12, mmatchIndex 13-14
+// An empty slot is 0 (a live slot has count >= 1).  Canonical bags are sorted
+// descending by slot value, so empty slots come last.
+constexpr u32 MSG_MASK = (1u << 30) - 1;
+constexpr u32 CNT_ONE = 1u << 30;
+RMC_HD u32 m_type(u32 m) { return m & 3u; }
+RMC_HD u32 m_src(u32 m) { return (m >> 2) & 7u; }
+RMC_HD u32 m_dst(u32 m) { return (m >> 5) & 7u; }
+RMC_HD u32 m_term(u32 m) { return (m >> 8) & 15u; }
+RMC_HD u32 m_cnt(u32 slot) { return slot >> 30; }
+RMC_HD u32 m_hdr(u32 type, u32 src, u32 dst, u32 term) {
+    return type | (src << 2) | (dst << 5) | (term << 8);
+}
+
+// ---- fingerprint ----------------------------------------------------------------
+// fp(s) = sum_i mix(w_i ^ tag_i) + sum_{live slots} mix(slot ^ tag_M)  (mod 2^64)
+// A sum of per-component mixes is canonical for the bag (order-free) and can be
+// updated in O(changed components) per successor.
+RMC_HD u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+RMC_HD u64 hS(u64 w, u32 i) { return mix64(w ^ ((u64)(i + 1) << 59)); }
+RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59)) : 0ull; }
+
+// ---- model parameters (runtime part) --------------------------------------------
+struct Params {
+    int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;
+    int off[11];  // family lane offsets; off[10] = lanes per state
+};
+
+// Lane table: Restart S, Timeout S, RequestVote S^2,
+// BecomeLeader S, ClientRequest S*V, AdvanceCommitIndex S, AppendEntries S^2,
+// Receive K, DuplicateMessage K, DropMessage K.
+template <int S, int K>
+inline void make_offsets(Params& P) {
+    const int sizes[10] = {S, S, S * S, S, S * P.V, S, S * S, K, K, K};
+    P.off[0] = 0;
+    for (int f = 0; f < 10; ++f) P.off[f + 1] = P.off[f] + sizes[f];
+}
+
+// A successor relative to its parent.
+struct Delta {
+    u64 w_new;    // new word of server `srv`
+    int srv;      // -1: no server word changes
+    int rm;       // bag slot to decrement, -1: none
+    u32 add;      // message (30 bits) to add when has_add
+    int has_add;
+    int en;       // lane enabled (counts as generated)
+};
+
+template <int S>
+RMC_HD u64 selw(const u64 (&w)[S], int i) {
+    u64 r = w[0];
+#pragma unroll
+    for (int k = 1; k < S; ++k) r = (i == k) ? w[k] : r;
+    return r;
+}
+template <int K>
+RMC_HD u32 selm(const u32 (&m)[K], int i) {
+    u32 r = m[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) r = (i == k) ? m[k] : r;
+    return r;
+}
+
+// Receive(m) raft.tla:388-403 for bag slot k (message `msg`).
+template <int S, int K>
+RMC_HD void receive_lane(const u64 (&w)[S], u32 msg, int k, Delta& d) {
+    const u32 i = m_dst(msg), j = m_src(msg), mterm = m_term(msg), mt = m_type(msg);
+    const u64 wi = selw<S>(w, (int)i);
+    const u32 ct = w_ct(wi), st = w_st(wi), len = w_len(wi);
+    d.srv = (int)i;
+    d.w_new = wi;
+    if (mterm > ct) {  // UpdateTerm :373-379 — m stays in the bag
+        u64 wn = setbits(wi, CT_SH, 4, mterm);
+        wn = setbits(wn, ST_SH, 2, FOLLOWER);
+        d.w_new = setbits(wn, VF_SH, 3, NILV);
+        d.en = 1;
+        return;
+    }
+    if (mt == RVQ) {  // HandleRequestVoteRequest :244-263 (mterm <= ct here)
+        const u32 lt = w_last_term(wi);
+        const u32 mlt = (msg >> 12) & 15u, mli = (msg >> 16) & 3u;
+        const bool log_ok = mlt > lt || (mlt == lt && mli >= len);
+        const u32 vf = w_vf(wi);
+        const bool grant = mterm == ct && log_ok && (vf == NILV || vf == j);
+        if (grant) d.w_new = setbits(wi, VF_SH, 3, j);
+        // Reply :102-103 — response carries mlog = log[i] (len + entries bits)
+        d.add = m_hdr(RVP, i, j, ct) | ((grant ? 1u : 0u) << 12) | (bits(wi, LEN_SH, 17) << 13);
+        d.has_add = 1;
+        d.rm = k;
+        d.en = 1;
+        return;
+    }
+    if (mt == RVP) {
+        d.rm = k;
+        d.en = 1;
+        if (mterm < ct) return;  // DropStaleResponse :382-385
+        // HandleRequestVoteResponse :267-279
+        u64 wn = wi | (1ull << (SL<S>::VR + (int)j));
+        if ((msg >> 12) & 1u) wn |= 1ull << (SL<S>::VG + (int)j);
+        d.w_new = wn;
+        return;
+    }
+    if (mt == AEQ) {  // HandleAppendEntriesRequest :347-356 (mterm <= ct here)
+        const u32 pidx = (msg >> 12) & 3u, pterm = (msg >> 14) & 15u;
+        const u32 nent = (msg >> 18) & 1u, ent = (msg >> 19) & 31u, mci = (msg >> 24) & 3u;
+        const bool log_ok = pidx == 0 || (pidx <= len && pterm == ent_term(w_ent(wi, pidx - 1)));
+        if (mterm < ct || (st == FOLLOWER && !log_ok)) {  // Reject :281-293
+            d.add = m_hdr(AEP, i, j, ct);  // msuccess FALSE, mmatchIndex 0
+            d.has_add = 1;
+            d.rm = k;
+            d.en = 1;
+            return;
+        }
+        if (st == CANDIDATE) {  // ReturnToFollowerState :295-299 — m stays
+            d.w_new = setbits(wi, ST_SH, 2, FOLLOWER);
+            d.en = 1;
+            return;
+        }
+        if (st != FOLLOWER) return;  // Leader with an equal-term request: no branch
+        const u32 index = pidx + 1;
+        const bool term_eq = len >= index && ent_term(w_ent(wi, index - 1)) == ent_term(ent);
+        if (nent == 0 || term_eq) {
+            // AppendEntriesAlreadyDone :301-317; UNCHANGED logVars after
+            // commitIndex' = [.. EXCEPT ![i] = m.mcommitIndex] is a TLC
+            // equality test: enabled only when mcommitIndex = commitIndex[i].
+            if (mci != w_ci(wi)) return;
+            d.add = m_hdr(AEP, i, j, ct) | (1u << 12) | ((pidx + nent) << 13);
+            d.has_add = 1;
+            d.rm = k;
+            d.en = 1;
+            return;
+        }
+        if (len >= index) {  // ConflictAppendEntriesRequest :319-325 — drop LAST entry, m stays
+            u64 wn = setbits(wi, LOG_SH + ENT_W * (int)(len - 1), ENT_W, 0);
+            d.w_new = setbits(wn, LEN_SH, 2, len - 1);
+            d.en = 1;
+            return;
+        }
+        if (len == pidx) {  // NoConflictAppendEntriesRequest :327-331 — m stays
+            if (len >= (u32)LOG_CAP) {  // Len = 4 > every allowed bound: out of constraint
+                d.w_new = setbits(wi, LEN_SH, 2, 3) | (1ull << 63);  // bit 63 marks overflow
+            } else {
+                u64 wn = setbits(wi, LOG_SH + ENT_W * (int)len, ENT_W, ent);
+                d.w_new = setbits(wn, LEN_SH, 2, len + 1);
+            }
+            d.en = 1;
+        }
+        return;
+    }
+    // AEP
+    d.rm = k;
+    d.en = 1;
+    if (mterm < ct) return;  // DropStaleResponse
+    // HandleAppendEntriesResponse :360-370 (no Leader guard)
+    if ((msg >> 12) & 1u) {
+        const u32 mm = (msg >> 13) & 3u;
+        u64 wn = setbits(wi, SL<S>::NI + 2 * (int)j, 2, mm);  // nextIndex = mm + 1 (stored -1)
+        d.w_new = setbits(wn, SL<S>::MI + 2 * (int)j, 2, mm);
+    } else {
+        const u32 nis = bits(wi, SL<S>::NI + 2 * (int)j, 2);  // nextIndex - 1
+        d.w_new = setbits(wi, SL<S>::NI + 2 * (int)j, 2, nis ? nis - 1 : 0);  // Max({ni-1, 1})
+    }
+}
+
+// Compute the delta of lane `lane` (0 <= lane < P.off[10]) on parent (w, m).
+template <int S, int K>
+RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Params& P, Delta& d) {
+    d.srv = -1;
+    d.rm = -1;
+    d.has_add = 0;
+    d.add = 0;
+    d.en = 0;
+    d.w_new = 0;
+    if (lane < P.off[1]) {  // Restart(i) :136-143
+        const int i = lane;
+        d.srv = i;
+        d.w_new = selw<S>(w, i) & RESTART_KEEP;
+        d.en = 1;
+    } else if (lane < P.off[2]) {  // Timeout(i) :146-154
+        const int i = lane - P.off[1];
+        const u64 wi = selw<S>(w, i);
+        const u32 st = w_st(wi);
+        if (st == FOLLOWER || st == CANDIDATE) {
+            const u32 ct1 = w_ct(wi) + 1;
+            u64 wn = setbits(wi, ST_SH, 2, CANDIDATE);
+            wn = setbits(wn, VF_SH, 3, NILV);
+            wn &= ~(((u64)SL<S>::SMASK << SL<S>::VR) | ((u64)SL<S>::SMASK << SL<S>::VG));
+            wn = setbits(wn, CT_SH, 4, ct1 & 15u) | ((u64)(ct1 >> 4) << 63);  // bit 63: term overflow
+            d.srv = i;
+            d.w_new = wn;
+            d.en = 1;
+        }
+    } else if (lane < P.off[3]) {  // RequestVote(i, j) :157-166 (no i /= j guard)
+        const int t = lane - P.off[2], i = t / S, j = t % S;
+        const u64 wi = selw<S>(w, i);
+        if (w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u)) {
+            d.add = m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16);
+            d.has_add = 1;
+            d.en = 1;
+        }
+    } else if (lane < P.off[4]) {  // BecomeLeader(i) :195-203
+        const int i = lane - P.off[3];
+        const u64 wi = selw<S>(w, i);
+        const u32 vg = w_vg<S>(wi);
+        const bool ok = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
+        if (w_st(wi) == CANDIDATE && ok) {
+            u64 wn = setbits(wi, ST_SH, 2, LEADER);
+            const u64 lenv = w_len(wi);  // nextIndex = Len + 1, stored minus one
+            u64 ni = 0;
+#pragma unroll
+            for (int q = 0; q < S; ++q) ni |= lenv << (2 * q);
+            wn = setbits(wn, SL<S>::NI, 2 * S, ni);
+            wn = setbits(wn, SL<S>::MI, 2 * S, 0);
+            d.srv = i;
+            d.w_new = wn;
+            d.en = 1;
+        }
+    } else if (lane < P.off[5]) {  // ClientRequest(i, v) :206-213
+        const int t = lane - P.off[4], i = t / P.V, v = t % P.V;
+        const u64 wi = selw<S>(w, i);
+        if (w_st(wi) == LEADER) {
+            const u32 len = w_len(wi);
+            if (len >= (u32)LOG_CAP) {
+                d.w_new = wi | (1ull << 63);  // Len = 4: out of every allowed constraint
+            } else {
+                u64 wn = setbits(wi, LOG_SH + ENT_W * (int)len, ENT_W, w_ct(wi) | ((u32)v << 4));
+                d.w_new = setbits(wn, LEN_SH, 2, len + 1);
+            }
+            d.srv = i;
+            d.en = 1;
+        }
+    } else if (lane < P.off[6]) {  // AdvanceCommitIndex(i) :219-236
+        const int i = lane - P.off[5];
+        const u64 wi = selw<S>(w, i);
+        if (w_st(wi) == LEADER) {
+            const u32 len = w_len(wi);
+            u32 best = 0;
+            for (u32 idx = 1; idx <= len; ++idx) {
+                u32 agree = 1u << i;
+#pragma unroll
+                for (int q = 0; q < S; ++q) agree |= (w_mi<S>(wi, q) >= idx ? 1u : 0u) << q;
+                if (2 * __builtin_popcount(agree) > S) best = idx;  // Max(agreeIndexes)
+            }
+            u64 wn = wi;
+            if (best > 0 && ent_term(w_ent(wi, best - 1)) == w_ct(wi)) wn = setbits(wi, CI_SH, 2, best);
+            d.srv = i;
+            d.w_new = wn;
+            d.en = 1;
+        }
+    } else if (lane < P.off[7]) {  // AppendEntries(i, j) :171-192
+        const int t = lane - P.off[6], i = t / S, j = t % S;
+        const u64 wi = selw<S>(w, i);
+        if (i != j && w_st(wi) == LEADER) {
+            const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
+            const u32 prev = ni - 1;
+            const u32 pterm = (prev > 0 && prev <= len) ? ent_term(w_ent(wi, prev - 1)) : 0u;
+            const u32 last = len < ni ? len : ni;  // Min({Len(log[i]), nextIndex[i][j]})
+            const u32 nent = ni <= last ? 1u : 0u; // SubSeq(log[i], ni, last): 0 or 1 entry
+            const u32 ent = nent ? w_ent(wi, ni - 1) : 0u;
+            const u32 ci = w_ci(wi), mci = ci < last ? ci : last;
+            d.add = m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | (prev << 12) | (pterm << 14) | (nent << 18) |
+                    (ent << 19) | (mci << 24);
+            d.has_add = 1;
+            d.en = 1;
+        }
+    } else if (lane < P.off[8]) {  // Receive(m) :388-403
+        const int k = lane - P.off[7];
+        const u32 sl = selm<K>(m, k);
+        if (sl) receive_lane<S, K>(w, sl & MSG_MASK, k, d);
+    } else if (lane < P.off[9]) {  // DuplicateMessage(m) :410-412
+        const int k = lane - P.off[8];
+        const u32 sl = selm<K>(m, k);
+        if (sl) {
+            d.add = sl & MSG_MASK;
+            d.has_add = 1;
+            d.en = 1;
+        }
+    } else {  // DropMessage(m) :415-417
+        const int k = lane - P.off[9];
+        const u32 sl = selm<K>(m, k);
+        if (sl) {
+            d.rm = k;
+            d.en = 1;
+        }
+    }
+}
+
+// Apply a delta: fingerprint and CONSTRAINT (parent assumed in-constraint).
+// Returns 1 if the successor is in the model; *h receives its fingerprint.
+template <int S, int K>
+RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d, const Params& P,
+                    u64* h) {
+    u64 hh = h0;
+    int nmsg = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
+    if (d.srv >= 0) {
+        const u64 wo = selw<S>(w, d.srv);
+        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
+        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
+        if (d.w_new != wo) hh += hS(d.w_new, (u32)d.srv) - hS(wo, (u32)d.srv);
+    }
+    if (d.rm >= 0) {
+        const u32 sl = selm<K>(m, d.rm);
+        hh -= hM(sl);
+        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
+        else nmsg -= 1;
+    }
+    if (d.has_add) {
+        int found = -1;
+#pragma unroll
+        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+        if (found >= 0) {
+            const u32 sl = selm<K>(m, found);
+            if ((int)m_cnt(sl) + 1 > P.max_dup) return 0;
+            hh += hM(sl + CNT_ONE) - hM(sl);
+        } else {
+            if (1 > P.max_dup) return 0;
+            nmsg += 1;
+            hh += hM(d.add | CNT_ONE);
+        }
+    }
+    if (nmsg > P.max_msgs) return 0;
+    *h = hh;
+    return 1;
+}
+
+template <int S, int K>
+RMC_HD u64 state_fp(const u64 (&w)[S], const u32 (&m)[K]) {
+    u64 h = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) h += hS(w[i], (u32)i);
+#pragma unroll
+    for (int q = 0; q < K; ++q) h += hM(m[q]);
+    return h;
+}
+
+// Materialise a successor (only called for in-model successors) and put the
+// bag in canonical order (descending, empty slots last).
+template <int S, int K>
+RMC_HD void materialise(const u64 (&w)[S], const u32 (&m)[K], const Delta& d, u64 (&wo)[S], u32 (&mo)[K]) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) wo[i] = (d.srv == i) ? d.w_new : w[i];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        u32 sl = m[q];
+        if (q == d.rm) sl = m_cnt(sl) > 1 ? sl - CNT_ONE : 0u;
+        mo[q] = sl;
+    }
+    if (d.has_add) {
+        int found = -1, hole = -1;
+#pragma unroll
+        for (int q = K - 1; q >= 0; --q) {
+            found = (mo[q] && (mo[q] & MSG_MASK) == d.add) ? q : found;
+            hole = mo[q] == 0 ? q : hole;
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            if (q == found) mo[q] += CNT_ONE;
+            else if (found < 0 && q == hole) mo[q] = d.add | CNT_ONE;
+        }
+    }
+    // odd-even transposition sort, descending (K passes)
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+#pragma unroll
+        for (int q = (p & 1); q + 1 < K; q += 2) {
+            const u32 a = mo[q], b = mo[q + 1];
+            mo[q] = a > b ? a : b;
+            mo[q + 1] = a > b ? b : a;
+        }
+    }
+}
+
+// ---- invariants (fused into the insert of a new state) -----------------------------
+template <int S, int K>
+RMC_HD int type_ok(const u64 (&w)[S], const u32 (&m)[K], int V) {  // raft.tla:482-492
+    for (int i = 0; i < S; ++i) {
+        const u64 wi = w[i];
+        if (w_st(wi) > LEADER) return 0;
+        const u32 vf = w_vf(wi);
+        if (vf != NILV && vf >= (u32)S) return 0;
+        for (u32 x = 0; x < w_len(wi); ++x)
+            if ((w_ent(wi, x) >> 4) >= (u32)V) return 0;
+        // nextIndex >= 1 holds by construction (stored minus one)
+    }
+    for (int q = 0; q < K; ++q) {
+        const u32 sl = m[q];
+        if (!sl) continue;
+        if (m_src(sl) >= (u32)S || m_dst(sl) >= (u32)S) return 0;
+    }
+    return 1;
+}
+template <int S>
+RMC_HD int one_leader_per_term(const u64 (&w)[S]) {
+    for (int i = 0; i < S; ++i)
+        for (int j = i + 1; j < S; ++j)
+            if (w_st(w[i]) == LEADER && w_st(w[j]) == LEADER && w_ct(w[i]) == w_ct(w[j])) return 0;
+    return 1;
+}
+template <int S>
+RMC_HD int log_matching(const u64 (&w)[S]) {  // raft.tla:1132-1136
+    for (int i = 0; i < S; ++i)
+        for (int j = i + 1; j < S; ++j) {
+            const u32 li = w_len(w[i]), lj = w_len(w[j]);
+            const u32 n = li < lj ? li : lj;
+            for (u32 x = 1; x <= n; ++x) {
+                if (ent_term(w_ent(w[i], x - 1)) != ent_term(w_ent(w[j], x - 1))) continue;
+                const u64 pm = (1ull << (ENT_W * x)) - 1;
+                if (((w[i] >> LOG_SH) & pm) != ((w[j] >> LOG_SH) & pm)) return 0;
+            }
+        }
+    return 1;
+}
+// 0 = all hold, else 1 + index of the first violated invariant bit.
+template <int S, int K>
+RMC_HD int check_invariants(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
+    if ((P.inv_mask & 1) && !type_ok<S, K>(w, m, P.V)) return 1;
+    if ((P.inv_mask & 2) && !one_leader_per_term<S>(w)) return 2;
+    if ((P.inv_mask & 4) && !log_matching<S>(w)) return 3;
+    return 0;
+}
+
+// ---- symmetry: server permutations -----------------------------------------------
+// perm p maps old server id -> new id.  A permuted word moves to position p[i].
+template <int S>
+RMC_HD u64 perm_word(u64 w, const int* p) {
+    u64 r = w & (0x3Full | (0x3ull << CI_SH) | (0x1FFFFull << LEN_SH));  // ct, st, ci, log
+    const u32 vf = w_vf(w);
+    r |= (u64)(vf == NILV ? NILV : (u32)p[vf]) << VF_SH;
+    for (int j = 0; j < S; ++j) {
+        const int pj = p[j];
+        r |= ((w >> (SL<S>::VR + j)) & 1ull) << (SL<S>::VR + pj);
+        r |= ((w >> (SL<S>::VG + j)) & 1ull) << (SL<S>::VG + pj);
+        r |= ((w >> (SL<S>::NI + 2 * j)) & 3ull) << (SL<S>::NI + 2 * pj);
+        r |= ((w >> (SL<S>::MI + 2 * j)) & 3ull) << (SL<S>::MI + 2 * pj);
+    }
+    return r;
+}
+RMC_HD u32 perm_slot(u32 sl, const int* p) {
+    if (!sl) return 0;
+    const u32 src = m_src(sl), dst = m_dst(sl);
+    return (sl & ~(0xFCu)) | ((u32)p[src] << 2) | ((u32)p[dst] << 5);
+}
+
+}  // namespace rmc

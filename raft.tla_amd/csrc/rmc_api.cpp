@@ -1,0 +1,573 @@
+// rmc_api.cpp — the C ABI of librmc.so (include/rmc.h): context, BFS driver,
+// codec, traces, and the differential-test entry point.
+//
+// Host side of the hot path: one HIP stream per context, one kernel launch
+// (plus one 40-byte counter read-back) per BFS level.  The level loop
+// replaces TLC's ModelChecker.runTLC / Worker loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rmc.h"
+#include "raft_packed.h"
+#include "rmc_internal.h"
+
+using namespace rmc;
+
+struct rmc_ctx {
+    rmc_config cfg{};
+    Shape sh{};
+    Params P{};
+    PermTable PT{};
+    int NW = 0;  // 32-bit words per packed state
+    hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // bracket each level's expansion launches
+    DevBufs B{};
+    Counters* h_ctr = nullptr;  // pinned
+    u32* d_staged = nullptr;
+    u64 table_slots = 0;
+    rmc_result res{};
+    std::string err;
+    std::vector<u64> level_start;  // level d (1-based) = [level_start[d-1], level_start[d])
+    int have_target = 0;           // a violation / deadlock state to trace
+    u64 target_idx = 0;
+};
+
+namespace {
+
+const char* kVersion = "rmc 1 (raft.tla BFS, gfx950 HIP, packed-delta lanes, HBM fp set)";
+
+int fail(rmc_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                              \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            return fail((c), e_ == hipErrorOutOfMemory ? RMC_E_NOMEM : RMC_E_HIP,                    \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                          \
+    } while (0)
+
+int kcap_for(int max_msgs) { return max_msgs <= 4 ? 4 : 8; }
+
+int validate(const rmc_config* c, std::string* why) {
+    auto bad = [&](const char* s) { *why = s; return RMC_E_INVAL; };
+    if (c->n_servers < 2 || c->n_servers > RMC_MAX_SERVERS) return bad("n_servers must be 2..5");
+    if (c->n_values < 1 || c->n_values > RMC_MAX_VALUES) return bad("n_values must be 1..2");
+    if (c->max_term < 1 || c->max_term > RMC_MAX_TERM) return bad("max_term must be 1..14");
+    if (c->max_log_len < 0 || c->max_log_len > RMC_MAX_LOG) return bad("max_log_len must be 0..3");
+    if (c->max_msgs < 0 || c->max_msgs > RMC_MAX_MSGS) return bad("max_msgs must be 0..8");
+    if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
+    if ((c->flags & RMC_FLAG_SYMMETRY) && c->n_servers > 4)
+        return bad("SYMMETRY is supported for up to 4 servers");
+    if (c->invariants & ~7u) return bad("unknown invariant bit");
+    return 0;
+}
+
+void fill_params(rmc_ctx* c) {
+    const rmc_config& g = c->cfg;
+    c->sh.S = g.n_servers;
+    c->sh.K = kcap_for(g.max_msgs);
+    c->sh.sym = (g.flags & RMC_FLAG_SYMMETRY) != 0;
+    c->NW = 2 * c->sh.S + c->sh.K;
+    Params& P = c->P;
+    P.V = g.n_values;
+    P.max_term = g.max_term;
+    P.max_log = g.max_log_len;
+    P.max_msgs = g.max_msgs;
+    P.max_dup = g.max_dup;
+    P.bug_quorum = (g.flags & RMC_FLAG_BUG_QUORUM) ? 1 : 0;
+    P.inv_mask = (int)g.invariants;
+    P.symmetry = c->sh.sym ? 1 : 0;
+    const int S = c->sh.S, K = c->sh.K;
+    const int sizes[10] = {S, S, S * S, S, S * P.V, S, S * S, K, K, K};
+    P.off[0] = 0;
+    for (int f = 0; f < 10; ++f) P.off[f + 1] = P.off[f] + sizes[f];
+    // permutations of 0..S-1 in lexicographic order (identity first)
+    memset(&c->PT, 0, sizeof c->PT);
+    if (S <= 4) {
+        int a[4] = {0, 1, 2, 3};
+        int n = 0;
+        do {
+            for (int i = 0; i < 4; ++i) c->PT.p[n][i] = (int8_t)a[i];
+            ++n;
+        } while (std::next_permutation(a, a + S));
+    }
+}
+
+int family_of(const Params& P, int lane) {
+    if (lane == 255) return -1;
+    for (int f = 0; f < 10; ++f)
+        if (lane < P.off[f + 1]) return f;
+    return -1;
+}
+
+// ---- codec ----------------------------------------------------------------------
+int encode_view(const rmc_ctx* c, const rmc_state_view& v, u32* out, std::string* why) {
+    const int S = c->sh.S, K = c->sh.K;
+    const int VR = VR_SH, VG = VR_SH + S, NI = VR_SH + 2 * S, MI = VR_SH + 4 * S;
+    auto bad = [&](const std::string& s) { *why = s; return RMC_E_INVAL; };
+    if (v.n_servers != S) return bad("view n_servers differs from config");
+    if (v.n_msgs < 0 || v.n_msgs > K) return bad("too many messages for the packed bag");
+    for (int i = 0; i < S; ++i) {
+        const int len = v.log_len[i];
+        if (v.currentTerm[i] < 0 || v.currentTerm[i] > 15) return bad("currentTerm out of packed range");
+        if (v.state[i] < 0 || v.state[i] > 2) return bad("state out of range");
+        if (v.votedFor[i] < -1 || v.votedFor[i] >= S) return bad("votedFor out of range");
+        if (v.commitIndex[i] < 0 || v.commitIndex[i] > 3) return bad("commitIndex out of packed range");
+        if (len < 0 || len > LOG_CAP) return bad("log length out of packed range");
+        u64 w = (u64)v.currentTerm[i] | ((u64)v.state[i] << ST_SH) |
+                ((u64)(v.votedFor[i] < 0 ? NILV : (u32)v.votedFor[i]) << VF_SH) | ((u64)v.commitIndex[i] << CI_SH) |
+                ((u64)len << LEN_SH);
+        for (int x = 0; x < len; ++x) {
+            const rmc_entry e = v.log[i][x];
+            if (e.term < 0 || e.term > 15 || e.value < 0 || e.value > 1) return bad("log entry out of range");
+            w |= (u64)(e.term | (e.value << 4)) << (LOG_SH + ENT_W * x);
+        }
+        if ((v.votesResponded[i] | v.votesGranted[i]) >> S) return bad("vote set out of range");
+        w |= (u64)v.votesResponded[i] << VR;
+        w |= (u64)v.votesGranted[i] << VG;
+        for (int j = 0; j < S; ++j) {
+            if (v.nextIndex[i][j] < 1 || v.nextIndex[i][j] > 4) return bad("nextIndex out of packed range");
+            if (v.matchIndex[i][j] < 0 || v.matchIndex[i][j] > 3) return bad("matchIndex out of packed range");
+            w |= (u64)(v.nextIndex[i][j] - 1) << (NI + 2 * j);
+            w |= (u64)v.matchIndex[i][j] << (MI + 2 * j);
+        }
+        out[2 * i] = (u32)w;
+        out[2 * i + 1] = (u32)(w >> 32);
+    }
+    std::vector<u32> slots;
+    for (int q = 0; q < v.n_msgs; ++q) {
+        const rmc_msg_view& m = v.msgs[q];
+        if (m.mtype < 0 || m.mtype > 3) return bad("mtype out of range");
+        if (m.msource < 0 || m.msource >= S || m.mdest < 0 || m.mdest >= S) return bad("message endpoint out of range");
+        if (m.mterm < 0 || m.mterm > 15) return bad("mterm out of packed range");
+        if (m.count < 1 || m.count > 3) return bad("message count out of packed range");
+        u32 s = m_hdr((u32)m.mtype, (u32)m.msource, (u32)m.mdest, (u32)m.mterm);
+        switch (m.mtype) {
+            case RVQ:
+                if (m.mlastLogTerm < 0 || m.mlastLogTerm > 15 || m.mlastLogIndex < 0 || m.mlastLogIndex > 3)
+                    return bad("RequestVoteRequest field out of packed range");
+                s |= ((u32)m.mlastLogTerm << 12) | ((u32)m.mlastLogIndex << 16);
+                break;
+            case RVP: {
+                if (m.mlog_len < 0 || m.mlog_len > 3) return bad("mlog too long");
+                u32 lg = (u32)m.mlog_len;
+                for (int x = 0; x < m.mlog_len; ++x) {
+                    if (m.mlog[x].term < 0 || m.mlog[x].term > 15 || m.mlog[x].value < 0 || m.mlog[x].value > 1)
+                        return bad("mlog entry out of range");
+                    lg |= (u32)(m.mlog[x].term | (m.mlog[x].value << 4)) << (2 + ENT_W * x);
+                }
+                s |= ((u32)(m.mvoteGranted != 0) << 12) | (lg << 13);
+                break;
+            }
+            case AEQ: {
+                if (m.mprevLogIndex < 0 || m.mprevLogIndex > 3 || m.mprevLogTerm < 0 || m.mprevLogTerm > 15 ||
+                    m.mentries_len < 0 || m.mentries_len > 1 || m.mcommitIndex < 0 || m.mcommitIndex > 3)
+                    return bad("AppendEntriesRequest field out of packed range");
+                u32 e = 0;
+                if (m.mentries_len) {
+                    if (m.mentries[0].term < 0 || m.mentries[0].term > 15 || m.mentries[0].value < 0 ||
+                        m.mentries[0].value > 1)
+                        return bad("mentries entry out of range");
+                    e = (u32)(m.mentries[0].term | (m.mentries[0].value << 4));
+                }
+                s |= ((u32)m.mprevLogIndex << 12) | ((u32)m.mprevLogTerm << 14) | ((u32)m.mentries_len << 18) |
+                     (e << 19) | ((u32)m.mcommitIndex << 24);
+                break;
+            }
+            default:
+                if (m.mmatchIndex < 0 || m.mmatchIndex > 3) return bad("mmatchIndex out of packed range");
+                s |= ((u32)(m.msuccess != 0) << 12) | ((u32)m.mmatchIndex << 13);
+        }
+        for (u32 o : slots)
+            if ((o & MSG_MASK) == s) return bad("duplicate message in bag view");
+        slots.push_back(s | ((u32)m.count << 30));
+    }
+    std::sort(slots.begin(), slots.end(), [](u32 a, u32 b) { return a > b; });
+    for (int q = 0; q < K; ++q) out[2 * S + q] = q < (int)slots.size() ? slots[q] : 0u;
+    return 0;
+}
+
+void decode_state(const rmc_ctx* c, const u32* in, rmc_state_view* v) {
+    const int S = c->sh.S, K = c->sh.K;
+    const int VR = VR_SH, VG = VR_SH + S, NI = VR_SH + 2 * S, MI = VR_SH + 4 * S;
+    memset(v, 0, sizeof *v);
+    v->n_servers = S;
+    for (int i = 0; i < S; ++i) {
+        const u64 w = (u64)in[2 * i] | ((u64)in[2 * i + 1] << 32);
+        v->currentTerm[i] = (int)w_ct(w);
+        v->state[i] = (int)w_st(w);
+        v->votedFor[i] = w_vf(w) == NILV ? -1 : (int)w_vf(w);
+        v->commitIndex[i] = (int)w_ci(w);
+        v->log_len[i] = (int)w_len(w);
+        for (u32 x = 0; x < w_len(w); ++x) {
+            v->log[i][x].term = (int)(w_ent(w, x) & 15u);
+            v->log[i][x].value = (int)(w_ent(w, x) >> 4);
+        }
+        v->votesResponded[i] = bits(w, VR, S);
+        v->votesGranted[i] = bits(w, VG, S);
+        for (int j = 0; j < S; ++j) {
+            v->nextIndex[i][j] = (int)bits(w, NI + 2 * j, 2) + 1;
+            v->matchIndex[i][j] = (int)bits(w, MI + 2 * j, 2);
+        }
+    }
+    int n = 0;
+    for (int q = 0; q < K; ++q) {
+        const u32 s = in[2 * S + q];
+        if (!s) continue;
+        rmc_msg_view& m = v->msgs[n++];
+        m.mtype = (int)m_type(s);
+        m.msource = (int)m_src(s);
+        m.mdest = (int)m_dst(s);
+        m.mterm = (int)m_term(s);
+        m.count = (int)m_cnt(s);
+        switch (m.mtype) {
+            case RVQ:
+                m.mlastLogTerm = (int)((s >> 12) & 15u);
+                m.mlastLogIndex = (int)((s >> 16) & 3u);
+                break;
+            case RVP: {
+                m.mvoteGranted = (int)((s >> 12) & 1u);
+                const u32 lg = (s >> 13) & 0x1FFFFu;
+                m.mlog_len = (int)(lg & 3u);
+                for (int x = 0; x < m.mlog_len; ++x) {
+                    const u32 e = (lg >> (2 + ENT_W * x)) & 31u;
+                    m.mlog[x].term = (int)(e & 15u);
+                    m.mlog[x].value = (int)(e >> 4);
+                }
+                break;
+            }
+            case AEQ: {
+                m.mprevLogIndex = (int)((s >> 12) & 3u);
+                m.mprevLogTerm = (int)((s >> 14) & 15u);
+                m.mentries_len = (int)((s >> 18) & 1u);
+                const u32 e = (s >> 19) & 31u;
+                if (m.mentries_len) {
+                    m.mentries[0].term = (int)(e & 15u);
+                    m.mentries[0].value = (int)(e >> 4);
+                }
+                m.mcommitIndex = (int)((s >> 24) & 3u);
+                break;
+            }
+            default:
+                m.msuccess = (int)((s >> 12) & 1u);
+                m.mmatchIndex = (int)((s >> 13) & 3u);
+        }
+    }
+    v->n_msgs = n;
+}
+
+void init_view(const rmc_config& g, rmc_state_view* v) {  // Init raft.tla:113-129
+    memset(v, 0, sizeof *v);
+    v->n_servers = g.n_servers;
+    for (int i = 0; i < g.n_servers; ++i) {
+        v->currentTerm[i] = 1;
+        v->state[i] = 0;
+        v->votedFor[i] = -1;
+        for (int j = 0; j < g.n_servers; ++j) v->nextIndex[i][j] = 1;
+    }
+}
+
+int reset_counters(rmc_ctx* c, bool keep_count) {
+    Counters h{};
+    h.count = keep_count ? c->h_ctr->count : 0;
+    h.viol = ~0ull;
+    h.deadlock = ~0ull;
+    *c->h_ctr = h;
+    HIPCHK(c, hipMemcpyAsync(c->B.ctr, c->h_ctr, sizeof(Counters), hipMemcpyHostToDevice, c->st));
+    return 0;
+}
+
+int read_counters(rmc_ctx* c) {
+    HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->B.ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rmc_version(void) { return kVersion; }
+
+const char* rmc_last_error(const rmc_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+size_t rmc_state_bytes(const rmc_config* cfg) {
+    if (!cfg) return 0;
+    return (size_t)(2 * cfg->n_servers + kcap_for(cfg->max_msgs)) * 4u;
+}
+
+int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
+    if (!cfg || !out) return RMC_E_INVAL;
+    *out = nullptr;
+    std::string why;
+    if (int rc = validate(cfg, &why)) {
+        fprintf(stderr, "rmc_create: %s\n", why.c_str());
+        return rc;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
+        fprintf(stderr, "rmc_create: no HIP device %d\n", cfg->device);
+        return RMC_E_NOGPU;
+    }
+    rmc_ctx* c = new rmc_ctx();
+    c->cfg = *cfg;
+    fill_params(c);
+    auto bail = [&](int rc) {
+        fprintf(stderr, "rmc_create: %s\n", c->err.c_str());
+        rmc_destroy(c);
+        return rc;
+    };
+    if (hipSetDevice(cfg->device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(RMC_E_NOGPU); }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) { c->err = "hipGetDeviceProperties failed"; return bail(RMC_E_NOGPU); }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        c->err = std::string("device is ") + prop.gcnArchName + ", librmc is built for gfx950 only";
+        return bail(RMC_E_NOGPU);
+    }
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        c->err = "stream/event creation failed";
+        return bail(RMC_E_HIP);
+    }
+
+    // ---- capacity: state store + parents + lanes + fingerprint set (load <= 0.5)
+    const u64 per_state = (u64)c->NW * 4 + 8 + 1;
+    u64 cap = cfg->state_capacity;
+    if (cap == 0) {
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        const u64 budget = (u64)((double)fr * 0.80);
+        cap = budget / (per_state + 32);  // table <= 4 slots per state after pow2 rounding
+        cap = std::min<u64>(cap, 1ull << 31);
+    }
+    cap = std::max<u64>(cap, 1024);
+    u64 slots = 1;
+    while (slots < 2 * cap) slots <<= 1;
+    c->table_slots = slots;
+    c->B.cap = cap;
+    c->B.tmask = slots - 1;
+    if (hipMalloc(&c->B.store, cap * (u64)c->NW * 4) != hipSuccess ||
+        hipMalloc(&c->B.parent, cap * 8) != hipSuccess || hipMalloc(&c->B.act, cap) != hipSuccess ||
+        hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
+        hipMalloc(&c->d_staged, (size_t)c->NW * 4 * 64) != hipSuccess) {
+        c->err = "device allocation failed (capacity " + std::to_string(cap) + " states)";
+        return bail(RMC_E_NOMEM);
+    }
+    if (hipHostMalloc(&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+        c->err = "pinned allocation failed";
+        return bail(RMC_E_NOMEM);
+    }
+    memset(c->h_ctr, 0, sizeof(Counters));
+    *out = c;
+    return 0;
+}
+
+void rmc_destroy(rmc_ctx* c) {
+    if (!c) return;
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    (void)hipFree(c->B.store);
+    (void)hipFree(c->B.parent);
+    (void)hipFree(c->B.act);
+    (void)hipFree(c->B.table);
+    (void)hipFree(c->B.ctr);
+    (void)hipFree(c->d_staged);
+    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+}
+
+int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
+    if (!c) return RMC_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    c->res = rmc_result{};
+    c->level_start.clear();
+    c->have_target = 0;
+    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    if (int rc = reset_counters(c, false)) return rc;
+
+    // ---- Init (raft.tla:125-129): one initial state
+    rmc_state_view iv;
+    init_view(c->cfg, &iv);
+    std::vector<u32> packed((size_t)c->NW);
+    std::string why;
+    if (encode_view(c, iv, packed.data(), &why)) return fail(c, RMC_E_INVAL, why);
+    HIPCHK(c, hipMemcpyAsync(c->d_staged, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
+    if (int rc = read_counters(c)) return rc;
+    c->res.generated = 1;
+    c->level_start.push_back(0);
+    c->level_start.push_back(c->h_ctr->count);
+    int depth = c->h_ctr->count ? 1 : 0;
+    if (c->h_ctr->viol != ~0ull) {
+        c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 3);
+        c->res.violation_depth = 1;
+        c->have_target = 1;
+        c->target_idx = c->h_ctr->viol >> 2;
+    }
+    const u64 CHUNK = 1ull << 26;
+    while (!c->have_target) {
+        const u64 lo = c->level_start[depth - 1], hi = c->level_start[depth];
+        if (lo == hi) break;  // fixpoint
+        if (c->cfg.max_depth > 0 && depth >= c->cfg.max_depth) {
+            c->res.left_on_queue = hi - lo;
+            break;
+        }
+        if (int rc = reset_counters(c, true)) return rc;
+        HIPCHK(c, hipEventRecord(c->ev0, c->st));
+        for (u64 a = lo; a < hi; a += CHUNK) {
+            const u64 b = std::min(hi, a + CHUNK);
+            HIPCHK(c, launch(c->sh, 0, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
+        }
+        HIPCHK(c, hipEventRecord(c->ev1, c->st));
+        if (int rc = read_counters(c)) return rc;
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->res.expand_kernel_seconds += 1e-3 * ms;
+        c->res.expand_launches += 1;
+        const Counters& k = *c->h_ctr;
+        if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
+        if (k.overflow) {
+            return fail(c, RMC_E_CAPACITY, "state store full (capacity " + std::to_string(c->B.cap) +
+                                                " states); raise rmc_config.state_capacity");
+        }
+        c->res.generated += k.generated;
+        const u64 nnew = k.count - hi;
+        if (nnew) {
+            ++depth;
+            c->level_start.push_back(k.count);
+        }
+        c->res.distinct = k.count;
+        if (k.viol != ~0ull) {
+            c->res.violated_inv = 1 << (int)(k.viol & 3);
+            c->res.violation_depth = depth;
+            c->have_target = 1;
+            c->target_idx = k.viol >> 2;
+        } else if ((c->cfg.flags & RMC_FLAG_CHECK_DEADLOCK) && k.deadlock != ~0ull) {
+            c->res.deadlock = 1;
+            c->have_target = 1;
+            c->target_idx = k.deadlock;
+        }
+        if (cb) {
+            rmc_level_stats ls{};
+            ls.level = nnew ? depth - 1 : depth;
+            ls.generated = c->res.generated;
+            ls.distinct = k.count;
+            ls.new_states = nnew;
+            ls.seconds = secs();
+            if (cb(&ls, user)) {
+                c->res.left_on_queue = nnew;
+                break;
+            }
+        }
+        if (!nnew) break;
+    }
+    c->res.distinct = c->level_start.back();
+    c->res.depth = depth;
+    const double D = (double)c->res.distinct, G = (double)c->res.generated;
+    c->res.collision_probability = D * G / 18446744073709551616.0;
+    c->res.seconds = secs();
+    return 0;
+}
+
+int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
+    if (!c || !out) return RMC_E_INVAL;
+    *out = c->res;
+    return 0;
+}
+
+int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* instances, size_t cap, size_t* len) {
+    if (!c || !len) return RMC_E_INVAL;
+    if (!c->have_target) return fail(c, RMC_E_STATE, "no violation or deadlock to trace");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    std::vector<u64> chain;
+    u64 idx = c->target_idx;
+    for (;;) {
+        chain.push_back(idx);
+        u64 p = 0;
+        HIPCHK(c, hipMemcpy(&p, c->B.parent + idx, 8, hipMemcpyDeviceToHost));
+        if (p == ~0ull || chain.size() > 100000) break;
+        idx = p;
+    }
+    std::reverse(chain.begin(), chain.end());
+    *len = chain.size();
+    std::vector<u32> buf((size_t)c->NW);
+    for (size_t q = 0; q < chain.size() && q < cap; ++q) {
+        HIPCHK(c, hipMemcpy(buf.data(), c->B.store + chain[q] * (u64)c->NW, buf.size() * 4, hipMemcpyDeviceToHost));
+        uint8_t a = 0;
+        HIPCHK(c, hipMemcpy(&a, c->B.act + chain[q], 1, hipMemcpyDeviceToHost));
+        if (states) decode_state(c, buf.data(), &states[q]);
+        if (families) families[q] = family_of(c->P, a);
+        if (instances) instances[q] = a == 255 ? -1 : a;
+    }
+    return 0;
+}
+
+int rmc_expand(rmc_ctx* c, const rmc_state_view* states, size_t n, rmc_succ_view* out, size_t cap, size_t* n_out) {
+    if (!c || (!states && n) || !n_out) return RMC_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    *n_out = 0;
+    if (n == 0) return 0;
+    const int NW = c->NW, RW = 6 + NW;
+    std::vector<u32> packed(n * (size_t)NW);
+    std::string why;
+    for (size_t t = 0; t < n; ++t)
+        if (encode_view(c, states[t], packed.data() + t * NW, &why))
+            return fail(c, RMC_E_INVAL, "state " + std::to_string(t) + ": " + why);
+    const u64 lanes = (u64)c->P.off[10];
+    const u64 rcap = std::max<u64>(1, std::min<u64>((u64)cap, n * lanes));
+    u32 *d_in = nullptr, *d_out = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    HIPCHK(c, hipMalloc(&d_in, packed.size() * 4));
+    HIPCHK(c, hipMalloc(&d_out, rcap * (u64)RW * 4));
+    HIPCHK(c, hipMalloc(&d_cnt, 8));
+    HIPCHK(c, hipMemcpy(d_in, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(d_cnt, 0, 8));
+    HIPCHK(c, launch(c->sh, 2, c->P, c->PT, c->B, (u64)n, 0, d_in, d_out, rcap, d_cnt, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    unsigned long long cnt = 0;
+    HIPCHK(c, hipMemcpy(&cnt, d_cnt, 8, hipMemcpyDeviceToHost));
+    const u64 got = std::min<u64>(cnt, rcap);
+    std::vector<u32> recs(got * (u64)RW);
+    if (got) HIPCHK(c, hipMemcpy(recs.data(), d_out, recs.size() * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cnt);
+    // deterministic order: (parent, lane)
+    std::vector<u64> order(got);
+    for (u64 q = 0; q < got; ++q) order[q] = q;
+    std::sort(order.begin(), order.end(), [&](u64 a, u64 b) {
+        const u32* ra = &recs[a * RW];
+        const u32* rb = &recs[b * RW];
+        const u64 pa = (u64)ra[0] | ((u64)ra[1] << 32), pb = (u64)rb[0] | ((u64)rb[1] << 32);
+        return pa != pb ? pa < pb : ra[2] < rb[2];
+    });
+    for (u64 q = 0; q < got && q < cap; ++q) {
+        const u32* r = &recs[order[q] * RW];
+        rmc_succ_view& s = out[q];
+        memset(&s, 0, sizeof s);
+        s.parent = (u64)r[0] | ((u64)r[1] << 32);
+        s.instance = (int)r[2];
+        s.family = family_of(c->P, (int)r[2]);
+        s.in_constraint = (int)r[3];
+        s.fingerprint = (u64)r[4] | ((u64)r[5] << 32);
+        if (s.in_constraint) decode_state(c, r + 6, &s.state);
+    }
+    *n_out = (size_t)cnt;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,44 @@
+// rmc_internal.h — structures shared by the host engine and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "raft_packed.h"
+
+namespace rmc {
+
+// Device-side counters of one BFS level (zeroed/reset by the host per level).
+struct Counters {
+    u64 count;      // next free index of the state store (= distinct so far)
+    u64 generated;  // successors generated in this launch
+    u64 viol;       // min over violating new states of (index << 2 | invariant), ~0 = none
+    u64 deadlock;   // min index of a state with no enabled lane, ~0 = none
+    u32 overflow;   // state store full
+    u32 table_full; // fingerprint set full
+};
+
+struct DevBufs {
+    u32* store;      // packed states, (2S + K) words each; levels are contiguous ranges
+    u64* parent;     // parent index per state (~0 for initial states)
+    uint8_t* act;    // lane that produced the state (255 for initial states)
+    u64* table;      // fingerprint set, power-of-two slots, 0 = empty
+    u64 tmask;       // slots - 1
+    u64 cap;         // state store capacity
+    Counters* ctr;
+};
+
+struct PermTable {
+    int8_t p[24][4];  // server permutations (old id -> new id), S <= 4
+};
+
+struct Shape {
+    int S, K;
+    bool sym;
+};
+
+// which: 0 = k_expand over store[a, b); 1 = k_seed of `a` staged states `in`;
+//        2 = k_list of `a` states `in` into `out` (cap records, *count).
+hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
+                  const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
+
+}  // namespace rmc

@@ -1,0 +1,329 @@
+// rmc_kernels.hip — gfx950 kernels of the raft.tla BFS (DESIGN.md "Kernels").
+//
+//  k_expand : one lane per frontier state; loops over the state's action lanes
+//             (Next raft.tla:421-430) in wave-uniform order, computes each
+//             successor as a delta + incremental fingerprint, filters the
+//             CONSTRAINT and stuttering successors, probes/CAS-inserts the
+//             fingerprint into the HBM open-addressing set, and for the lanes
+//             that won: wave-aggregated slot allocation, materialise, store,
+//             parent pointer, fused invariant check.  Replaces TLC's worker
+//             loop body (getNextStates + FPSet.put + invariant check).
+//  k_seed   : inserts initial states (Init raft.tla:125-129) the same way.
+//  k_list   : the same lane code with every enabled successor written out
+//             (no dedup) — the differential-test entry point (rmc_expand).
+#include <hip/hip_runtime.h>
+
+#include "raft_packed.h"
+#include "rmc_internal.h"
+
+namespace rmc {
+
+__device__ __forceinline__ u64 bcast64(u64 v, int src) {
+    const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, src);
+    const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), src);
+    return ((u64)hi << 32) | lo;
+}
+
+// Open-addressing insert of a non-zero 64-bit fingerprint, linear probing.
+// Returns 1 if this lane inserted the key, 0 if it was present (or the table
+// is full, flagged in *full).  Plain probe loads may be stale only in the
+// EMPTY direction (slots go 0 -> key once); the CAS (agent scope, executed at
+// the memory side) settles every race.
+__device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 key, u32* full) {
+    u64 s = key & mask;
+    for (u64 n = 0; n <= mask; ++n) {
+        const u64 cur = table[s];
+        if (cur == key) return 0;
+        if (cur == 0) {
+            const u64 prev = atomicCAS((unsigned long long*)&table[s], 0ull, (unsigned long long)key);
+            if (prev == 0) return 1;
+            if (prev == key) return 0;
+        }
+        s = (s + 1) & mask;
+    }
+    atomicOr(full, 1u);
+    return 0;
+}
+
+template <int S, int K>
+__device__ __forceinline__ void load_state(const u32* __restrict__ base, u64 (&w)[S], u32 (&m)[K]) {
+    const u64* ws = reinterpret_cast<const u64*>(base);
+#pragma unroll
+    for (int i = 0; i < S; ++i) w[i] = ws[i];
+    if constexpr (K % 4 == 0) {
+        const uint4* ms = reinterpret_cast<const uint4*>(base + 2 * S);
+#pragma unroll
+        for (int q = 0; q < K / 4; ++q) {
+            const uint4 v = ms[q];
+            m[4 * q] = v.x; m[4 * q + 1] = v.y; m[4 * q + 2] = v.z; m[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < K; ++q) m[q] = base[2 * S + q];
+    }
+}
+
+template <int S, int K>
+__device__ __forceinline__ void store_state(u32* __restrict__ base, const u64 (&w)[S], const u32 (&m)[K]) {
+    u64* ws = reinterpret_cast<u64*>(base);
+#pragma unroll
+    for (int i = 0; i < S; ++i) ws[i] = w[i];
+#pragma unroll
+    for (int q = 0; q < K; ++q) base[2 * S + q] = m[q];
+}
+
+// Fingerprints of every server permutation of a full state.
+template <int S, int K, int NP>
+__device__ __forceinline__ void perm_fps(const u64 (&w)[S], const u32 (&m)[K], const PermTable& PT, u64 (&hp)[NP]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        int pm[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) pm[i] = PT.p[p][i];
+        u64 h = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) h += hS(perm_word<S>(w[i], pm), (u32)pm[i]);
+#pragma unroll
+        for (int q = 0; q < K; ++q) h += hM(perm_slot(m[q], pm));
+        hp[p] = h;
+    }
+}
+
+// Canonical key of a successor under SYMMETRY Permutations(Server): the least
+// permuted fingerprint, computed incrementally from the parent's per-permutation
+// fingerprints (the delta touches one server word and <= 2 bag slots).
+template <int S, int K, int NP>
+__device__ __forceinline__ u64 canon_key(const u64 (&w)[S], const u32 (&m)[K], const u64 (&hp)[NP],
+                                         const Delta& d, const PermTable& PT) {
+    u64 best = ~0ull;
+    const u64 wo = d.srv >= 0 ? selw<S>(w, d.srv) : 0ull;
+    u32 rm_old = 0, rm_new = 0, add_old = 0, add_new = 0;
+    if (d.rm >= 0) {
+        rm_old = selm<K>(m, d.rm);
+        rm_new = m_cnt(rm_old) > 1 ? rm_old - CNT_ONE : 0u;
+    }
+    if (d.has_add) {
+        int found = -1;
+#pragma unroll
+        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+        add_old = found >= 0 ? selm<K>(m, found) : 0u;
+        add_new = found >= 0 ? add_old + CNT_ONE : (d.add | CNT_ONE);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        int pm[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) pm[i] = PT.p[p][i];
+        u64 h = hp[p];
+        if (d.srv >= 0 && d.w_new != wo) {
+            int ps = pm[0];
+#pragma unroll
+            for (int i = 1; i < S; ++i) ps = (d.srv == i) ? pm[i] : ps;
+            h += hS(perm_word<S>(d.w_new, pm), (u32)ps) - hS(perm_word<S>(wo, pm), (u32)ps);
+        }
+        if (d.rm >= 0) h += hM(perm_slot(rm_new, pm)) - hM(perm_slot(rm_old, pm));
+        if (d.has_add) h += hM(perm_slot(add_new, pm)) - hM(perm_slot(add_old, pm));
+        best = h < best ? h : best;
+    }
+    return best;
+}
+
+template <int S> struct NPerm { static constexpr int v = S == 1 ? 1 : S == 2 ? 2 : S == 3 ? 6 : 24; };
+
+// Wave-aggregated allocation of store slots for the lanes with is_new set,
+// then materialise + store + parent + invariants.  Must be reached by every
+// lane of the wave (it contains a ballot).
+template <int S, int K>
+__device__ __forceinline__ void commit_new(int is_new, const u64 (&w)[S], const u32 (&m)[K], const Delta& d,
+                                           const Params& P, const DevBufs& B, u64 parent_idx, int lane) {
+    const u64 bal = __ballot(is_new);
+    if (bal == 0) return;
+    const int me = (int)__lane_id();
+    const int leader = __ffsll((long long)bal) - 1;
+    u64 base = 0;
+    if (me == leader) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)__popcll(bal));
+    base = bcast64(base, leader);
+    if (!is_new) return;
+    const u64 ni = base + (u64)__popcll(bal & ((1ull << me) - 1ull));
+    if (ni >= B.cap) {
+        atomicOr(&B.ctr->overflow, 1u);
+        return;
+    }
+    u64 wo[S];
+    u32 mo[K];
+    materialise<S, K>(w, m, d, wo, mo);
+    store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
+    B.parent[ni] = parent_idx;
+    B.act[ni] = (uint8_t)lane;
+    const int v = check_invariants<S, K>(wo, mo, P);
+    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
+}
+
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    constexpr int NW = 2 * S + K;
+    constexpr int NP = SYM ? NPerm<S>::v : 1;
+    const u64 idx = lo + (u64)blockIdx.x * 256ull + threadIdx.x;
+    const bool live = idx < hi;
+    u64 w[S];
+    u32 m[K];
+    if (live) {
+        load_state<S, K>(B.store + idx * (u64)NW, w, m);
+    } else {
+#pragma unroll
+        for (int i = 0; i < S; ++i) w[i] = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) m[q] = 0;
+    }
+    const u64 h0 = state_fp<S, K>(w, m);
+    u64 hp[NP];
+    if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
+    u32 gen = 0;
+    const int nl = P.off[10];
+    for (int lane = 0; lane < nl; ++lane) {  // wave-uniform loop
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        const int en = d.en && live;
+        gen += (u32)en;
+        u64 h = 0;
+        int is_new = 0;
+        if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
+            u64 key = h;
+            if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
+            key = key ? key : 1ull;
+            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        }
+        commit_new<S, K>(is_new, w, m, d, P, B, idx, lane);
+    }
+    if (live && gen == 0) atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)idx);
+    // wave reduction of the generated count, one atomic per wave
+    u32 g = gen;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) g += __shfl_xor(g, off);
+    if (__lane_id() == 0 && g) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)g);
+}
+
+// Insert n staged initial states (packed) into the set and the store.
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT, const DevBufs B, const u32* staged,
+                                              u64 n) {
+    constexpr int NW = 2 * S + K;
+    constexpr int NP = SYM ? NPerm<S>::v : 1;
+    const u64 t = (u64)blockIdx.x * 256ull + threadIdx.x;
+    const bool live = t < n;
+    u64 w[S];
+    u32 m[K];
+    if (live) {
+        load_state<S, K>(staged + t * (u64)NW, w, m);
+    } else {
+#pragma unroll
+        for (int i = 0; i < S; ++i) w[i] = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) m[q] = 0;
+    }
+    int is_new = 0;
+    if (live) {
+        u64 key = state_fp<S, K>(w, m);
+        if constexpr (SYM) {
+            u64 hp[NP];
+            perm_fps<S, K, NP>(w, m, PT, hp);
+            key = ~0ull;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
+        }
+        key = key ? key : 1ull;
+        is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+    }
+    Delta d;  // identity delta: the state itself
+    d.srv = -1; d.rm = -1; d.has_add = 0; d.add = 0; d.en = 1; d.w_new = 0;
+    commit_new<S, K>(is_new, w, m, d, P, B, ~0ull, 255);
+}
+
+// Every enabled lane of n given states, written out without dedup.
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT, const u32* in, u64 n, u32* out,
+                                              u64 cap, unsigned long long* count) {
+    constexpr int NW = 2 * S + K;
+    constexpr int NP = SYM ? NPerm<S>::v : 1;
+    constexpr int RW = 6 + NW;  // record: parent(2) lane(1) flags(1) fp(2) + state
+    const u64 t = (u64)blockIdx.x * 256ull + threadIdx.x;
+    if (t >= n) return;
+    u64 w[S];
+    u32 m[K];
+    load_state<S, K>(in + t * (u64)NW, w, m);
+    const u64 h0 = state_fp<S, K>(w, m);
+    u64 hp[NP];
+    if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
+    const int nl = P.off[10];
+    for (int lane = 0; lane < nl; ++lane) {
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        if (!d.en) continue;
+        u64 h = 0;
+        const int in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
+        if (in_model) {
+            if constexpr (SYM) h = canon_key<S, K, NP>(w, m, hp, d, PT);
+        }
+        const u64 o = atomicAdd(count, 1ull);
+        if (o >= cap) continue;
+        u32* r = out + o * (u64)RW;
+        r[0] = (u32)t; r[1] = (u32)(t >> 32); r[2] = (u32)lane; r[3] = (u32)in_model;
+        r[4] = (u32)h; r[5] = (u32)(h >> 32);
+        u64 wo[S];
+        u32 mo[K];
+        if (in_model) {
+            materialise<S, K>(w, m, d, wo, mo);
+        } else {
+#pragma unroll
+            for (int i = 0; i < S; ++i) wo[i] = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) mo[q] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < S; ++i) { r[6 + 2 * i] = (u32)wo[i]; r[7 + 2 * i] = (u32)(wo[i] >> 32); }
+#pragma unroll
+        for (int q = 0; q < K; ++q) r[6 + 2 * S + q] = mo[q];
+    }
+}
+
+// ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
+template <int S, int K, bool SYM>
+static hipError_t launch_t(int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
+                           const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
+    const u64 n = which == 0 ? (b - a) : a;
+    if (n == 0) return hipSuccess;
+    const u64 blocks = (n + 255) / 256;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    if (which == 0) {
+        hipLaunchKernelGGL((k_expand<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, a, b);
+    } else if (which == 1) {
+        hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
+    } else {
+        hipLaunchKernelGGL((k_list<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, in, a, out, cap,
+                           count);
+    }
+    return hipGetLastError();
+}
+
+template <int S, int K>
+static hipError_t launch_sk(bool sym, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
+                            const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
+    if constexpr (S <= 4) {
+        if (sym) return launch_t<S, K, true>(which, P, PT, B, a, b, in, out, cap, count, st);
+    } else {
+        if (sym) return hipErrorInvalidValue;
+    }
+    return launch_t<S, K, false>(which, P, PT, B, a, b, in, out, cap, count, st);
+}
+
+hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
+                  const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
+#define RMC_CASE(SS, KK) \
+    if (sh.S == SS && sh.K == KK) return launch_sk<SS, KK>(sh.sym, which, P, PT, B, a, b, in, out, cap, count, st);
+    RMC_CASE(2, 4) RMC_CASE(2, 8) RMC_CASE(3, 4) RMC_CASE(3, 8) RMC_CASE(4, 4) RMC_CASE(4, 8) RMC_CASE(5, 4)
+    RMC_CASE(5, 8)
+#undef RMC_CASE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace rmc

@@ -1,0 +1,191 @@
+// rmc_tlc.cpp — `rmc-tlc`, a drop-in for `java tlc2.TLC` on raft.tla models.
+//
+// Same command line shape as TLC (`[-workers N] [-config X.cfg] [-depth N]
+// [-deadlock] X.tla`) and the same summary lines, so scripts that grep TLC's
+// output ("states generated", "distinct states found", "depth of the complete
+// state graph", "Error: Invariant ... is violated", "State N:") keep working.
+// It is the host side above the C ABI (include/rmc.h); Java users bind the
+// same symbols through Panama.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <vector>
+
+#include "../../include/rmc.h"
+
+namespace {
+
+const char* kFamilies[10] = {"Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
+                             "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage", "DropMessage"};
+const char* kRoles[3] = {"Follower", "Candidate", "Leader"};
+const char* kMtypes[4] = {"RequestVoteRequest", "RequestVoteResponse", "AppendEntriesRequest",
+                          "AppendEntriesResponse"};
+
+std::string srv(int i) { return "r" + std::to_string(i + 1); }
+std::string val(int v) { return "v" + std::to_string(v + 1); }
+
+std::string seq(const rmc_entry* e, int n) {
+    if (n == 0) return "<<>>";
+    std::string s = "<<";
+    for (int x = 0; x < n; ++x) {
+        if (x) s += ", ";
+        s += "[term |-> " + std::to_string(e[x].term) + ", value |-> " + val(e[x].value) + "]";
+    }
+    return s + ">>";
+}
+
+template <class F>
+std::string fn(int S, F f) {  // (r1 :> f(0) @@ r2 :> f(1) ...)
+    std::string s = "(";
+    for (int i = 0; i < S; ++i) {
+        if (i) s += " @@ ";
+        s += srv(i) + " :> " + f(i);
+    }
+    return s + ")";
+}
+
+std::string set_of(uint32_t m, int S) {
+    std::string s = "{";
+    bool first = true;
+    for (int i = 0; i < S; ++i)
+        if (m >> i & 1) { s += (first ? "" : ", ") + srv(i); first = false; }
+    return s + "}";
+}
+
+std::string msg(const rmc_msg_view& m) {
+    std::string s = "[mtype |-> " + std::string(kMtypes[m.mtype]) + ", mterm |-> " + std::to_string(m.mterm);
+    switch (m.mtype) {
+        case 0: s += ", mlastLogTerm |-> " + std::to_string(m.mlastLogTerm) + ", mlastLogIndex |-> " +
+                     std::to_string(m.mlastLogIndex); break;
+        case 1: s += std::string(", mvoteGranted |-> ") + (m.mvoteGranted ? "TRUE" : "FALSE") + ", mlog |-> " +
+                     seq(m.mlog, m.mlog_len); break;
+        case 2: s += ", mprevLogIndex |-> " + std::to_string(m.mprevLogIndex) + ", mprevLogTerm |-> " +
+                     std::to_string(m.mprevLogTerm) + ", mentries |-> " + seq(m.mentries, m.mentries_len) +
+                     ", mcommitIndex |-> " + std::to_string(m.mcommitIndex); break;
+        default: s += std::string(", msuccess |-> ") + (m.msuccess ? "TRUE" : "FALSE") + ", mmatchIndex |-> " +
+                      std::to_string(m.mmatchIndex);
+    }
+    return s + ", msource |-> " + srv(m.msource) + ", mdest |-> " + srv(m.mdest) + "]";
+}
+
+void print_state(const rmc_state_view& v) {
+    const int S = v.n_servers;
+    std::string bag = v.n_msgs ? "(" : "<<>>";
+    for (int q = 0; q < v.n_msgs; ++q) {
+        if (q) bag += " @@ ";
+        bag += msg(v.msgs[q]) + " :> " + std::to_string(v.msgs[q].count);
+    }
+    if (v.n_msgs) bag += ")";
+    printf("/\\ messages = %s\n", bag.c_str());
+    printf("/\\ currentTerm = %s\n", fn(S, [&](int i) { return std::to_string(v.currentTerm[i]); }).c_str());
+    printf("/\\ state = %s\n", fn(S, [&](int i) { return std::string(kRoles[v.state[i]]); }).c_str());
+    printf("/\\ votedFor = %s\n",
+           fn(S, [&](int i) { return v.votedFor[i] < 0 ? std::string("Nil") : srv(v.votedFor[i]); }).c_str());
+    printf("/\\ log = %s\n", fn(S, [&](int i) { return seq(v.log[i], v.log_len[i]); }).c_str());
+    printf("/\\ commitIndex = %s\n", fn(S, [&](int i) { return std::to_string(v.commitIndex[i]); }).c_str());
+    printf("/\\ votesResponded = %s\n", fn(S, [&](int i) { return set_of(v.votesResponded[i], S); }).c_str());
+    printf("/\\ votesGranted = %s\n", fn(S, [&](int i) { return set_of(v.votesGranted[i], S); }).c_str());
+    printf("/\\ nextIndex = %s\n", fn(S, [&](int i) {
+               return fn(S, [&](int j) { return std::to_string(v.nextIndex[i][j]); });
+           }).c_str());
+    printf("/\\ matchIndex = %s\n", fn(S, [&](int i) {
+               return fn(S, [&](int j) { return std::to_string(v.matchIndex[i][j]); });
+           }).c_str());
+}
+
+const char* inv_name(int bit) {
+    switch (bit) {
+        case RMC_INV_TYPEOK: return "TypeOK";
+        case RMC_INV_ONE_LEADER: return "OneLeaderPerTerm";
+        case RMC_INV_LOG_MATCHING: return "LogMatching";
+    }
+    return "?";
+}
+
+int progress(const rmc_level_stats* s, void*) {
+    printf("Progress(%d) at %.2fs: %llu states generated, %llu distinct states found, %llu states left on queue.\n",
+           s->level + 1, s->seconds, (unsigned long long)s->generated, (unsigned long long)s->distinct,
+           (unsigned long long)s->new_states);
+    fflush(stdout);
+    return 0;
+}
+
+int usage() {
+    fprintf(stderr, "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N] X.tla\n");
+    return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string cfg, tla;
+    int depth = 0, device = 0, nodeadlock = 0;
+    unsigned long long capacity = 0;
+    for (int a = 1; a < argc; ++a) {
+        std::string s = argv[a];
+        auto next = [&]() -> const char* { return a + 1 < argc ? argv[++a] : nullptr; };
+        if (s == "-config") { const char* v = next(); if (!v) return usage(); cfg = v; }
+        else if (s == "-depth") { const char* v = next(); if (!v) return usage(); depth = atoi(v); }
+        else if (s == "-deadlock") nodeadlock = 1;  // TLC: -deadlock turns deadlock checking OFF
+        else if (s == "-device") { const char* v = next(); if (!v) return usage(); device = atoi(v); }
+        else if (s == "-capacity") { const char* v = next(); if (!v) return usage(); capacity = strtoull(v, nullptr, 10); }
+        else if (s == "-workers") { if (!next()) return usage(); }  // accepted for compatibility
+        else if (s[0] == '-') { fprintf(stderr, "unsupported option %s\n", s.c_str()); return usage(); }
+        else tla = s;
+    }
+    if (tla.empty()) return usage();
+    if (cfg.empty()) cfg = (tla.size() > 4 && tla.substr(tla.size() - 4) == ".tla" ? tla.substr(0, tla.size() - 4) : tla) + ".cfg";
+    printf("rmc-tlc: %s\n", rmc_version());
+    rmc_config c;
+    char err[512];
+    int rc = rmc_config_from_files(cfg.c_str(), tla.c_str(), &c, err, sizeof err);
+    if (rc) { printf("Error: %s\n", err); return 1; }
+    c.device = device;
+    c.max_depth = depth;
+    c.state_capacity = capacity;
+    if (nodeadlock) c.flags &= ~RMC_FLAG_CHECK_DEADLOCK;
+    printf("Model: %d servers, %d values, CONSTRAINT MaxTerm=%d MaxLogLen=%d MaxMsgs=%d MaxDup=%d%s%s\n",
+           c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,
+           (c.flags & RMC_FLAG_SYMMETRY) ? ", SYMMETRY Permutations(Server)" : "",
+           (c.flags & RMC_FLAG_BUG_QUORUM) ? ", BecomeLeader quorum guard weakened" : "");
+    rmc_ctx* ctx = nullptr;
+    rc = rmc_create(&c, &ctx);
+    if (rc) { printf("Error: rmc_create failed (%d)\n", rc); return 1; }
+    printf("Computing initial states...\n");
+    rc = rmc_run_bfs(ctx, progress, nullptr);
+    if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
+    rmc_result r;
+    rmc_get_result(ctx, &r);
+    int exitcode = 0;
+    if (r.violated_inv || r.deadlock) {
+        if (r.violated_inv) printf("Error: Invariant %s is violated.\n", inv_name(r.violated_inv));
+        else printf("Error: Deadlock reached.\n");
+        printf("Error: The behavior up to this point is:\n");
+        size_t len = 0;
+        rmc_trace(ctx, nullptr, nullptr, nullptr, 0, &len);
+        std::vector<rmc_state_view> st(len);
+        std::vector<int32_t> fam(len), inst(len);
+        rmc_trace(ctx, st.data(), fam.data(), inst.data(), len, &len);
+        for (size_t k = 0; k < len; ++k) {
+            if (fam[k] < 0) printf("State %zu: <Initial predicate>\n", k + 1);
+            else printf("State %zu: <%s lane %d of module raft>\n", k + 1, kFamilies[fam[k]], inst[k]);
+            print_state(st[k]);
+            printf("\n");
+        }
+        exitcode = 12;
+    } else {
+        printf("Model checking completed. No error has been found.\n");
+        printf("  Estimates of the probability that TLC did not check all reachable states\n"
+               "  because two distinct states had the same fingerprint:\n"
+               "  calculated (optimistic):  val = %.1E\n", r.collision_probability);
+    }
+    printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
+           (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
+    printf("The depth of the complete state graph search is %d.\n", r.depth);
+    printf("Finished in %.0fms (%.0f distinct states/s)\n", r.seconds * 1e3, r.distinct / (r.seconds > 0 ? r.seconds : 1));
+    rmc_destroy(ctx);
+    return exitcode;
+}

@@ -1,0 +1,210 @@
+"""Python binding of librmc.so (include/rmc.h) — used by tests and bench.py.
+
+The product is the HIP library; this module is a thin ctypes layer with the
+same names and meanings as the C ABI.  It never falls back to a CPU path:
+if `lib/librmc.so` is missing, importing `rmc.native()` raises.
+
+TLC correspondence: `Config` = the .cfg bounds,
+`Checker.run()` = `tlc2.TLC` BFS to fixpoint, `Result` = TLC's summary
+("N states generated, M distinct states found, Q left on queue", depth).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
+
+MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8
+FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM = 1, 2, 4
+INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING = 1, 2, 4
+INV_NAMES = {INV_TYPEOK: "TypeOK", INV_ONE_LEADER: "OneLeaderPerTerm",
+             INV_LOG_MATCHING: "LogMatching"}
+FAMILIES = ("Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
+            "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
+            "DropMessage")
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "HIP", -28: "CAPACITY", -19: "NOGPU",
+          -74: "PARSE", -71: "STATE"}
+
+
+class Config(C.Structure):
+    _fields_ = [("n_servers", C.c_int32), ("n_values", C.c_int32), ("max_term", C.c_int32),
+                ("max_log_len", C.c_int32), ("max_msgs", C.c_int32), ("max_dup", C.c_int32),
+                ("flags", C.c_uint32), ("invariants", C.c_uint32), ("device", C.c_int32),
+                ("max_depth", C.c_int32), ("state_capacity", C.c_uint64), ("seed", C.c_uint64)]
+
+
+class Result(C.Structure):
+    _fields_ = [("generated", C.c_uint64), ("distinct", C.c_uint64), ("left_on_queue", C.c_uint64),
+                ("depth", C.c_int32), ("violated_inv", C.c_int32), ("violation_depth", C.c_int32),
+                ("deadlock", C.c_int32), ("collision_probability", C.c_double),
+                ("seconds", C.c_double), ("expand_kernel_seconds", C.c_double),
+                ("expand_launches", C.c_uint64)]
+
+
+class LevelStats(C.Structure):
+    _fields_ = [("level", C.c_int32), ("pad", C.c_int32), ("generated", C.c_uint64),
+                ("distinct", C.c_uint64), ("new_states", C.c_uint64), ("seconds", C.c_double)]
+
+
+class Entry(C.Structure):
+    _fields_ = [("term", C.c_int32), ("value", C.c_int32)]
+
+
+class MsgView(C.Structure):
+    _fields_ = [("mtype", C.c_int32), ("mterm", C.c_int32), ("msource", C.c_int32),
+                ("mdest", C.c_int32), ("mlastLogTerm", C.c_int32), ("mlastLogIndex", C.c_int32),
+                ("mvoteGranted", C.c_int32), ("mlog_len", C.c_int32), ("mlog", Entry * MAX_LOG),
+                ("mprevLogIndex", C.c_int32), ("mprevLogTerm", C.c_int32),
+                ("mentries_len", C.c_int32), ("mentries", Entry * 1), ("mcommitIndex", C.c_int32),
+                ("msuccess", C.c_int32), ("mmatchIndex", C.c_int32), ("count", C.c_int32)]
+
+
+class StateView(C.Structure):
+    _fields_ = [("n_servers", C.c_int32), ("n_msgs", C.c_int32),
+                ("currentTerm", C.c_int32 * MAX_SERVERS), ("state", C.c_int32 * MAX_SERVERS),
+                ("votedFor", C.c_int32 * MAX_SERVERS), ("commitIndex", C.c_int32 * MAX_SERVERS),
+                ("log_len", C.c_int32 * MAX_SERVERS),
+                ("log", (Entry * MAX_LOG) * MAX_SERVERS),
+                ("votesResponded", C.c_uint32 * MAX_SERVERS),
+                ("votesGranted", C.c_uint32 * MAX_SERVERS),
+                ("nextIndex", (C.c_int32 * MAX_SERVERS) * MAX_SERVERS),
+                ("matchIndex", (C.c_int32 * MAX_SERVERS) * MAX_SERVERS),
+                ("msgs", MsgView * MAX_MSGS)]
+
+
+class SuccView(C.Structure):
+    _fields_ = [("parent", C.c_uint64), ("family", C.c_int32), ("instance", C.c_int32),
+                ("in_constraint", C.c_int32), ("pad", C.c_int32), ("fingerprint", C.c_uint64),
+                ("state", StateView)]
+
+
+PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.POINTER(LevelStats), C.c_void_p)
+
+# Every symbol include/rmc.h declares (checked by tests/test_abi.py).
+EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_run_bfs",
+           "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
+           "rmc_config_from_files")
+
+_lib = None
+
+
+def native():
+    """Load lib/librmc.so (built by `make -C raft.tla_amd`); raise if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"librmc.so not built: {LIB_PATH} (run __graft_entry__.build())")
+        lib = C.CDLL(LIB_PATH)
+        lib.rmc_create.argtypes = [C.POINTER(Config), C.POINTER(C.c_void_p)]
+        lib.rmc_create.restype = C.c_int
+        lib.rmc_destroy.argtypes = [C.c_void_p]
+        lib.rmc_destroy.restype = None
+        lib.rmc_last_error.argtypes = [C.c_void_p]
+        lib.rmc_last_error.restype = C.c_char_p
+        lib.rmc_version.argtypes = []
+        lib.rmc_version.restype = C.c_char_p
+        lib.rmc_run_bfs.argtypes = [C.c_void_p, PROGRESS_FN, C.c_void_p]
+        lib.rmc_run_bfs.restype = C.c_int
+        lib.rmc_get_result.argtypes = [C.c_void_p, C.POINTER(Result)]
+        lib.rmc_get_result.restype = C.c_int
+        lib.rmc_trace.argtypes = [C.c_void_p, C.POINTER(StateView), C.POINTER(C.c_int32),
+                                  C.POINTER(C.c_int32), C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.rmc_trace.restype = C.c_int
+        lib.rmc_state_bytes.argtypes = [C.POINTER(Config)]
+        lib.rmc_state_bytes.restype = C.c_size_t
+        lib.rmc_expand.argtypes = [C.c_void_p, C.POINTER(StateView), C.c_size_t,
+                                   C.POINTER(SuccView), C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.rmc_expand.restype = C.c_int
+        lib.rmc_config_from_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Config),
+                                              C.c_char_p, C.c_size_t]
+        lib.rmc_config_from_files.restype = C.c_int
+        _lib = lib
+    return _lib
+
+
+class RmcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rmc error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+def make_config(n_servers=3, n_values=2, max_term=2, max_log_len=1, max_msgs=2, max_dup=1,
+                symmetry=False, bug_quorum=False, invariants=INV_TYPEOK, check_deadlock=True,
+                device=0, max_depth=0, state_capacity=0):
+    flags = (FLAG_SYMMETRY if symmetry else 0) | (FLAG_BUG_QUORUM if bug_quorum else 0) | \
+        (FLAG_CHECK_DEADLOCK if check_deadlock else 0)
+    return Config(n_servers, n_values, max_term, max_log_len, max_msgs, max_dup, flags,
+                  invariants, device, max_depth, state_capacity, 0)
+
+
+def config_from_files(cfg_path, tla_path=None):
+    lib = native()
+    cfg = Config()
+    err = C.create_string_buffer(512)
+    rc = lib.rmc_config_from_files(cfg_path.encode(), tla_path.encode() if tla_path else None,
+                                   C.byref(cfg), err, 512)
+    if rc:
+        raise RmcError(rc, err.value.decode())
+    return cfg
+
+
+class Checker:
+    """One model-checking context on one GPU (rmc_ctx)."""
+
+    def __init__(self, cfg: Config):
+        self.lib = native()
+        self.cfg = cfg
+        self.ctx = C.c_void_p()
+        rc = self.lib.rmc_create(C.byref(cfg), C.byref(self.ctx))
+        if rc:
+            raise RmcError(rc, "rmc_create failed (see stderr)")
+
+    def close(self):
+        if self.ctx:
+            self.lib.rmc_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc):
+        if rc:
+            raise RmcError(rc, self.lib.rmc_last_error(self.ctx).decode())
+
+    def run(self, progress=None) -> Result:
+        levels = []
+
+        def cb(p, _u):
+            s = p.contents
+            levels.append((s.level, s.generated, s.distinct, s.new_states, s.seconds))
+            return int(bool(progress and progress(s)))
+
+        fn = PROGRESS_FN(cb)
+        self._check(self.lib.rmc_run_bfs(self.ctx, fn, None))
+        res = Result()
+        self._check(self.lib.rmc_get_result(self.ctx, C.byref(res)))
+        self.levels = levels
+        return res
+
+    def trace(self):
+        n = C.c_size_t()
+        self._check(self.lib.rmc_trace(self.ctx, None, None, None, 0, C.byref(n)))
+        st = (StateView * n.value)()
+        fam = (C.c_int32 * n.value)()
+        inst = (C.c_int32 * n.value)()
+        self._check(self.lib.rmc_trace(self.ctx, st, fam, inst, n.value, C.byref(n)))
+        return [(fam[k], inst[k], st[k]) for k in range(n.value)]
+
+    def expand(self, views):
+        arr = (StateView * len(views))(*views)
+        lanes_max = 5 + 5 + 25 + 5 + 10 + 5 + 25 + 3 * 8
+        cap = max(1, len(views) * lanes_max)
+        out = (SuccView * cap)()
+        n = C.c_size_t()
+        self._check(self.lib.rmc_expand(self.ctx, arr, len(views), out, cap, C.byref(n)))
+        return [out[k] for k in range(min(n.value, cap))]

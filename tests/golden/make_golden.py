@@ -1,0 +1,56 @@
+"""Generates tests/golden/oracle_levels.json from the C oracle (oracle/rmc_oracle.c).
+
+The reference ships no golden vectors for this path, and TLC
+is absent from this container, so these fixtures are produced by the repo's
+own CPU restatements.  Tiny configs are cross-checked against the Python
+restatement (oracle/raft_spec.py) in tests/test_oracle.py; the hand-derived
+KATs of SURVEY.md §4 are asserted there too.  Run from the repo root:
+    python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+from tests import oracle_c  # noqa: E402
+
+# name: (S, V, MaxTerm, MaxLog, MaxMsgs, MaxDup, bug, inv_mask, sym, max_levels)
+CONFIGS = {
+    "tiny2": (2, 1, 2, 1, 2, 1, 0, 1, 0, 0),
+    "tiny2_v2": (2, 2, 3, 2, 2, 1, 0, 1, 0, 0),
+    "small": (3, 2, 2, 1, 1, 1, 0, 1, 0, 0),
+    "small_sym": (3, 2, 2, 1, 1, 1, 0, 1, 1, 0),
+    "s3_v1_msgs1": (3, 1, 2, 1, 1, 1, 0, 1, 0, 0),
+    "bounded_prefix14": (3, 2, 2, 1, 2, 1, 0, 1, 0, 14),
+    "bounded_sym_prefix16": (3, 2, 2, 1, 2, 1, 0, 1, 1, 16),
+    "msgs5_dup2_prefix9": (3, 2, 3, 2, 5, 2, 0, 1, 0, 9),
+    "s4_prefix10": (4, 1, 2, 1, 2, 1, 0, 1, 0, 10),
+    "s5_prefix9": (5, 2, 2, 1, 2, 1, 0, 1, 0, 9),
+    "bug_one_leader": (3, 2, 3, 1, 3, 1, 1, 2, 0, 0),
+    "bug_log_matching": (3, 2, 3, 1, 3, 1, 1, 4, 0, 0),
+    "bug_both": (3, 2, 3, 1, 3, 1, 1, 6, 0, 0),
+}
+
+
+def main():
+    out = {}
+    for name, (S, V, mt, ml, mm, md, bug, inv, sym, lv) in CONFIGS.items():
+        r, ln, lg = oracle_c.bfs(S, V, mt, ml, mm, md, bug=bug, inv=inv, sym=sym, threads=8,
+                                 max_levels=lv, capacity=1 << 25)
+        out[name] = dict(params=dict(n_servers=S, n_values=V, max_term=mt, max_log_len=ml,
+                                     max_msgs=mm, max_dup=md, bug_quorum=bug, invariants=inv,
+                                     symmetry=sym, max_depth=lv),
+                         generated=r.generated, distinct=r.distinct, depth=r.depth,
+                         left_on_queue=r.left_on_queue, violated_inv=r.violated_inv,
+                         violation_depth=r.violation_depth, level_new=ln,
+                         level_generated=lg[:r.depth])
+        print(name, r.distinct, r.generated, r.depth, r.violated_inv, r.violation_depth,
+              f"{r.seconds:.2f}s", flush=True)
+    with open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,132 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the oracles.
+
+Bit-exact bar (integer work): distinct/generated counts, per-level new-state
+counts, depth, violation depth, and per-lane successor sets on fuzzed states
+must equal the oracle's."""
+import json
+import os
+import random
+from collections import Counter, defaultdict
+
+import pytest
+
+import rmc
+from oracle import raft_spec as R
+from tests.convert import from_view, random_state, to_view
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_levels.json")))
+
+
+def cfg_from(p, capacity=1 << 25):
+    return rmc.make_config(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                           max_log_len=p["max_log_len"], max_msgs=p["max_msgs"],
+                           max_dup=p["max_dup"], symmetry=bool(p["symmetry"]),
+                           bug_quorum=bool(p["bug_quorum"]), invariants=p["invariants"],
+                           max_depth=p["max_depth"], state_capacity=capacity)
+
+
+def run(cfg):
+    with rmc.Checker(cfg) as ck:
+        res = ck.run()
+        levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+        trace = ck.trace() if (res.violated_inv or res.deadlock) else None
+    return res, levels, trace
+
+
+def test_kat_first_levels():
+    """SURVEY.md §4 KATs: 1/3/18 new states, 6 and 27 generated (levels 1-2)."""
+    cfg = rmc.make_config(max_term=14, max_log_len=3, max_msgs=8, max_dup=3, max_depth=3,
+                          state_capacity=1 << 16)
+    res, levels, _ = run(cfg)
+    assert levels == [1, 3, 18]
+    assert (res.generated, res.distinct, res.depth, res.left_on_queue) == (34, 22, 3, 18)
+    cfg = rmc.make_config(max_term=14, max_log_len=3, max_msgs=8, max_dup=3, max_depth=3,
+                          symmetry=True, state_capacity=1 << 16)
+    res, levels, _ = run(cfg)
+    assert levels == [1, 1, 5]
+    assert res.generated == 1 + 6 + 9
+
+
+BFS_CASES = ["tiny2", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
+             "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9"]
+
+
+@pytest.mark.parametrize("name", BFS_CASES)
+def test_bfs_matches_oracle(name):
+    g = GOLDEN[name]
+    res, levels, _ = run(cfg_from(g["params"]))
+    assert levels == g["level_new"]
+    assert res.distinct == g["distinct"]
+    assert res.generated == g["generated"]
+    assert res.depth == g["depth"]
+    assert res.left_on_queue == g["left_on_queue"]
+    assert res.violated_inv == 0 and res.deadlock == 0
+
+
+@pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both"])
+def test_bug_variant_violation_and_trace(name):
+    g = GOLDEN[name]
+    p = g["params"]
+    res, levels, trace = run(cfg_from(p))
+    assert res.violated_inv == g["violated_inv"]
+    assert res.violation_depth == g["violation_depth"]
+    assert res.distinct == g["distinct"] and res.generated == g["generated"]
+    # the trace is a behaviour of the spec from Init to a violating state
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
+                    bug_quorum=True)
+    assert len(trace) == res.violation_depth
+    states = [from_view(v) for _f, _i, v in trace]
+    assert states[0] == R.init_state(model) and trace[0][0] == -1
+    for a, b, (fam, _inst, _v) in zip(states, states[1:], trace[1:]):
+        succ = {(f, t) for f, _p, t in R.successors(model, a)}
+        assert (rmc.FAMILIES[fam], b) in succ
+        assert R.in_constraint(model, b)
+    inv = {rmc.INV_ONE_LEADER: R.one_leader_per_term, rmc.INV_LOG_MATCHING: R.log_matching}
+    assert not inv[res.violated_inv](model, states[-1])
+    assert all(inv[res.violated_inv](model, s) for s in states[:-1])
+
+
+FUZZ = [
+    dict(n_servers=3, n_values=2, max_term=3, max_log=2, max_msgs=4, max_dup=2),
+    dict(n_servers=3, n_values=2, max_term=4, max_log=3, max_msgs=7, max_dup=3),
+    dict(n_servers=2, n_values=1, max_term=2, max_log=1, max_msgs=2, max_dup=1),
+    dict(n_servers=4, n_values=2, max_term=3, max_log=2, max_msgs=4, max_dup=2),
+    dict(n_servers=5, n_values=2, max_term=3, max_log=3, max_msgs=6, max_dup=2),
+    dict(n_servers=3, n_values=2, max_term=3, max_log=3, max_msgs=4, max_dup=1, bug_quorum=True),
+]
+
+
+@pytest.mark.parametrize("k", range(len(FUZZ)))
+def test_expand_matches_oracle_on_fuzzed_states(k):
+    """Differential fuzzing in the spirit of SmokeInit:
+    every lane of random type-correct states, GPU vs the Python restatement."""
+    m = R.Model(**FUZZ[k])
+    rng = random.Random(1000 + k)
+    states = [random_state(m, rng) for _ in range(600)]
+    cfg = rmc.make_config(n_servers=m.n_servers, n_values=m.n_values, max_term=m.max_term,
+                          max_log_len=m.max_log, max_msgs=m.max_msgs, max_dup=m.max_dup,
+                          bug_quorum=m.bug_quorum, state_capacity=1 << 12)
+    with rmc.Checker(cfg) as ck:
+        out = ck.expand([to_view(m, s) for s in states])
+    gpu_gen = defaultdict(Counter)
+    gpu_in = defaultdict(Counter)
+    fps = {}
+    for sv in out:
+        fam = rmc.FAMILIES[sv.family]
+        gpu_gen[sv.parent][fam] += 1
+        if sv.in_constraint:
+            t = from_view(sv.state)
+            gpu_in[sv.parent][(fam, t)] += 1
+            assert fps.setdefault(t, sv.fingerprint) == sv.fingerprint  # fp is a function of the state
+    for idx, s in enumerate(states):
+        ora_gen = Counter()
+        ora_in = Counter()
+        for f, _p, t in R.successors(m, s):
+            ora_gen[f] += 1
+            if R.in_constraint(m, t):
+                ora_in[(f, t)] += 1
+        assert gpu_gen[idx] == ora_gen, (idx, s)
+        assert gpu_in[idx] == ora_in, (idx, s)
