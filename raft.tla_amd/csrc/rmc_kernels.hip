@@ -159,48 +159,127 @@ __device__ __forceinline__ void commit_new(int is_new, const u64 (&w)[S], const 
     if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
 }
 
+// Per-wave list of new states, kept in LDS until a flush materialises them.
+constexpr int WCAP = 512;
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Materialise the wave's n listed new states: ONE global allocation atomic per
+// flush, then each lane re-derives one listed successor from its parent
+// (same lane_delta code, deterministic), stores it, its parent pointer and
+// lane, and runs the fused invariant checks.  Convergent: the whole wave
+// runs it together, so the rare new-state path does not serialise the
+// per-lane expansion loop.
+template <int S, int K>
+__device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                          const uint8_t* l_lane, u32 n) {
+    constexpr int NW = 2 * S + K;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    u64 base = 0;
+    if (me == 0) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)n);
+    base = bcast64(base, 0);
+    for (u32 e = (u32)me; e < n; e += 64) {
+        const u64 rel = l_rel[e];
+        const int lane = l_lane[e];
+        const u64 ni = base + e;
+        if (ni >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, d, wo, mo);
+        store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
+        B.parent[ni] = lo + rel;
+        B.act[ni] = (uint8_t)lane;
+        const int v = check_invariants<S, K>(wo, mo, P);
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
+    }
+    wave_sync_lds();
+}
+
+// Grid-stride over 256-state tiles of the frontier [lo, hi).
 template <int S, int K, bool SYM>
 __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr int NP = SYM ? NPerm<S>::v : 1;
-    const u64 idx = lo + (u64)blockIdx.x * 256ull + threadIdx.x;
-    const bool live = idx < hi;
-    u64 w[S];
-    u32 m[K];
-    if (live) {
-        load_state<S, K>(B.store + idx * (u64)NW, w, m);
-    } else {
-#pragma unroll
-        for (int i = 0; i < S; ++i) w[i] = 0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) m[q] = 0;
-    }
-    const u64 h0 = state_fp<S, K>(w, m);
-    u64 hp[NP];
-    if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
-    u32 gen = 0;
+    __shared__ u32 s_rel[4][WCAP];
+    __shared__ uint8_t s_lane[4][WCAP];
+    const int wv = (int)(threadIdx.x >> 6);
+    const int me = (int)__lane_id();
+    const u64 lt_mask = (1ull << me) - 1ull;
+    u32* l_rel = s_rel[wv];
+    uint8_t* l_lane = s_lane[wv];
+    u32 n = 0;  // wave-uniform list length
+    u64 gen = 0;
+    const u64 nf = hi - lo;
     const int nl = P.off[10];
-    for (int lane = 0; lane < nl; ++lane) {  // wave-uniform loop
-        Delta d;
-        lane_delta<S, K>(w, m, lane, P, d);
-        const int en = d.en && live;
-        gen += (u32)en;
-        u64 h = 0;
-        int is_new = 0;
-        if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
-            u64 key = h;
-            if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
-            key = key ? key : 1ull;
-            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
-        }
-        commit_new<S, K>(is_new, w, m, d, P, B, idx, lane);
-    }
-    if (live && gen == 0) atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)idx);
-    // wave reduction of the generated count, one atomic per wave
-    u32 g = gen;
+    for (u64 tile = (u64)blockIdx.x * 256ull; tile < nf; tile += (u64)gridDim.x * 256ull) {
+        const u64 rel = tile + threadIdx.x;
+        const bool live = rel < nf;
+        u64 w[S];
+        u32 m[K];
+        if (live) {
+            load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        } else {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) g += __shfl_xor(g, off);
-    if (__lane_id() == 0 && g) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)g);
+            for (int i = 0; i < S; ++i) w[i] = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) m[q] = 0;
+        }
+        const u64 h0 = state_fp<S, K>(w, m);
+        u64 hp[NP];
+        if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
+        u32 g = 0;
+        for (int lane = 0; lane < nl; ++lane) {  // wave-uniform loop
+            Delta d;
+            lane_delta<S, K>(w, m, lane, P, d);
+            const int en = d.en && live;
+            g += (u32)en;
+            u64 h = 0;
+            int is_new = 0;
+            if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
+                u64 key = h;
+                if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
+                key = key ? key : 1ull;
+                is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+            }
+            const u64 bal = __ballot(is_new);
+            if (bal) {
+                if (is_new) {
+                    const u32 pos = n + (u32)__popcll(bal & lt_mask);
+                    l_rel[pos] = (u32)rel;
+                    l_lane[pos] = (uint8_t)lane;
+                }
+                n += (u32)__popcll(bal);
+                if (n > (u32)(WCAP - 64)) {
+                    flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
+                    n = 0;
+                }
+            }
+        }
+        if (live && g == 0) atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)(lo + rel));
+        gen += g;
+    }
+    if (n) flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
+    // wave reduction of the generated count, one atomic per wave
+    u64 gs = gen;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const u32 lo32 = (u32)__shfl_xor((int)(u32)gs, off);
+        const u32 hi32 = (u32)__shfl_xor((int)(u32)(gs >> 32), off);
+        gs += ((u64)hi32 << 32) | lo32;
+    }
+    if (me == 0 && gs) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)gs);
 }
 
 // Insert n staged initial states (packed) into the set and the store.
@@ -287,6 +366,8 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
 }
 
 // ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
+static const u64 kExpandGrid = 2048;
+
 template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                            const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
@@ -295,7 +376,9 @@ static hipError_t launch_t(int which, const Params& P, const PermTable& PT, cons
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     if (which == 0) {
-        hipLaunchKernelGGL((k_expand<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, a, b);
+        // grid-stride: about 8 resident 256-thread blocks per CU x 256 CUs
+        const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
+        hipLaunchKernelGGL((k_expand<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 1) {
         hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
     } else {

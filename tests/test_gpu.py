@@ -49,14 +49,14 @@ def test_kat_first_levels():
     assert res.generated == 1 + 6 + 9
 
 
-BFS_CASES = ["tiny2", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
+BFS_CASES = ["bounded_full", "tiny2", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
              "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9"]
 
 
 @pytest.mark.parametrize("name", BFS_CASES)
 def test_bfs_matches_oracle(name):
     g = GOLDEN[name]
-    res, levels, _ = run(cfg_from(g["params"]))
+    res, levels, _ = run(cfg_from(g["params"], capacity=max(1 << 25, int(g["distinct"] * 1.25))))
     assert levels == g["level_new"]
     assert res.distinct == g["distinct"]
     assert res.generated == g["generated"]
