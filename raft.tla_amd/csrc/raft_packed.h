@@ -122,18 +122,21 @@ struct Delta {
     int en;       // lane enabled (counts as generated)
 };
 
+// Runtime-indexed reads of register arrays as AND/OR masks: a select chain
+// gets folded by the compiler into a dynamically indexed load, which forces
+// the array out of registers into scratch (cdna_hip_programming.md §5.4 r20).
 template <int S>
 RMC_HD u64 selw(const u64 (&w)[S], int i) {
-    u64 r = w[0];
+    u64 r = 0;
 #pragma unroll
-    for (int k = 1; k < S; ++k) r = (i == k) ? w[k] : r;
+    for (int k = 0; k < S; ++k) r |= w[k] & (0ull - (u64)(i == k));
     return r;
 }
 template <int K>
 RMC_HD u32 selm(const u32 (&m)[K], int i) {
-    u32 r = m[0];
+    u32 r = 0;
 #pragma unroll
-    for (int k = 1; k < K; ++k) r = (i == k) ? m[k] : r;
+    for (int k = 0; k < K; ++k) r |= m[k] & (0u - (u32)(i == k));
     return r;
 }
 

@@ -45,6 +45,18 @@ __device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 
     return 0;
 }
 
+// Same protocol, given the already-loaded content `cur` of the first slot.
+__device__ __forceinline__ int fp_resolve(u64* __restrict__ table, u64 mask, u64 key, u64 cur, u32* full) {
+    if (cur == key) return 0;
+    const u64 s = key & mask;
+    if (cur == 0) {
+        const u64 prev = atomicCAS((unsigned long long*)&table[s], 0ull, (unsigned long long)key);
+        if (prev == 0) return 1;
+        if (prev == key) return 0;
+    }
+    return fp_insert(table, mask, key, full);  // rare: continue linear probing
+}
+
 template <int S, int K>
 __device__ __forceinline__ void load_state(const u32* __restrict__ base, u64 (&w)[S], u32 (&m)[K]) {
     const u64* ws = reinterpret_cast<const u64*>(base);
@@ -207,13 +219,16 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
     wave_sync_lds();
 }
 
-// Grid-stride over 256-state tiles of the frontier [lo, hi).
-template <int S, int K, bool SYM>
+// Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
+// processed BATCH at a time so BATCH fingerprint probes per thread are in
+// flight together (the kernel is bound by probe latency, not bandwidth).
+template <int S, int K, bool SYM, int BATCH>
 __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr int NP = SYM ? NPerm<S>::v : 1;
     __shared__ u32 s_rel[4][WCAP];
     __shared__ uint8_t s_lane[4][WCAP];
+    __shared__ u64 s_key[BATCH][256];
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
     const u64 lt_mask = (1ull << me) - 1ull;
@@ -240,30 +255,66 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
         u64 hp[NP];
         if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
         u32 g = 0;
-        for (int lane = 0; lane < nl; ++lane) {  // wave-uniform loop
-            Delta d;
-            lane_delta<S, K>(w, m, lane, P, d);
-            const int en = d.en && live;
-            g += (u32)en;
-            u64 h = 0;
-            int is_new = 0;
-            if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
-                u64 key = h;
-                if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
-                key = key ? key : 1ull;
-                is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
-            }
-            const u64 bal = __ballot(is_new);
-            if (bal) {
-                if (is_new) {
-                    const u32 pos = n + (u32)__popcll(bal & lt_mask);
-                    l_rel[pos] = (u32)rel;
-                    l_lane[pos] = (uint8_t)lane;
+        for (int lane0 = 0; lane0 < nl; lane0 += BATCH) {  // wave-uniform loop
+            // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe)
+            for (int b = 0; b < BATCH; ++b) {
+                const int lane = lane0 + b;
+                u64 key = 0;
+                if (lane < nl) {
+                    Delta d;
+                    lane_delta<S, K>(w, m, lane, P, d);
+                    const int en = d.en && live;
+                    g += (u32)en;
+                    u64 h = 0;
+                    if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
+                        key = h;
+                        if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
+                        key = key ? key : 1ull;
+                    }
                 }
-                n += (u32)__popcll(bal);
-                if (n > (u32)(WCAP - 64)) {
-                    flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
-                    n = 0;
+                s_key[b][threadIdx.x] = key;
+            }
+            // (b) BATCH independent first-slot probes in flight at once
+            u64 key[BATCH], cur[BATCH];
+#pragma unroll
+            for (int b = 0; b < BATCH; ++b) {
+                key[b] = s_key[b][threadIdx.x];
+                cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
+            }
+            // (c) resolve: hit -> duplicate; empty -> CAS; mismatch -> slow path
+            u32 newbits = 0, slowbits = 0;
+#pragma unroll
+            for (int b = 0; b < BATCH; ++b) {
+                if (!key[b] || cur[b] == key[b]) continue;
+                if (cur[b] == 0) {
+                    const u64 prev = atomicCAS((unsigned long long*)&B.table[key[b] & B.tmask], 0ull,
+                                               (unsigned long long)key[b]);
+                    if (prev == 0) newbits |= 1u << b;
+                    else if (prev != key[b]) slowbits |= 1u << b;
+                } else {
+                    slowbits |= 1u << b;
+                }
+            }
+            while (slowbits) {  // rare: linear probing past an occupied first slot
+                const int b = __builtin_ctz(slowbits);
+                slowbits &= slowbits - 1;
+                if (fp_insert(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full)) newbits |= 1u << b;
+            }
+            // (d) list the winners (wave-aggregated, no global atomics)
+            for (int b = 0; b < BATCH; ++b) {
+                const int is_new = (newbits >> b) & 1u;
+                const u64 bal = __ballot(is_new);
+                if (bal) {
+                    if (is_new) {
+                        const u32 pos = n + (u32)__popcll(bal & lt_mask);
+                        l_rel[pos] = (u32)rel;
+                        l_lane[pos] = (uint8_t)(lane0 + b);
+                    }
+                    n += (u32)__popcll(bal);
+                    if (n > (u32)(WCAP - 64)) {
+                        flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
+                        n = 0;
+                    }
                 }
             }
         }
@@ -368,6 +419,15 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
 // ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
 static const u64 kExpandGrid = 2048;
 
+// Probes in flight per thread (RMC_BATCH=4|8, default 8): a tuning knob.
+static int expand_batch() {
+    static int b = [] {
+        const char* e = getenv("RMC_BATCH");
+        return (e && atoi(e) == 4) ? 4 : 8;
+    }();
+    return b;
+}
+
 template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                            const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
@@ -378,7 +438,10 @@ static hipError_t launch_t(int which, const Params& P, const PermTable& PT, cons
     if (which == 0) {
         // grid-stride: about 8 resident 256-thread blocks per CU x 256 CUs
         const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
-        hipLaunchKernelGGL((k_expand<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        if (expand_batch() == 4)
+            hipLaunchKernelGGL((k_expand<S, K, SYM, 4>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        else
+            hipLaunchKernelGGL((k_expand<S, K, SYM, 8>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 1) {
         hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
     } else {
