@@ -26,9 +26,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBounded.cfg"))
-    ap.add_argument("--capacity", type=int, default=0, help="state capacity per GPU (0 = auto)")
-    ap.add_argument("--cpu-levels", type=int, default=24,
+    ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBench.cfg"))
+    ap.add_argument("--capacity", type=int, default=1_500_000_000,
+                    help="state capacity per GPU (0 = auto from free HBM)")
+    ap.add_argument("--no-probe-ceiling", action="store_true",
+                    help="skip the random-probe microbenchmark (roofline ceiling)")
+    ap.add_argument("--cpu-levels", type=int, default=22,
                     help="BFS levels of the same model timed on the host CPU oracle")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -64,6 +67,10 @@ def main():
     cfg.device = local if world > 1 else 0
     cfg.state_capacity = a.capacity
     W = rmc.native().rmc_state_bytes(cfg)
+    # roofline ceiling of the fingerprint set: random 8-B probes over 64 GB
+    r_max = None
+    if not a.no_probe_ceiling:
+        r_max = rmc.probe_bench(device=cfg.device, table_bytes=64 << 30, accesses=1 << 32, mode=0)
 
     def barrier():
         if dist is not None:
@@ -88,9 +95,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     per_step = dt / a.steps
-    G, D = res.generated, res.distinct
-    b_alg = G * 64 + D * (2 * W + 16)  # per run
-    achieved = b_alg / (kern / a.steps) / 1e9 if kern > 0 else 0.0
+    G, D, NP = res.generated, res.distinct, res.probes
+    # algorithmic bytes per run (DESIGN.md "Roofline"): one random 64-B granule
+    # per fingerprint probe + the new state written, read back as frontier,
+    # its 8-B parent pointer and 8-B fingerprint
+    b_alg = NP * 64 + D * (2 * W + 16)
+    ks = kern / a.steps
+    achieved = b_alg / ks / 1e9 if ks > 0 else 0.0
     out = {
         "metric": METRIC,
         "value": D / per_step,
@@ -118,6 +129,10 @@ def main():
             "kernel": "k_expand", "kernel_ms_per_step": kern / a.steps * 1e3,
             "launches_per_step": launches // a.steps,
             "alg_bytes_per_step": b_alg,
+            "probes_per_step": NP,
+            "probe_rate_per_s": NP / ks if ks > 0 else 0.0,
+            "probe_ceiling_per_s": r_max,
+            "frac_of_probe_ceiling": (NP / ks / r_max) if (ks > 0 and r_max) else None,
         },
     }
     if rank == 0 and not a.no_cpu:

@@ -89,6 +89,7 @@ typedef struct rmc_result {
     double expand_kernel_seconds; /* device time of the expansion kernels, HIP events on */
                                   /* the ctx stream (sum over levels)                    */
     uint64_t expand_launches;  /* levels expanded (one timed launch group per level)    */
+    uint64_t probes;           /* fingerprint-set probes (successors that reached the set) */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */
@@ -183,6 +184,13 @@ int rmc_trace(rmc_ctx* ctx, rmc_state_view* states, int32_t* families, int32_t* 
 size_t rmc_state_bytes(const rmc_config* cfg);
 int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_view* out,
                size_t cap, size_t* n_out);
+
+/* ---- roofline microbenchmark -----------------------------------------------
+ * Random 8-byte accesses into a table of table_bytes on `device`, 8 in flight
+ * per thread, the access pattern of the fingerprint set: mode 0 = loads,
+ * mode 1 = CAS.  *per_second receives accesses/s (device time, HIP events).
+ * This is R_max of SURVEY.md §8d (no TLC analog). */
+int rmc_probe_bench(int device, uint64_t table_bytes, uint64_t accesses, int mode, double* per_second);
 
 /* ---- front-end -----------------------------------------------------------
  * Reads a TLC model (.tla root module + .cfg) of raft.tla and fills *cfg.

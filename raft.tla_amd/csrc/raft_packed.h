@@ -99,18 +99,24 @@ RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59)) : 0ul
 // ---- model parameters (runtime part) --------------------------------------------
 struct Params {
     int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;
-    int off[11];  // family lane offsets; off[10] = lanes per state
+    int off[11];  // family lane offsets (= Lanes<S,K>::off, for host code)
 };
 
 // Lane table: Restart S, Timeout S, RequestVote S^2,
-// BecomeLeader S, ClientRequest S*V, AdvanceCommitIndex S, AppendEntries S^2,
-// Receive K, DuplicateMessage K, DropMessage K.
+// BecomeLeader S, ClientRequest S*VMAX (lanes with v >= |Value| are never
+// enabled), AdvanceCommitIndex S, AppendEntries S^2, Receive K,
+// DuplicateMessage K, DropMessage K.  Compile-time, so an unrolled lane loop
+// folds each lane's family dispatch away.
+constexpr int VMAX = 2;
 template <int S, int K>
-inline void make_offsets(Params& P) {
-    const int sizes[10] = {S, S, S * S, S, S * P.V, S, S * S, K, K, K};
-    P.off[0] = 0;
-    for (int f = 0; f < 10; ++f) P.off[f + 1] = P.off[f] + sizes[f];
-}
+struct Lanes {
+    static constexpr int size(int f) {
+        return f == 0 ? S : f == 1 ? S : f == 2 ? S * S : f == 3 ? S : f == 4 ? S * VMAX
+             : f == 5 ? S : f == 6 ? S * S : K;
+    }
+    static constexpr int off(int f) { return f == 0 ? 0 : off(f - 1) + size(f - 1); }
+    static constexpr int N = off(10);
+};
 
 // A successor relative to its parent.
 struct Delta {
@@ -241,22 +247,30 @@ RMC_HD void receive_lane(const u64 (&w)[S], u32 msg, int k, Delta& d) {
     }
 }
 
-// Compute the delta of lane `lane` (0 <= lane < P.off[10]) on parent (w, m).
+// Compute the delta of lane `lane` (0 <= lane < Lanes<S,K>::N) on parent (w, m).
 template <int S, int K>
 RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Params& P, Delta& d) {
+    // Offsets read from the kernel argument (equal to Lanes<S,K>::off): as
+    // opaque runtime values they keep the family dispatch a branch tree; as
+    // compile-time constants the compiler if-converts every family into
+    // straight-line selects and the kernel needs 4x the registers.
+    struct {
+        const int* o;
+        RMC_HD int off(int f) const { return o[f]; }
+    } L{P.off};
     d.srv = -1;
     d.rm = -1;
     d.has_add = 0;
     d.add = 0;
     d.en = 0;
     d.w_new = 0;
-    if (lane < P.off[1]) {  // Restart(i) :136-143
+    if (lane < L.off(1)) {  // Restart(i) :136-143
         const int i = lane;
         d.srv = i;
         d.w_new = selw<S>(w, i) & RESTART_KEEP;
         d.en = 1;
-    } else if (lane < P.off[2]) {  // Timeout(i) :146-154
-        const int i = lane - P.off[1];
+    } else if (lane < L.off(2)) {  // Timeout(i) :146-154
+        const int i = lane - L.off(1);
         const u64 wi = selw<S>(w, i);
         const u32 st = w_st(wi);
         if (st == FOLLOWER || st == CANDIDATE) {
@@ -269,16 +283,16 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.w_new = wn;
             d.en = 1;
         }
-    } else if (lane < P.off[3]) {  // RequestVote(i, j) :157-166 (no i /= j guard)
-        const int t = lane - P.off[2], i = t / S, j = t % S;
+    } else if (lane < L.off(3)) {  // RequestVote(i, j) :157-166 (no i /= j guard)
+        const int t = lane - L.off(2), i = t / S, j = t % S;
         const u64 wi = selw<S>(w, i);
         if (w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u)) {
             d.add = m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16);
             d.has_add = 1;
             d.en = 1;
         }
-    } else if (lane < P.off[4]) {  // BecomeLeader(i) :195-203
-        const int i = lane - P.off[3];
+    } else if (lane < L.off(4)) {  // BecomeLeader(i) :195-203
+        const int i = lane - L.off(3);
         const u64 wi = selw<S>(w, i);
         const u32 vg = w_vg<S>(wi);
         const bool ok = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
@@ -294,10 +308,10 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.w_new = wn;
             d.en = 1;
         }
-    } else if (lane < P.off[5]) {  // ClientRequest(i, v) :206-213
-        const int t = lane - P.off[4], i = t / P.V, v = t % P.V;
+    } else if (lane < L.off(5)) {  // ClientRequest(i, v) :206-213
+        const int t = lane - L.off(4), i = t / VMAX, v = t % VMAX;
         const u64 wi = selw<S>(w, i);
-        if (w_st(wi) == LEADER) {
+        if (v < P.V && w_st(wi) == LEADER) {
             const u32 len = w_len(wi);
             if (len >= (u32)LOG_CAP) {
                 d.w_new = wi | (1ull << 63);  // Len = 4: out of every allowed constraint
@@ -308,8 +322,8 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.srv = i;
             d.en = 1;
         }
-    } else if (lane < P.off[6]) {  // AdvanceCommitIndex(i) :219-236
-        const int i = lane - P.off[5];
+    } else if (lane < L.off(6)) {  // AdvanceCommitIndex(i) :219-236
+        const int i = lane - L.off(5);
         const u64 wi = selw<S>(w, i);
         if (w_st(wi) == LEADER) {
             const u32 len = w_len(wi);
@@ -326,8 +340,8 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.w_new = wn;
             d.en = 1;
         }
-    } else if (lane < P.off[7]) {  // AppendEntries(i, j) :171-192
-        const int t = lane - P.off[6], i = t / S, j = t % S;
+    } else if (lane < L.off(7)) {  // AppendEntries(i, j) :171-192
+        const int t = lane - L.off(6), i = t / S, j = t % S;
         const u64 wi = selw<S>(w, i);
         if (i != j && w_st(wi) == LEADER) {
             const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
@@ -342,12 +356,12 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.has_add = 1;
             d.en = 1;
         }
-    } else if (lane < P.off[8]) {  // Receive(m) :388-403
-        const int k = lane - P.off[7];
+    } else if (lane < L.off(8)) {  // Receive(m) :388-403
+        const int k = lane - L.off(7);
         const u32 sl = selm<K>(m, k);
         if (sl) receive_lane<S, K>(w, sl & MSG_MASK, k, d);
-    } else if (lane < P.off[9]) {  // DuplicateMessage(m) :410-412
-        const int k = lane - P.off[8];
+    } else if (lane < L.off(9)) {  // DuplicateMessage(m) :410-412
+        const int k = lane - L.off(8);
         const u32 sl = selm<K>(m, k);
         if (sl) {
             d.add = sl & MSG_MASK;
@@ -355,7 +369,7 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.en = 1;
         }
     } else {  // DropMessage(m) :415-417
-        const int k = lane - P.off[9];
+        const int k = lane - L.off(9);
         const u32 sl = selm<K>(m, k);
         if (sl) {
             d.rm = k;
@@ -501,14 +515,18 @@ RMC_HD int check_invariants(const u64 (&w)[S], const u32 (&m)[K], const Params& 
 }
 
 // ---- symmetry: server permutations -----------------------------------------------
-// perm p maps old server id -> new id.  A permuted word moves to position p[i].
+// A permutation p (old server id -> new id, S <= 4) is packed 2 bits per
+// entry into a u32 `code`, so applying it is shifts and masks: a small array
+// indexed by runtime ids would be forced out of registers.
+RMC_HD u32 pe(u32 code, u32 x) { return (code >> (2 * x)) & 3u; }
 template <int S>
-RMC_HD u64 perm_word(u64 w, const int* p) {
+RMC_HD u64 perm_word(u64 w, u32 code) {  // the word moves to position pe(code, i)
     u64 r = w & (0x3Full | (0x3ull << CI_SH) | (0x1FFFFull << LEN_SH));  // ct, st, ci, log
     const u32 vf = w_vf(w);
-    r |= (u64)(vf == NILV ? NILV : (u32)p[vf]) << VF_SH;
+    r |= (u64)(vf == NILV ? NILV : pe(code, vf)) << VF_SH;
+#pragma unroll
     for (int j = 0; j < S; ++j) {
-        const int pj = p[j];
+        const int pj = (int)pe(code, (u32)j);
         r |= ((w >> (SL<S>::VR + j)) & 1ull) << (SL<S>::VR + pj);
         r |= ((w >> (SL<S>::VG + j)) & 1ull) << (SL<S>::VG + pj);
         r |= ((w >> (SL<S>::NI + 2 * j)) & 3ull) << (SL<S>::NI + 2 * pj);
@@ -516,10 +534,9 @@ RMC_HD u64 perm_word(u64 w, const int* p) {
     }
     return r;
 }
-RMC_HD u32 perm_slot(u32 sl, const int* p) {
+RMC_HD u32 perm_slot(u32 sl, u32 code) {
     if (!sl) return 0;
-    const u32 src = m_src(sl), dst = m_dst(sl);
-    return (sl & ~(0xFCu)) | ((u32)p[src] << 2) | ((u32)p[dst] << 5);
+    return (sl & ~(0xFCu)) | (pe(code, m_src(sl)) << 2) | (pe(code, m_dst(sl)) << 5);
 }
 
 }  // namespace rmc

@@ -88,7 +88,7 @@ void fill_params(rmc_ctx* c) {
     P.inv_mask = (int)g.invariants;
     P.symmetry = c->sh.sym ? 1 : 0;
     const int S = c->sh.S, K = c->sh.K;
-    const int sizes[10] = {S, S, S * S, S, S * P.V, S, S * S, K, K, K};
+    const int sizes[10] = {S, S, S * S, S, S * VMAX, S, S * S, K, K, K};  // = Lanes<S,K>
     P.off[0] = 0;
     for (int f = 0; f < 10; ++f) P.off[f + 1] = P.off[f] + sizes[f];
     // permutations of 0..S-1 in lexicographic order (identity first)
@@ -97,7 +97,9 @@ void fill_params(rmc_ctx* c) {
         int a[4] = {0, 1, 2, 3};
         int n = 0;
         do {
-            for (int i = 0; i < 4; ++i) c->PT.p[n][i] = (int8_t)a[i];
+            u32 code = 0;
+            for (int i = 0; i < 4; ++i) code |= (u32)a[i] << (2 * i);
+            c->PT.code[n] = code;
             ++n;
         } while (std::next_permutation(a, a + S));
     }
@@ -445,6 +447,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                                                 " states); raise rmc_config.state_capacity");
         }
         c->res.generated += k.generated;
+        c->res.probes += k.probes;
         const u64 nnew = k.count - hi;
         if (nnew) {
             ++depth;
@@ -514,6 +517,44 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
         if (instances) instances[q] = a == 255 ? -1 : a;
     }
     return 0;
+}
+
+int rmc_probe_bench(int device, uint64_t table_bytes, uint64_t accesses, int mode, double* per_second) {
+    if (!per_second || table_bytes < 4096 || accesses == 0 || (mode != 0 && mode != 1)) return RMC_E_INVAL;
+    if (hipSetDevice(device) != hipSuccess) return RMC_E_NOGPU;
+    u64 slots = 1;
+    while (slots * 2 * 8 <= table_bytes) slots <<= 1;
+    u64* table = nullptr;
+    u64* sink = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = 0;
+    const u64 threads = 256ull * 2048;                       // 8 blocks of 256 per CU
+    const u32 iters = (u32)std::max<u64>(1, accesses / (threads * 8));
+    float ms = 0.f;
+    if (hipMalloc(&table, slots * 8) != hipSuccess || hipMalloc(&sink, 8) != hipSuccess) { rc = RMC_E_NOMEM; goto out; }
+    if (hipStreamCreate(&st) != hipSuccess || hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+        rc = RMC_E_HIP;
+        goto out;
+    }
+    if (hipMemsetAsync(table, 0, slots * 8, st) != hipSuccess) { rc = RMC_E_HIP; goto out; }
+    // warm-up launch (page mapping, clocks), then the timed one
+    if (launch_probe_bench(table, slots - 1, threads, 1, mode, sink, st) != hipSuccess) { rc = RMC_E_HIP; goto out; }
+    if (hipEventRecord(e0, st) != hipSuccess) { rc = RMC_E_HIP; goto out; }
+    if (launch_probe_bench(table, slots - 1, threads, iters, mode, sink, st) != hipSuccess) { rc = RMC_E_HIP; goto out; }
+    if (hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+        rc = RMC_E_HIP;
+        goto out;
+    }
+    *per_second = (double)threads * 8.0 * iters / (1e-3 * ms);
+out:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    (void)hipFree(table);
+    (void)hipFree(sink);
+    return rc;
 }
 
 int rmc_expand(rmc_ctx* c, const rmc_state_view* states, size_t n, rmc_succ_view* out, size_t cap, size_t* n_out) {

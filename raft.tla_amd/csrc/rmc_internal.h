@@ -15,6 +15,7 @@ struct Counters {
     u64 deadlock;   // min index of a state with no enabled lane, ~0 = none
     u32 overflow;   // state store full
     u32 table_full; // fingerprint set full
+    u64 probes;     // fingerprint-set probes issued by k_expand
 };
 
 struct DevBufs {
@@ -28,7 +29,7 @@ struct DevBufs {
 };
 
 struct PermTable {
-    int8_t p[24][4];  // server permutations (old id -> new id), S <= 4
+    u32 code[24];  // server permutations (old id -> new id), 2 bits per id, S <= 4
 };
 
 struct Shape {
@@ -40,5 +41,8 @@ struct Shape {
 //        2 = k_list of `a` states `in` into `out` (cap records, *count).
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
+
+// Random-probe microbenchmark over table[mask + 1] (mode 0 loads, 1 CAS).
+hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st);
 
 }  // namespace rmc

@@ -89,12 +89,10 @@ template <int S, int K, int NP>
 __device__ __forceinline__ void perm_fps(const u64 (&w)[S], const u32 (&m)[K], const PermTable& PT, u64 (&hp)[NP]) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-        int pm[S];
-#pragma unroll
-        for (int i = 0; i < S; ++i) pm[i] = PT.p[p][i];
+        const u32 pm = PT.code[p];
         u64 h = 0;
 #pragma unroll
-        for (int i = 0; i < S; ++i) h += hS(perm_word<S>(w[i], pm), (u32)pm[i]);
+        for (int i = 0; i < S; ++i) h += hS(perm_word<S>(w[i], pm), pe(pm, (u32)i));
 #pragma unroll
         for (int q = 0; q < K; ++q) h += hM(perm_slot(m[q], pm));
         hp[p] = h;
@@ -123,15 +121,11 @@ __device__ __forceinline__ u64 canon_key(const u64 (&w)[S], const u32 (&m)[K], c
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-        int pm[S];
-#pragma unroll
-        for (int i = 0; i < S; ++i) pm[i] = PT.p[p][i];
+        const u32 pm = PT.code[p];
         u64 h = hp[p];
         if (d.srv >= 0 && d.w_new != wo) {
-            int ps = pm[0];
-#pragma unroll
-            for (int i = 1; i < S; ++i) ps = (d.srv == i) ? pm[i] : ps;
-            h += hS(perm_word<S>(d.w_new, pm), (u32)ps) - hS(perm_word<S>(wo, pm), (u32)ps);
+            const u32 ps = pe(pm, (u32)d.srv);
+            h += hS(perm_word<S>(d.w_new, pm), ps) - hS(perm_word<S>(wo, pm), ps);
         }
         if (d.rm >= 0) h += hM(perm_slot(rm_new, pm)) - hM(perm_slot(rm_old, pm));
         if (d.has_add) h += hM(perm_slot(add_new, pm)) - hM(perm_slot(add_old, pm));
@@ -236,8 +230,9 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
     uint8_t* l_lane = s_lane[wv];
     u32 n = 0;  // wave-uniform list length
     u64 gen = 0;
+    u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
     const u64 nf = hi - lo;
-    const int nl = P.off[10];
+    const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
     for (u64 tile = (u64)blockIdx.x * 256ull; tile < nf; tile += (u64)gridDim.x * 256ull) {
         const u64 rel = tile + threadIdx.x;
         const bool live = rel < nf;
@@ -255,8 +250,8 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
         u64 hp[NP];
         if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
         u32 g = 0;
-        for (int lane0 = 0; lane0 < nl; lane0 += BATCH) {  // wave-uniform loop
-            // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe)
+        for (int lane0 = 0; lane0 < nl; lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
+            // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
             for (int b = 0; b < BATCH; ++b) {
                 const int lane = lane0 + b;
                 u64 key = 0;
@@ -281,6 +276,8 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                 key[b] = s_key[b][threadIdx.x];
                 cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
             }
+#pragma unroll
+            for (int b = 0; b < BATCH; ++b) pr += (u64)__popcll(__ballot(key[b] != 0));  // wave-uniform
             // (c) resolve: hit -> duplicate; empty -> CAS; mismatch -> slow path
             u32 newbits = 0, slowbits = 0;
 #pragma unroll
@@ -322,15 +319,41 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
         gen += g;
     }
     if (n) flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
-    // wave reduction of the generated count, one atomic per wave
+    // wave reductions of the generated and probe counts, one atomic each per wave
     u64 gs = gen;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const u32 lo32 = (u32)__shfl_xor((int)(u32)gs, off);
-        const u32 hi32 = (u32)__shfl_xor((int)(u32)(gs >> 32), off);
-        gs += ((u64)hi32 << 32) | lo32;
-    }
+    for (int off = 32; off > 0; off >>= 1)
+        gs += (u64)(u32)__shfl_xor((int)(u32)gs, off) | ((u64)(u32)__shfl_xor((int)(u32)(gs >> 32), off) << 32);
     if (me == 0 && gs) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)gs);
+    if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+}
+
+// Probe-rate microbenchmark (the roofline ceiling for k_expand): every thread
+// issues `iters` rounds of BATCH independent random 8-byte accesses into a
+// table of `mask + 1` slots — plain loads (mode 0) or CAS (mode 1) — the
+// access pattern of the fingerprint set, with no successor computation.
+template <int BATCH>
+__global__ __launch_bounds__(256) void k_probe_bench(u64* table, u64 mask, u32 iters, int mode, u64* sink) {
+    const u64 t = (u64)blockIdx.x * 256ull + threadIdx.x;
+    u64 acc = 0;
+    for (u32 it = 0; it < iters; ++it) {
+        u64 v[BATCH];
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+            const u64 key = mix64(t * 0x9E3779B97F4A7C15ull + (u64)it * BATCH + b) | 1ull;
+            if (mode == 0) v[b] = table[key & mask];
+            else v[b] = atomicCAS((unsigned long long*)&table[key & mask], 0ull, (unsigned long long)key);
+        }
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) acc ^= v[b];
+    }
+    if (acc == 0x5A5A5A5A5A5A5A5Aull) sink[0] = acc;  // keeps the loads live
+}
+
+hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st) {
+    hipLaunchKernelGGL((k_probe_bench<8>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, table, mask,
+                       iters, mode, sink);
+    return hipGetLastError();
 }
 
 // Insert n staged initial states (packed) into the set and the store.
@@ -384,7 +407,8 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
     const u64 h0 = state_fp<S, K>(w, m);
     u64 hp[NP];
     if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
-    const int nl = P.off[10];
+    const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
+#pragma unroll 1
     for (int lane = 0; lane < nl; ++lane) {
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);

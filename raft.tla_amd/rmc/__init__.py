@@ -40,7 +40,7 @@ class Result(C.Structure):
                 ("depth", C.c_int32), ("violated_inv", C.c_int32), ("violation_depth", C.c_int32),
                 ("deadlock", C.c_int32), ("collision_probability", C.c_double),
                 ("seconds", C.c_double), ("expand_kernel_seconds", C.c_double),
-                ("expand_launches", C.c_uint64)]
+                ("expand_launches", C.c_uint64), ("probes", C.c_uint64)]
 
 
 class LevelStats(C.Structure):
@@ -85,7 +85,7 @@ PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.POINTER(LevelStats), C.c_void_p)
 # Every symbol include/rmc.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_run_bfs",
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
-           "rmc_config_from_files")
+           "rmc_config_from_files", "rmc_probe_bench")
 
 _lib = None
 
@@ -120,6 +120,9 @@ def native():
         lib.rmc_config_from_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Config),
                                               C.c_char_p, C.c_size_t]
         lib.rmc_config_from_files.restype = C.c_int
+        lib.rmc_probe_bench.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int,
+                                        C.POINTER(C.c_double)]
+        lib.rmc_probe_bench.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -148,6 +151,16 @@ def config_from_files(cfg_path, tla_path=None):
     if rc:
         raise RmcError(rc, err.value.decode())
     return cfg
+
+
+def probe_bench(device=0, table_bytes=64 << 30, accesses=1 << 31, mode=0):
+    """Random 8-byte probe (mode 0) / CAS (mode 1) rate over a table of
+    table_bytes: the roofline ceiling R_max of the fingerprint set."""
+    rate = C.c_double()
+    rc = native().rmc_probe_bench(device, table_bytes, accesses, mode, C.byref(rate))
+    if rc:
+        raise RmcError(rc, "rmc_probe_bench failed")
+    return rate.value
 
 
 class Checker:
