@@ -2,8 +2,11 @@
 (BASELINE.json metric) on MI355X, one process per GPU.
 
 A "step" is one complete breadth-first search of the bounded MCraft model to
-its fixpoint (time-to-fixpoint); `value` = distinct states / seconds per step.
-The workload is deterministic: no random inputs exist for an exhaustive BFS.
+its fixpoint (time-to-fixpoint); `value` = distinct states / seconds per step,
+whole job.  The workload is deterministic: an exhaustive BFS has no input data.
+With N > 1 ranks the fingerprint space is sharded over the GPUs (rmc.dist:
+owner-routed successors, RCCL all-to-all per frontier chunk) and the SAME
+model is searched, so scaling is strong.
 """
 import argparse
 import json
@@ -27,8 +30,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBench.cfg"))
-    ap.add_argument("--capacity", type=int, default=1_500_000_000,
-                    help="state capacity per GPU (0 = auto from free HBM)")
+    ap.add_argument("--capacity", type=int, default=0,
+                    help="state capacity per GPU (0 = 1.5e9 / world * 1.3 for the bench model)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
+    ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK (one GPU per rank)")
+    ap.add_argument("--chunk", type=int, default=1 << 21, help="frontier states per exchange")
+    ap.add_argument("--cap-per-dest", type=int, default=1 << 23, help="outbox records per rank")
     ap.add_argument("--no-probe-ceiling", action="store_true",
                     help="skip the random-probe microbenchmark (roofline ceiling)")
     ap.add_argument("--cpu-levels", type=int, default=22,
@@ -52,6 +59,21 @@ def cpu_baseline(cfg, levels):
                       f"same model: {r.distinct} distinct / {r.generated} generated in {r.seconds:.2f} s"}
 
 
+def pmc_traffic(config_path):
+    """HBM bytes per k_expand launch from the committed rocprofv3 PMC profile
+    of this same command (profiles/<round>/pmc_traffic_<cfg>.json): PMC
+    counters cannot be read live inside the timed run."""
+    stem = os.path.splitext(os.path.basename(config_path))[0]
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None, None
+    for rnd in sorted(os.listdir(pdir), reverse=True):
+        pf = os.path.join(pdir, rnd, f"pmc_traffic_{stem}.json")
+        if os.path.exists(pf):
+            return json.load(open(pf))["hbm_bytes_per_launch"], os.path.relpath(pf, ROOT)
+    return None, None
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,47 +83,68 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dev = a.device if a.device >= 0 else local
+        torch.cuda.set_device(dev)
+        dist.init_process_group(a.dist_backend, init_method="env://")
     cfg = rmc.config_from_files(a.config)
-    cfg.device = local if world > 1 else 0
-    cfg.state_capacity = a.capacity
+    cfg.device = (a.device if a.device >= 0 else local) if world > 1 else max(a.device, 0)
+    cfg.state_capacity = a.capacity or int(1.5e9 / world * (1.3 if world > 1 else 1.0))
     W = rmc.native().rmc_state_bytes(cfg)
     # roofline ceiling of the fingerprint set: random 8-B probes over 64 GB
     r_max = None
-    if not a.no_probe_ceiling:
+    if not a.no_probe_ceiling and world == 1:
         r_max = rmc.probe_bench(device=cfg.device, table_bytes=64 << 30, accesses=1 << 32, mode=0)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    def one_run(ck, first):
+        if world == 1:
+            r = ck.run()
+            return r.distinct, r.generated, r.depth, r.probes, r.expand_kernel_seconds, r.expand_launches
+        from rmc import dist as rdist
+        k0 = ck.result().expand_kernel_seconds if not first else 0.0
+        l0 = ck.result().expand_launches if not first else 0
+        r = rdist.run(ck, chunk_states=a.chunk, cap_per_dest=a.cap_per_dest, sent_cache_slots=1 << 27,
+                      init=first)
+        cr = ck.result()
+        return (r.distinct, r.generated, r.depth, r.probes, cr.expand_kernel_seconds - k0,
+                cr.expand_launches - l0)
+
     with rmc.Checker(cfg) as ck:
+        first = True
         for _ in range(a.warmup):
-            ck.run()
+            one_run(ck, first)
+            first = False
         barrier()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         kern = 0.0
         launches = 0
         for _ in range(a.steps):
-            res = ck.run()
-            kern += res.expand_kernel_seconds
-            launches += res.expand_launches
+            D, G, depth, NP, ks, nl = one_run(ck, first)
+            first = False
+            kern += ks
+            launches += nl
         barrier()
         dt = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([dt], device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     per_step = dt / a.steps
-    G, D, NP = res.generated, res.distinct, res.probes
     # algorithmic bytes per run (DESIGN.md "Roofline"): one random 64-B granule
     # per fingerprint probe + the new state written, read back as frontier,
     # its 8-B parent pointer and 8-B fingerprint
     b_alg = NP * 64 + D * (2 * W + 16)
     ks = kern / a.steps
+    nlaunch = max(1, launches // a.steps)
     achieved = b_alg / ks / 1e9 if ks > 0 else 0.0
+    traffic, tsrc = pmc_traffic(a.config) if world == 1 else (None, None)
     out = {
         "metric": METRIC,
         "value": D / per_step,
@@ -119,23 +162,26 @@ def main():
             "workload": os.path.basename(a.config) + f": raft.tla, {cfg.n_servers} servers, "
                         f"{cfg.n_values} values, CONSTRAINT MaxTerm={cfg.max_term} MaxLogLen="
                         f"{cfg.max_log_len} MaxMsgs={cfg.max_msgs} MaxDup={cfg.max_dup}, BFS to fixpoint",
-            "distinct": D, "generated": G, "depth": res.depth,
+            "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
-            "parallelism": f"fp-sharded x{world}" if world > 1 else "single GPU",
+            "parallelism": f"fingerprint-sharded x{world} (RCCL all-to-all)" if world > 1 else "single GPU",
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "k_expand", "kernel_ms_per_step": kern / a.steps * 1e3,
-            "launches_per_step": launches // a.steps,
-            "alg_bytes_per_step": b_alg,
-            "probes_per_step": NP,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+            "kernel": "k_expand", "kernel_ms_per_step": ks * 1e3 if world == 1 else None,
+            "launches_per_step": nlaunch, "alg_bytes_per_launch": b_alg / nlaunch,
+            "alg_bytes_per_step": b_alg, "probes_per_step": NP,
             "probe_rate_per_s": NP / ks if ks > 0 else 0.0,
             "probe_ceiling_per_s": r_max,
             "frac_of_probe_ceiling": (NP / ks / r_max) if (ks > 0 and r_max) else None,
         },
     }
-    if rank == 0 and not a.no_cpu:
+    if world > 1:
+        out["roofline"]["note"] = "per-rank kernel time of rank 0; achieved is rank 0's share"
+        out["roofline"]["achieved"] = (b_alg / world) / ks / 1e9 if ks > 0 else 0.0
+        out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
+    if rank == 0 and not a.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_levels)
     if rank == 0:
         print(json.dumps(out), flush=True)

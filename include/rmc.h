@@ -88,7 +88,7 @@ typedef struct rmc_result {
     double seconds;            /* wall time of rmc_run_bfs                              */
     double expand_kernel_seconds; /* device time of the expansion kernels, HIP events on */
                                   /* the ctx stream (sum over levels)                    */
-    uint64_t expand_launches;  /* levels expanded (one timed launch group per level)    */
+    uint64_t expand_launches;  /* expansion kernel launches (levels are split in chunks) */
     uint64_t probes;           /* fingerprint-set probes (successors that reached the set) */
 } rmc_result;
 
@@ -184,6 +184,26 @@ int rmc_trace(rmc_ctx* ctx, rmc_state_view* states, int32_t* families, int32_t* 
 size_t rmc_state_bytes(const rmc_config* cfg);
 int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_view* out,
                size_t cap, size_t* n_out);
+
+/* ---- sharded BFS over several GPUs (one process per GPU) --------------------
+ * Replaces TLC's distributed mode (TLCServer/TLCWorker with a partitioned
+ * FPSet).  Fingerprints are owned by rank
+ * ((fp >> 32) * world) >> 32; each rank stores and expands the states it owns.
+ * Per level, every rank runs:
+ *   loop { rmc_dist_expand(chunk) -> per-destination record counts;
+ *          host all-to-all of counts and records (torch.distributed / RCCL);
+ *          rmc_dist_insert(received records) } until every rank's frontier is done;
+ *   rmc_dist_end_level -> local stats; host all-reduce; stop when no rank has new states.
+ * A record is rmc_dist_record_words() u32: the packed successor, its
+ * fingerprint, the global parent ref (rank << 48 | index) and the lane.
+ * The outbox is caller-owned device memory: [world][cap_per_dest][record]. */
+int rmc_dist_init(rmc_ctx* ctx, int32_t rank, int32_t world, uint64_t sent_cache_slots);
+size_t rmc_dist_record_words(const rmc_ctx* ctx);
+int rmc_dist_start(rmc_ctx* ctx);
+int rmc_dist_expand(rmc_ctx* ctx, uint64_t max_states, uint32_t* outbox, uint64_t cap_per_dest,
+                    uint64_t* send_counts, int32_t* frontier_done);
+int rmc_dist_insert(rmc_ctx* ctx, const uint32_t* inbox, uint64_t n_records);
+int rmc_dist_end_level(rmc_ctx* ctx, uint64_t* out5);
 
 /* ---- roofline microbenchmark -----------------------------------------------
  * Random 8-byte accesses into a table of table_bytes on `device`, 8 in flight

@@ -96,6 +96,11 @@ RMC_HD u64 mix64(u64 z) {
 RMC_HD u64 hS(u64 w, u32 i) { return mix64(w ^ ((u64)(i + 1) << 59)); }
 RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59)) : 0ull; }
 
+// Owner rank of a fingerprint in sharded mode: its top 32 bits scaled to
+// [0, world).  The fingerprint-set slot uses the low bits, so every shard's
+// table stays uniformly loaded.
+RMC_HD u32 owner_of(u64 key, u32 world) { return (u32)(((key >> 32) * (u64)world) >> 32); }
+
 // ---- model parameters (runtime part) --------------------------------------------
 struct Params {
     int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;

@@ -37,6 +37,12 @@ struct rmc_ctx {
     std::vector<u64> level_start;  // level d (1-based) = [level_start[d-1], level_start[d])
     int have_target = 0;           // a violation / deadlock state to trace
     u64 target_idx = 0;
+    // sharded mode (rmc_dist_*): one ctx per GPU process, exchange by the host driver
+    int dist = 0;
+    u64 sent_slots = 0;
+    u64* h_ocount = nullptr;  // pinned [world]
+    u64 cursor = 0;           // next unexpanded state of the current local frontier
+    int depth = 0;
 };
 
 namespace {
@@ -370,6 +376,9 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         return bail(RMC_E_NOMEM);
     }
     memset(c->h_ctr, 0, sizeof(Counters));
+    c->B.rank = 0;
+    c->B.world = 1;
+    c->B.ref_tag = 0;
     *out = c;
     return 0;
 }
@@ -383,6 +392,9 @@ void rmc_destroy(rmc_ctx* c) {
     (void)hipFree(c->B.table);
     (void)hipFree(c->B.ctr);
     (void)hipFree(c->d_staged);
+    (void)hipFree(c->B.sent);
+    (void)hipFree(c->B.ocount);
+    if (c->h_ocount) (void)hipHostFree(c->h_ocount);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -433,13 +445,13 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         for (u64 a = lo; a < hi; a += CHUNK) {
             const u64 b = std::min(hi, a + CHUNK);
             HIPCHK(c, launch(c->sh, 0, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
+            c->res.expand_launches += 1;
         }
         HIPCHK(c, hipEventRecord(c->ev1, c->st));
         if (int rc = read_counters(c)) return rc;
         float ms = 0.f;
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->res.expand_kernel_seconds += 1e-3 * ms;
-        c->res.expand_launches += 1;
         const Counters& k = *c->h_ctr;
         if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
         if (k.overflow) {
@@ -516,6 +528,125 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
         if (families) families[q] = family_of(c->P, a);
         if (instances) instances[q] = a == 255 ? -1 : a;
     }
+    return 0;
+}
+
+// ---- sharded BFS (one process per GPU; the host driver does the all-to-all) ----
+int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_slots) {
+    if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return RMC_E_INVAL;
+    if (c->sh.sym) return fail(c, RMC_E_INVAL, "sharded mode does not support SYMMETRY yet");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    u64 slots = 1;
+    while (slots < std::max<u64>(sent_cache_slots, 1024)) slots <<= 1;
+    (void)hipFree(c->B.sent);
+    (void)hipFree(c->B.ocount);
+    if (c->h_ocount) (void)hipHostFree(c->h_ocount);
+    c->B.sent = nullptr;
+    c->B.ocount = nullptr;
+    c->h_ocount = nullptr;
+    HIPCHK(c, hipMalloc(&c->B.sent, slots * 8));
+    HIPCHK(c, hipMalloc(&c->B.ocount, 64 * 8));
+    HIPCHK(c, hipHostMalloc(&c->h_ocount, 64 * 8, hipHostMallocDefault));
+    c->sent_slots = slots;
+    c->B.smask = slots - 1;
+    c->B.rank = (u32)rank;
+    c->B.world = (u32)world;
+    c->B.ref_tag = (u64)rank << 48;
+    c->dist = 1;
+    return 0;
+}
+
+size_t rmc_dist_record_words(const rmc_ctx* c) { return c ? (size_t)c->NW + 6 : 0; }
+
+int rmc_dist_start(rmc_ctx* c) {
+    if (!c || !c->dist) return RMC_E_STATE;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    c->res = rmc_result{};
+    c->level_start.clear();
+    c->have_target = 0;
+    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    HIPCHK(c, hipMemsetAsync(c->B.sent, 0, c->sent_slots * 8, c->st));
+    if (int rc = reset_counters(c, false)) return rc;
+    rmc_state_view iv;
+    init_view(c->cfg, &iv);
+    std::vector<u32> packed((size_t)c->NW);
+    std::string why;
+    if (encode_view(c, iv, packed.data(), &why)) return fail(c, RMC_E_INVAL, why);
+    HIPCHK(c, hipMemcpyAsync(c->d_staged, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
+    if (int rc = read_counters(c)) return rc;
+    c->res.generated = c->B.rank == 0 ? 1 : 0;  // the initial state is counted once, globally
+    c->level_start.push_back(0);
+    c->level_start.push_back(c->h_ctr->count);
+    c->cursor = 0;
+    c->depth = 1;
+    if (int rc = reset_counters(c, true)) return rc;
+    return 0;
+}
+
+int rmc_dist_expand(rmc_ctx* c, uint64_t max_states, uint32_t* outbox, uint64_t cap_per_dest, uint64_t* send_counts,
+                    int32_t* frontier_done) {
+    if (!c || !c->dist || !send_counts || !frontier_done || (!outbox && c->B.world > 1)) return RMC_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const u64 hi = c->level_start.back();
+    const u64 a = c->cursor, b = std::min<u64>(hi, a + std::max<u64>(max_states, 1));
+    for (u32 d = 0; d < c->B.world; ++d) send_counts[d] = 0;
+    if (a < b) {
+        c->B.outbox = outbox;
+        c->B.ocap = cap_per_dest;
+        HIPCHK(c, hipMemsetAsync(c->B.ocount, 0, 8 * c->B.world, c->st));
+        HIPCHK(c, hipEventRecord(c->ev0, c->st));
+        HIPCHK(c, launch(c->sh, 3, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
+        HIPCHK(c, hipEventRecord(c->ev1, c->st));
+        HIPCHK(c, hipMemcpyAsync(c->h_ocount, c->B.ocount, 8 * c->B.world, hipMemcpyDeviceToHost, c->st));
+        if (int rc = read_counters(c)) return rc;
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->res.expand_kernel_seconds += 1e-3 * ms;
+        c->res.expand_launches += 1;
+        if (c->h_ctr->overflow & 2u)
+            return fail(c, RMC_E_CAPACITY, "outbox full: lower max_states or raise cap_per_dest");
+        if (c->h_ctr->overflow) return fail(c, RMC_E_CAPACITY, "state store full");
+        if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
+        for (u32 d = 0; d < c->B.world; ++d) send_counts[d] = c->h_ocount[d];
+    }
+    c->cursor = b;
+    *frontier_done = b >= hi ? 1 : 0;
+    return 0;
+}
+
+int rmc_dist_insert(rmc_ctx* c, const uint32_t* inbox, uint64_t n_records) {
+    if (!c || !c->dist || (!inbox && n_records)) return RMC_E_INVAL;
+    if (n_records == 0) return 0;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, launch(c->sh, 4, c->P, c->PT, c->B, n_records, 0, inbox, nullptr, 0, nullptr, c->st));
+    if (int rc = read_counters(c)) return rc;
+    if (c->h_ctr->overflow) return fail(c, RMC_E_CAPACITY, "state store full");
+    if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
+    return 0;
+}
+
+// Closes the current level on this rank.  out[0..4] = new states stored here
+// (the next local frontier), successors generated here, probes, 1 + index of
+// a violating state (0 = none), violated invariant bit.
+int rmc_dist_end_level(rmc_ctx* c, uint64_t* out) {
+    if (!c || !c->dist || !out) return RMC_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (int rc = read_counters(c)) return rc;
+    const Counters k = *c->h_ctr;
+    const u64 hi = c->level_start.back();
+    out[0] = k.count - hi;
+    out[1] = k.generated;
+    out[2] = k.probes;
+    out[3] = k.viol != ~0ull ? (k.viol >> 2) + 1 : 0;
+    out[4] = k.viol != ~0ull ? (1ull << (k.viol & 3)) : 0;
+    c->res.generated += k.generated;
+    c->res.probes += k.probes;
+    c->res.distinct = k.count;  // states stored on this rank
+    c->level_start.push_back(k.count);
+    c->cursor = hi;
+    c->depth += 1;
+    if (int rc = reset_counters(c, true)) return rc;
     return 0;
 }
 

@@ -26,6 +26,14 @@ struct DevBufs {
     u64 tmask;       // slots - 1
     u64 cap;         // state store capacity
     Counters* ctr;
+    // sharded mode (rank/world > 1 GPU processes; single mode: rank 0, world 1)
+    u32 rank, world;
+    u64 ref_tag;               // (rank << 48): parent refs are global (rank, index)
+    u64* sent;                 // lossy cache of fingerprints already shipped to their owner
+    u64 smask;                 // sent-cache slots - 1
+    u32* outbox;               // [world][ocap][NW + 6] records, caller-owned
+    u64 ocap;                  // records per destination
+    unsigned long long* ocount;  // [world] records written per destination
 };
 
 struct PermTable {
@@ -38,7 +46,9 @@ struct Shape {
 };
 
 // which: 0 = k_expand over store[a, b); 1 = k_seed of `a` staged states `in`;
-//        2 = k_list of `a` states `in` into `out` (cap records, *count).
+//        2 = k_list of `a` states `in` into `out` (cap records, *count);
+//        3 = sharded k_expand over store[a, b) (outbox in B);
+//        4 = k_insert_remote of `a` received records `in`.
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 

@@ -205,7 +205,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         u32 mo[K];
         materialise<S, K>(w, m, d, wo, mo);
         store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
-        B.parent[ni] = lo + rel;
+        B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
@@ -213,21 +213,97 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
     wave_sync_lds();
 }
 
+template <int S, int K>
+__device__ __forceinline__ u64 fp_of_materialised(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
+    const u64 h = state_fp<S, K>(w, m);  // = the incremental key: the fp is order-free
+    return h ? h : 1ull;
+}
+
+// Sharded mode: the listed successors carry their owner rank.  Owned ones are
+// stored as above; the others are materialised into the outbox of their owner
+// as records {state, fingerprint, global parent ref, lane} (RecW words), for
+// the host driver's all-to-all.  Slots are reserved with one atomic per
+// destination per 64-entry round.
+template <int S, int K>
+__device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                           const uint8_t* l_lane, const uint8_t* l_dest, u32 n) {
+    constexpr int NW = 2 * S + K, RW = NW + 6;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    const u64 lt = (1ull << me) - 1ull;
+    for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
+        const u32 e = e0 + (u32)me;
+        const bool valid = e < n;
+        const u32 dest = valid ? l_dest[e] : 0xFFu;
+        u64 slot = ~0ull;
+        for (u32 dd = 0; dd < B.world; ++dd) {
+            const u64 bal = __ballot(valid && dest == dd);
+            if (!bal) continue;
+            const int leader = __ffsll((long long)bal) - 1;
+            u64 base = 0;
+            unsigned long long* ctr = dd == B.rank ? (unsigned long long*)&B.ctr->count : &B.ocount[dd];
+            if (me == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(bal));
+            base = bcast64(base, leader);
+            if (valid && dest == dd) slot = base + (u64)__popcll(bal & lt);
+        }
+        if (!valid) continue;
+        const u64 rel = l_rel[e];
+        const int lane = l_lane[e];
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, d, wo, mo);
+        if (dest == B.rank) {
+            if (slot >= B.cap) {
+                atomicOr(&B.ctr->overflow, 1u);
+                continue;
+            }
+            store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
+            B.parent[slot] = B.ref_tag | (lo + rel);
+            B.act[slot] = (uint8_t)lane;
+            const int v = check_invariants<S, K>(wo, mo, P);
+            if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 2) | (u64)(v - 1)));
+        } else {
+            if (slot >= B.ocap) {
+                atomicOr(&B.ctr->overflow, 2u);
+                continue;
+            }
+            u32* r = B.outbox + ((u64)dest * B.ocap + slot) * (u64)RW;
+            store_state<S, K>(r, wo, mo);
+            const u64 key = fp_of_materialised<S, K>(wo, mo, P);
+            const u64 ref = B.ref_tag | (lo + rel);
+            r[NW] = (u32)key; r[NW + 1] = (u32)(key >> 32);
+            r[NW + 2] = (u32)ref; r[NW + 3] = (u32)(ref >> 32);
+            r[NW + 4] = (u32)lane; r[NW + 5] = 0;
+        }
+    }
+    wave_sync_lds();
+}
+
 // Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
 // processed BATCH at a time so BATCH fingerprint probes per thread are in
 // flight together (the kernel is bound by probe latency, not bandwidth).
-template <int S, int K, bool SYM, int BATCH>
+// DIST: sharded mode — successors owned by another rank are looked up in the
+// local sent-cache instead of the set and, if not sent before, shipped
+// through the outbox (flush_dist).
+template <int S, int K, bool SYM, int BATCH, bool DIST>
 __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr int NP = SYM ? NPerm<S>::v : 1;
     __shared__ u32 s_rel[4][WCAP];
     __shared__ uint8_t s_lane[4][WCAP];
+    __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? WCAP : 1];
     __shared__ u64 s_key[BATCH][256];
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
     const u64 lt_mask = (1ull << me) - 1ull;
     u32* l_rel = s_rel[wv];
     uint8_t* l_lane = s_lane[wv];
+    uint8_t* l_dest = s_dest[DIST ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u64 gen = 0;
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
@@ -274,7 +350,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
                 key[b] = s_key[b][threadIdx.x];
-                cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
+                if constexpr (DIST) {
+                    const bool remote = key[b] && owner_of(key[b], B.world) != B.rank;
+                    cur[b] = !key[b] ? 0ull : remote ? B.sent[(key[b] >> 8) & B.smask] : B.table[key[b] & B.tmask];
+                } else {
+                    cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
+                }
             }
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) pr += (u64)__popcll(__ballot(key[b] != 0));  // wave-uniform
@@ -283,6 +364,13 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
                 if (!key[b] || cur[b] == key[b]) continue;
+                if constexpr (DIST) {
+                    if (owner_of(key[b], B.world) != B.rank) {  // not sent before (lossy cache): ship it
+                        B.sent[(key[b] >> 8) & B.smask] = key[b];
+                        newbits |= 1u << b;
+                        continue;
+                    }
+                }
                 if (cur[b] == 0) {
                     const u64 prev = atomicCAS((unsigned long long*)&B.table[key[b] & B.tmask], 0ull,
                                                (unsigned long long)key[b]);
@@ -306,10 +394,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
                         l_rel[pos] = (u32)rel;
                         l_lane[pos] = (uint8_t)(lane0 + b);
+                        if constexpr (DIST) l_dest[pos] = (uint8_t)owner_of(s_key[b][threadIdx.x], B.world);
                     }
                     n += (u32)__popcll(bal);
                     if (n > (u32)(WCAP - 64)) {
-                        flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
+                        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
+                        else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
                     }
                 }
@@ -318,13 +408,82 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
         if (live && g == 0) atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)(lo + rel));
         gen += g;
     }
-    if (n) flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
+    if (n) {
+        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
+        else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
+    }
     // wave reductions of the generated and probe counts, one atomic each per wave
     u64 gs = gen;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
         gs += (u64)(u32)__shfl_xor((int)(u32)gs, off) | ((u64)(u32)__shfl_xor((int)(u32)(gs >> 32), off) << 32);
     if (me == 0 && gs) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)gs);
+    if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+}
+
+// Sharded mode, owner side: insert the n records received from other ranks
+// (k_expand<DIST> outboxes after the all-to-all).  A winning record's state is
+// copied into the store with its global parent ref; same per-wave list and
+// single allocation atomic per flush as k_expand.
+template <int S, int K>
+__device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, const u32* inbox, const u32* l_idx,
+                                             u32 n) {
+    constexpr int NW = 2 * S + K, RW = NW + 6;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    u64 base = 0;
+    if (me == 0) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)n);
+    base = bcast64(base, 0);
+    for (u32 e = (u32)me; e < n; e += 64) {
+        const u64 ni = base + e;
+        if (ni >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
+        const u32* r = inbox + (u64)l_idx[e] * RW;
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(r, w, m);
+        store_state<S, K>(B.store + ni * (u64)NW, w, m);
+        B.parent[ni] = (u64)r[NW + 2] | ((u64)r[NW + 3] << 32);
+        B.act[ni] = (uint8_t)r[NW + 4];
+        const int v = check_invariants<S, K>(w, m, P);
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
+    }
+    wave_sync_lds();
+}
+
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_insert_remote(const Params P, const DevBufs B, const u32* inbox, u64 n) {
+    constexpr int NW = 2 * S + K, RW = NW + 6;
+    __shared__ u32 s_idx[4][WCAP];
+    const int wv = (int)(threadIdx.x >> 6);
+    const int me = (int)__lane_id();
+    const u64 lt = (1ull << me) - 1ull;
+    u32* l_idx = s_idx[wv];
+    u32 cnt = 0;
+    u64 pr = 0;
+    for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
+        const u64 t = t0 + threadIdx.x;
+        const bool live = t < n;
+        int is_new = 0;
+        if (live) {
+            const u32* r = inbox + t * (u64)RW;
+            const u64 key = (u64)r[NW] | ((u64)r[NW + 1] << 32);
+            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        }
+        pr += (u64)__popcll(__ballot(live));
+        const u64 bal = __ballot(is_new);
+        if (bal) {
+            if (is_new) l_idx[cnt + (u32)__popcll(bal & lt)] = (u32)t;
+            cnt += (u32)__popcll(bal);
+            if (cnt > (u32)(WCAP - 64)) {
+                flush_remote<S, K>(P, B, inbox, l_idx, cnt);
+                cnt = 0;
+            }
+        }
+    }
+    if (cnt) flush_remote<S, K>(P, B, inbox, l_idx, cnt);
     if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
 }
 
@@ -385,7 +544,8 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
             for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
         }
         key = key ? key : 1ull;
-        is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        // sharded mode: only the owner of an initial state stores it
+        if (owner_of(key, B.world) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
     }
     Delta d;  // identity delta: the state itself
     d.srv = -1; d.rm = -1; d.has_add = 0; d.add = 0; d.en = 1; d.w_new = 0;
@@ -443,29 +603,26 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
 // ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
 static const u64 kExpandGrid = 2048;
 
-// Probes in flight per thread (RMC_BATCH=4|8, default 8): a tuning knob.
-static int expand_batch() {
-    static int b = [] {
-        const char* e = getenv("RMC_BATCH");
-        return (e && atoi(e) == 4) ? 4 : 8;
-    }();
-    return b;
-}
+// Probes in flight per thread: 8 (measured best of 4/8 on MI355X).
+constexpr int kBatch = 8;
 
 template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                            const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-    const u64 n = which == 0 ? (b - a) : a;
+    const u64 n = (which == 0 || which == 3) ? (b - a) : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs
+    const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
     if (which == 0) {
-        // grid-stride: about 8 resident 256-thread blocks per CU x 256 CUs
-        const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
-        if (expand_batch() == 4)
-            hipLaunchKernelGGL((k_expand<S, K, SYM, 4>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-        else
-            hipLaunchKernelGGL((k_expand<S, K, SYM, 8>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+    } else if (which == 3) {
+        if constexpr (SYM) return hipErrorInvalidValue;  // sharded mode: no symmetry yet
+        else hipLaunchKernelGGL((k_expand<S, K, false, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+    } else if (which == 4) {
+        if constexpr (SYM) return hipErrorInvalidValue;
+        else hipLaunchKernelGGL((k_insert_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, in, a);
     } else if (which == 1) {
         hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
     } else {

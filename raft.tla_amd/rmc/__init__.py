@@ -85,7 +85,8 @@ PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.POINTER(LevelStats), C.c_void_p)
 # Every symbol include/rmc.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_run_bfs",
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
-           "rmc_config_from_files", "rmc_probe_bench")
+           "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
+           "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level")
 
 _lib = None
 
@@ -123,6 +124,19 @@ def native():
         lib.rmc_probe_bench.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int,
                                         C.POINTER(C.c_double)]
         lib.rmc_probe_bench.restype = C.c_int
+        lib.rmc_dist_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_uint64]
+        lib.rmc_dist_init.restype = C.c_int
+        lib.rmc_dist_record_words.argtypes = [C.c_void_p]
+        lib.rmc_dist_record_words.restype = C.c_size_t
+        lib.rmc_dist_start.argtypes = [C.c_void_p]
+        lib.rmc_dist_start.restype = C.c_int
+        lib.rmc_dist_expand.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
+        lib.rmc_dist_expand.restype = C.c_int
+        lib.rmc_dist_insert.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        lib.rmc_dist_insert.restype = C.c_int
+        lib.rmc_dist_end_level.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        lib.rmc_dist_end_level.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -202,6 +216,11 @@ class Checker:
         res = Result()
         self._check(self.lib.rmc_get_result(self.ctx, C.byref(res)))
         self.levels = levels
+        return res
+
+    def result(self) -> Result:
+        res = Result()
+        self._check(self.lib.rmc_get_result(self.ctx, C.byref(res)))
         return res
 
     def trace(self):

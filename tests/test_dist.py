@@ -1,0 +1,74 @@
+"""Sharded multi-rank BFS: N ranks must reproduce the single-GPU / oracle
+counts exactly ("run N shards as N ranks on one GPU and
+require counts identical to N=1").
+
+The GPU tests run 2 and 4 ranks sharing the box's one GPU over gloo; the
+8-GPU RCCL run is the driver's scaling bench.  The CPU test exercises the
+host-side exchange protocol (rmc.dist.exchange) with world size 2 on gloo."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))
+
+
+def _torchrun(nproc, args, port):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+
+
+EXCHANGE_WORKER = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.path.join(sys.argv[1], 'raft.tla_amd'))
+from rmc.dist import exchange
+dist.init_process_group('gloo', init_method='env://')
+r, w = dist.get_rank(), dist.get_world_size()
+cap, rw = 8, 3
+ob = torch.zeros((w, cap, rw), dtype=torch.int32)
+send = [(r + d) % 3 for d in range(w)]
+for d in range(w):
+    for k in range(send[d]):
+        ob[d, k] = torch.tensor([r, d, k])
+out, rc = exchange(ob, send)
+row = 0
+for s in range(w):
+    assert rc[s] == (s + r) % 3, (rc, s, r)
+    for k in range(rc[s]):
+        assert out[row].tolist() == [s, r, k]
+        row += 1
+assert row == out.shape[0]
+dist.destroy_process_group()
+"""
+
+
+def test_exchange_protocol_gloo_world2(tmp_path):
+    script = tmp_path / "xw.py"
+    script.write_text(EXCHANGE_WORKER)
+    r = _torchrun(2, [str(script), ROOT], 29611)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,nproc", [("tiny2_v2", 2), ("small", 2), ("small", 4),
+                                        ("s5_prefix9", 2)])
+def test_sharded_bfs_matches_oracle(case, nproc, tmp_path):
+    g = GOLDEN[case]
+    if g["params"]["max_depth"]:
+        pytest.skip("sharded runs go to fixpoint")
+    out = tmp_path / "r.json"
+    r = _torchrun(nproc, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out",
+                          str(out), "--device", "0", "--backend", "gloo"], 29620 + nproc)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert res["distinct"] == g["distinct"]
+    assert res["generated"] == g["generated"]
+    assert res["depth"] == g["depth"]
+    assert [1] + [x for x in res["levels"] if x] == g["level_new"]
+    assert res["rerun"] == [g["distinct"], g["generated"], g["depth"]]
+    assert res["records_sent"] > 0
