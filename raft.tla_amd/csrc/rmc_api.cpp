@@ -493,7 +493,8 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.distinct = c->level_start.back();
     c->res.depth = depth;
     const double D = (double)c->res.distinct, G = (double)c->res.generated;
-    c->res.collision_probability = D * G / 18446744073709551616.0;
+    // TLC's "calculated (optimistic)" fingerprint-collision estimate
+    c->res.collision_probability = D * (G - D) / 18446744073709551616.0;
     c->res.seconds = secs();
     return 0;
 }
