@@ -553,6 +553,8 @@ int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_s
     c->B.rank = (u32)rank;
     c->B.world = (u32)world;
     c->B.ref_tag = (u64)rank << 48;
+    const char* om = getenv("RMC_OWNER");  // partition: 0 fingerprint, 1 server-0 word, 2 servers 0+1
+    c->B.owner_mode = om ? (u32)std::min(2, std::max(0, atoi(om))) : 1u;
     c->dist = 1;
     return 0;
 }

@@ -28,6 +28,7 @@ struct DevBufs {
     Counters* ctr;
     // sharded mode (rank/world > 1 GPU processes; single mode: rank 0, world 1)
     u32 rank, world;
+    u32 owner_mode;            // 0: owner by fingerprint, 1: by server 0's word
     u64 ref_tag;               // (rank << 48): parent refs are global (rank, index)
     u64* sent;                 // lossy cache of fingerprints already shipped to their owner
     u64 smask;                 // sent-cache slots - 1

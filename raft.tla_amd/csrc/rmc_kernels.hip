@@ -213,6 +213,18 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
     wave_sync_lds();
 }
 
+// Owner rank of a state in sharded mode.  Mode 0: by fingerprint.  Mode 1: by
+// server 0's word — a successor that does not touch server 0 (bag-only
+// actions, actions of the other servers) stays on its parent's rank, so far
+// fewer successors cross GPUs; balance relies on server 0's many word values.
+// Mode 2: by the words of servers 0 and 1 (more distinct values: better
+// balance, successors of two servers cross).
+__device__ __forceinline__ u32 owner_state(u64 key, u64 w0, u64 w1, const DevBufs& B) {
+    if (B.owner_mode == 1) return owner_of(mix64(w0 ^ 0x6a09e667f3bcc909ull), B.world);
+    if (B.owner_mode == 2) return owner_of(mix64(w0 ^ 0x6a09e667f3bcc909ull) + mix64(w1 ^ 0xbb67ae8584caa73bull), B.world);
+    return owner_of(key, B.world);
+}
+
 template <int S, int K>
 __device__ __forceinline__ u64 fp_of_materialised(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
     const u64 h = state_fp<S, K>(w, m);  // = the incremental key: the fp is order-free
@@ -298,6 +310,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
     __shared__ uint8_t s_lane[4][WCAP];
     __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? WCAP : 1];
     __shared__ u64 s_key[BATCH][256];
+    __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
     const u64 lt_mask = (1ull << me) - 1ull;
@@ -341,6 +354,9 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                         key = h;
                         if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
                         key = key ? key : 1ull;
+                        if constexpr (DIST)
+                            s_own[b][threadIdx.x] = (uint8_t)owner_state(key, d.srv == 0 ? d.w_new : w[0],
+                                                                         d.srv == 1 ? d.w_new : w[1], B);
                     }
                 }
                 s_key[b][threadIdx.x] = key;
@@ -351,7 +367,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
             for (int b = 0; b < BATCH; ++b) {
                 key[b] = s_key[b][threadIdx.x];
                 if constexpr (DIST) {
-                    const bool remote = key[b] && owner_of(key[b], B.world) != B.rank;
+                    const bool remote = key[b] && s_own[b][threadIdx.x] != B.rank;
                     cur[b] = !key[b] ? 0ull : remote ? B.sent[(key[b] >> 8) & B.smask] : B.table[key[b] & B.tmask];
                 } else {
                     cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
@@ -365,7 +381,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
             for (int b = 0; b < BATCH; ++b) {
                 if (!key[b] || cur[b] == key[b]) continue;
                 if constexpr (DIST) {
-                    if (owner_of(key[b], B.world) != B.rank) {  // not sent before (lossy cache): ship it
+                    if (s_own[b][threadIdx.x] != B.rank) {  // not sent before (lossy cache): ship it
                         B.sent[(key[b] >> 8) & B.smask] = key[b];
                         newbits |= 1u << b;
                         continue;
@@ -394,7 +410,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
                         l_rel[pos] = (u32)rel;
                         l_lane[pos] = (uint8_t)(lane0 + b);
-                        if constexpr (DIST) l_dest[pos] = (uint8_t)owner_of(s_key[b][threadIdx.x], B.world);
+                        if constexpr (DIST) l_dest[pos] = s_own[b][threadIdx.x];
                     }
                     n += (u32)__popcll(bal);
                     if (n > (u32)(WCAP - 64)) {
@@ -545,7 +561,7 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
         }
         key = key ? key : 1ull;
         // sharded mode: only the owner of an initial state stores it
-        if (owner_of(key, B.world) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        if (owner_state(key, w[0], w[1], B) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
     }
     Delta d;  // identity delta: the state itself
     d.srv = -1; d.rm = -1; d.has_add = 0; d.add = 0; d.en = 1; d.w_new = 0;

@@ -1,12 +1,15 @@
-"""One rank of a sharded BFS (launched by tests/test_dist.py via torchrun).
+"""One rank of a sharded BFS (launched by tests/test_dist.py or by hand via
+torchrun).
 
 Every rank uses GPU `--device` (several ranks may share one GPU with the gloo
-backend), runs rmc.dist.run on a golden config and rank 0 writes the global
-result as JSON."""
+backend), runs rmc.dist.run on a golden config (`--case`) or a TLC model
+(`--cfg`), and rank 0 writes the global result plus per-rank balance stats as
+JSON."""
 import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -20,29 +23,50 @@ from rmc import dist as rdist  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--case", required=True)
+    ap.add_argument("--case")
+    ap.add_argument("--cfg")
     ap.add_argument("--out", required=True)
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK")
     ap.add_argument("--chunk", type=int, default=1 << 16)
+    ap.add_argument("--cap-per-dest", type=int, default=1 << 20)
+    ap.add_argument("--capacity", type=int, default=0)
+    ap.add_argument("--rerun", type=int, default=1)
     args = ap.parse_args()
-    g = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))[args.case]
-    p = g["params"]
     dist.init_process_group(args.backend, init_method="env://")
-    rank = dist.get_rank()
+    rank, world = dist.get_rank(), dist.get_world_size()
     dev = args.device if args.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
-    cfg = rmc.make_config(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
-                          max_log_len=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
-                          bug_quorum=bool(p["bug_quorum"]), invariants=p["invariants"],
-                          device=dev, state_capacity=max(1 << 20, g["distinct"]))
+    if args.case:
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))[args.case]
+        p = g["params"]
+        cfg = rmc.make_config(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                              max_log_len=p["max_log_len"], max_msgs=p["max_msgs"],
+                              max_dup=p["max_dup"], bug_quorum=bool(p["bug_quorum"]),
+                              invariants=p["invariants"], device=dev,
+                              state_capacity=args.capacity or max(1 << 20, g["distinct"]))
+    else:
+        cfg = rmc.config_from_files(args.cfg)
+        cfg.device = dev
+        cfg.state_capacity = args.capacity or (1 << 26)
     with rmc.Checker(cfg) as ck:
-        r = rdist.run(ck, chunk_states=args.chunk, cap_per_dest=1 << 20, sent_cache_slots=1 << 20)
-        r2 = rdist.run(ck, chunk_states=args.chunk, cap_per_dest=1 << 20, init=False)  # re-run
+        t0 = time.time()
+        r = rdist.run(ck, chunk_states=args.chunk, cap_per_dest=args.cap_per_dest,
+                      sent_cache_slots=1 << 24)
+        wall = time.time() - t0
+        local = ck.result()
+        reruns = [rdist.run(ck, chunk_states=args.chunk, cap_per_dest=args.cap_per_dest, init=False)
+                  for _ in range(args.rerun)]
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, dict(rank=rank, distinct=local.distinct,
+                                          records_sent=r.records_sent))
     if rank == 0:
         json.dump(dict(distinct=r.distinct, generated=r.generated, depth=r.depth,
                        levels=r.levels, violated_inv=r.violated_inv,
                        violation_depth=r.violation_depth, records_sent=r.records_sent,
-                       rerun=[r2.distinct, r2.generated, r2.depth]), open(args.out, "w"))
+                       per_rank=per_rank, wall_s=wall,
+                       owner_mode=os.environ.get("RMC_OWNER", "1"),
+                       rerun=[[x.distinct, x.generated, x.depth] for x in reruns]),
+                  open(args.out, "w"))
     dist.destroy_process_group()
 
 

@@ -70,5 +70,6 @@ def test_sharded_bfs_matches_oracle(case, nproc, tmp_path):
     assert res["generated"] == g["generated"]
     assert res["depth"] == g["depth"]
     assert [1] + [x for x in res["levels"] if x] == g["level_new"]
-    assert res["rerun"] == [g["distinct"], g["generated"], g["depth"]]
+    assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
     assert res["records_sent"] > 0
+    assert sum(p["distinct"] for p in res["per_rank"]) == g["distinct"]
