@@ -131,6 +131,14 @@ def main():
             launches += nl
         barrier()
         dt = time.perf_counter() - t0
+        salt_check = None
+        if world == 1:  # untimed: same search under another fingerprint salt
+            ck.set_seed(0x5A17ED)
+            r2 = ck.run()
+            ck.set_seed(0)
+            salt_check = {"salt": 0x5A17ED, "distinct": r2.distinct, "generated": r2.generated,
+                          "depth": r2.depth,
+                          "agrees": (r2.distinct, r2.generated, r2.depth) == (D, G, depth)}
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
@@ -165,6 +173,7 @@ def main():
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
             "parallelism": f"fingerprint-sharded x{world} (RCCL all-to-all)" if world > 1 else "single GPU",
+            "fp_salt_crosscheck": salt_check,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

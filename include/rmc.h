@@ -70,7 +70,9 @@ typedef struct rmc_config {
     int32_t device;           /* HIP device ordinal                               */
     int32_t max_depth;        /* 0 = unbounded; else stop after this many levels  */
     uint64_t state_capacity;  /* distinct states this GPU may store; 0 = auto     */
-    uint64_t seed;            /* simulation seed (unused by BFS)                  */
+    uint64_t seed;            /* BFS: fingerprint salt (0 = default hash; two runs */
+                              /* with different salts and equal counts rule out   */
+                              /* fingerprint collisions); simulation: RNG seed     */
 } rmc_config;
 
 /* End-of-run summary.  Replaces TLC's stdout summary lines:
@@ -166,6 +168,8 @@ const char* rmc_version(void);                    /* "rmc <abi> gfx950 ..."     
  * enqueue).  Blocks until fixpoint, first violation, deadlock (when checked),
  * max_depth, or the callback asks to stop. */
 int rmc_run_bfs(rmc_ctx* ctx, rmc_progress_fn cb, void* user);
+/* Changes rmc_config.seed (fingerprint salt) for the next run on this ctx. */
+int rmc_set_seed(rmc_ctx* ctx, uint64_t seed);
 int rmc_get_result(const rmc_ctx* ctx, rmc_result* out);
 
 /* Counterexample: the states from an initial state to the violating (or
@@ -184,6 +188,37 @@ int rmc_trace(rmc_ctx* ctx, rmc_state_view* states, int32_t* families, int32_t* 
 size_t rmc_state_bytes(const rmc_config* cfg);
 int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_view* out,
                size_t cap, size_t* n_out);
+
+/* ---- simulation (TLC -simulate; Smokeraft.cfg, config 4) ---------------------
+ * Replaces TLC's Simulator: random behaviours, each from a random initial state
+ * and then a uniformly random enabled successor per step, invariants checked on
+ * every state.  smoke_k > 0 draws the initial states like SmokeInit
+ * (Smokeraft.tla:64-76: one RandomSubset(k, .) per variable, k^9 states, over
+ * SmokeNat = 0..smoke_nat, SmokeInt = -1..1, BoundedSeq(.,3)/(.,1) logs);
+ * smoke_k = 0 starts from Init.  TLC's StopAfter (a 1-s budget,
+ * Smokeraft.tla:88-92) is replaced by an explicit behaviour count.  A step
+ * whose chosen successor exceeds the packed capacity ends that behaviour and is
+ * counted in `truncated`. */
+typedef struct rmc_sim_config {
+    uint64_t behaviours;       /* random behaviours to run                        */
+    int32_t depth;             /* states per behaviour (TLC -depth, default 100)  */
+    int32_t smoke_k;           /* SmokeInit RandomSubset size k; 0 = Init         */
+    int32_t smoke_nat;         /* SmokeNat = 0..smoke_nat (default 2)             */
+    int32_t pad;
+    uint64_t seed;             /* RNG seed for the SmokeInit draws and the walks  */
+} rmc_sim_config;
+typedef struct rmc_sim_result {
+    uint64_t behaviours, steps, init_states, truncated, deadlocked;
+    int32_t violated_inv;      /* RMC_INV_* bit of the first violation, or 0      */
+    int32_t violation_depth;   /* its state index in the behaviour (1 = initial)  */
+    uint64_t violation_behaviour;
+    double seconds;            /* wall time incl. the SmokeInit draw              */
+    double kernel_seconds;     /* device time of the walks (HIP events)           */
+} rmc_sim_result;
+int rmc_simulate(rmc_ctx* ctx, const rmc_sim_config* sc, rmc_sim_result* out);
+/* Re-runs behaviour `behaviour` of the same rmc_sim_config and returns its states. */
+int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, rmc_state_view* states,
+                   size_t cap, size_t* len);
 
 /* ---- sharded BFS over several GPUs (one process per GPU) --------------------
  * Replaces TLC's distributed mode (TLCServer/TLCWorker with a partitioned

@@ -69,7 +69,8 @@ template <int S> RMC_HD u32 w_mi(u64 w, u32 j) { return bits(w, SL<S>::MI + 2 * 
 //  bits 0-1 mtype, 2-4 msource, 5-7 mdest, 8-11 mterm, 12-29 body, 30-31 count (1..3)
 //  RVQ body: mlastLogTerm 12-15, mlastLogIndex 16-17
 //  RVP body: mvoteGranted 12, mlog 13-29 (= server-word bits 11-27: len + entries)
-//  AEQ body: mprevLogIndex 12-13, mprevLogTerm 14-17, Len(mentries) 18, entry 19-23, mcommitIndex 24-25
+//  AEQ body: mprevLogIndex+1 12-14 (Smokeraft's -1 included), mprevLogTerm 15-18, Len(mentries) 19,
+//            entry 20-24, mcommitIndex 25-26
 //  AEP body: msuccess 12, mmatchIndex 13-14
 // An empty slot is 0 (a live slot has count >= 1).  Canonical bags are sorted
 // descending by slot value, so empty slots come last.
@@ -93,8 +94,20 @@ RMC_HD u64 mix64(u64 z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
-RMC_HD u64 hS(u64 w, u32 i) { return mix64(w ^ ((u64)(i + 1) << 59)); }
-RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59)) : 0ull; }
+// Fingerprint salt (rmc_config.seed): XORed into the low 59 bits of every mix
+// input, it selects another member of the hash family, so two BFS runs with
+// different seeds that report the same counts rule out fingerprint
+// collisions in practice.  Device copy set per run (set_fp_salt); 0 = default.
+#if defined(__HIPCC__)
+static __constant__ u64 c_fp_salt;  // visible to both passes (HIP_SYMBOL needs the host shadow)
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RMC_FP_SALT c_fp_salt
+#else
+#define RMC_FP_SALT 0ull
+#endif
+RMC_HD u64 hS(u64 w, u32 i) { return mix64(w ^ ((u64)(i + 1) << 59) ^ RMC_FP_SALT); }
+RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59) ^ RMC_FP_SALT) : 0ull; }
 
 // Owner rank of a fingerprint in sharded mode: its top 32 bits scaled to
 // [0, world).  The fingerprint-set slot uses the low bits, so every shard's
@@ -191,9 +204,11 @@ RMC_HD void receive_lane(const u64 (&w)[S], u32 msg, int k, Delta& d) {
         return;
     }
     if (mt == AEQ) {  // HandleAppendEntriesRequest :347-356 (mterm <= ct here)
-        const u32 pidx = (msg >> 12) & 3u, pterm = (msg >> 14) & 15u;
-        const u32 nent = (msg >> 18) & 1u, ent = (msg >> 19) & 31u, mci = (msg >> 24) & 3u;
-        const bool log_ok = pidx == 0 || (pidx <= len && pterm == ent_term(w_ent(wi, pidx - 1)));
+        const u32 pe = (msg >> 12) & 7u, pterm = (msg >> 15) & 15u;  // pe = mprevLogIndex + 1
+        const u32 nent = (msg >> 19) & 1u, ent = (msg >> 20) & 31u, mci = (msg >> 25) & 3u;
+        const u32 pidx = pe - 1u;  // only read when pe >= 1 (mprevLogIndex >= 0)
+        // mprevLogIndex = -1 (Smokeraft.tla:35) fails both disjuncts of logOk
+        const bool log_ok = pe == 1u || (pe > 1u && pidx <= len && pterm == ent_term(w_ent(wi, pidx - 1)));
         if (mterm < ct || (st == FOLLOWER && !log_ok)) {  // Reject :281-293
             d.add = m_hdr(AEP, i, j, ct);  // msuccess FALSE, mmatchIndex 0
             d.has_add = 1;
@@ -356,8 +371,8 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             const u32 nent = ni <= last ? 1u : 0u; // SubSeq(log[i], ni, last): 0 or 1 entry
             const u32 ent = nent ? w_ent(wi, ni - 1) : 0u;
             const u32 ci = w_ci(wi), mci = ci < last ? ci : last;
-            d.add = m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | (prev << 12) | (pterm << 14) | (nent << 18) |
-                    (ent << 19) | (mci << 24);
+            d.add = m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | ((prev + 1u) << 12) | (pterm << 15) | (nent << 19) |
+                    (ent << 20) | (mci << 25);
             d.has_add = 1;
             d.en = 1;
         }

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -178,7 +179,7 @@ int encode_view(const rmc_ctx* c, const rmc_state_view& v, u32* out, std::string
                 break;
             }
             case AEQ: {
-                if (m.mprevLogIndex < 0 || m.mprevLogIndex > 3 || m.mprevLogTerm < 0 || m.mprevLogTerm > 15 ||
+                if (m.mprevLogIndex < -1 || m.mprevLogIndex > 3 || m.mprevLogTerm < 0 || m.mprevLogTerm > 15 ||
                     m.mentries_len < 0 || m.mentries_len > 1 || m.mcommitIndex < 0 || m.mcommitIndex > 3)
                     return bad("AppendEntriesRequest field out of packed range");
                 u32 e = 0;
@@ -188,8 +189,8 @@ int encode_view(const rmc_ctx* c, const rmc_state_view& v, u32* out, std::string
                         return bad("mentries entry out of range");
                     e = (u32)(m.mentries[0].term | (m.mentries[0].value << 4));
                 }
-                s |= ((u32)m.mprevLogIndex << 12) | ((u32)m.mprevLogTerm << 14) | ((u32)m.mentries_len << 18) |
-                     (e << 19) | ((u32)m.mcommitIndex << 24);
+                s |= ((u32)(m.mprevLogIndex + 1) << 12) | ((u32)m.mprevLogTerm << 15) |
+                     ((u32)m.mentries_len << 19) | (e << 20) | ((u32)m.mcommitIndex << 25);
                 break;
             }
             default:
@@ -255,15 +256,15 @@ void decode_state(const rmc_ctx* c, const u32* in, rmc_state_view* v) {
                 break;
             }
             case AEQ: {
-                m.mprevLogIndex = (int)((s >> 12) & 3u);
-                m.mprevLogTerm = (int)((s >> 14) & 15u);
-                m.mentries_len = (int)((s >> 18) & 1u);
-                const u32 e = (s >> 19) & 31u;
+                m.mprevLogIndex = (int)((s >> 12) & 7u) - 1;
+                m.mprevLogTerm = (int)((s >> 15) & 15u);
+                m.mentries_len = (int)((s >> 19) & 1u);
+                const u32 e = (s >> 20) & 31u;
                 if (m.mentries_len) {
                     m.mentries[0].term = (int)(e & 15u);
                     m.mentries[0].value = (int)(e >> 4);
                 }
-                m.mcommitIndex = (int)((s >> 24) & 3u);
+                m.mcommitIndex = (int)((s >> 25) & 3u);
                 break;
             }
             default:
@@ -411,6 +412,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->level_start.clear();
     c->have_target = 0;
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     if (int rc = reset_counters(c, false)) return rc;
 
     // ---- Init (raft.tla:125-129): one initial state
@@ -499,6 +501,12 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     return 0;
 }
 
+int rmc_set_seed(rmc_ctx* c, uint64_t seed) {
+    if (!c) return RMC_E_INVAL;
+    c->cfg.seed = seed;
+    return 0;
+}
+
 int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
     if (!c || !out) return RMC_E_INVAL;
     *out = c->res;
@@ -529,6 +537,227 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
         if (families) families[q] = family_of(c->P, a);
         if (instances) instances[q] = a == 255 ? -1 : a;
     }
+    return 0;
+}
+
+}  // extern "C"
+
+// ---- simulation: SmokeInit sampler (Smokeraft.tla:4-76) and random walks -------
+namespace {
+
+// RandomSubset(k, X): k distinct random elements of X, X given by a sampler.
+template <class T, class F>
+std::vector<T> random_subset(int k, F draw, std::mt19937_64& g) {
+    std::vector<T> out;
+    for (int guard = 0; (int)out.size() < k && guard < 100000; ++guard) {
+        T x = draw(g);
+        if (std::find(out.begin(), out.end(), x) == out.end()) out.push_back(x);
+    }
+    return out;
+}
+
+struct SmokeDomains {
+    int S, V, nat;
+    int uni(std::mt19937_64& g, int lo, int hi) const {  // uniform in lo..hi
+        return lo + (int)(g() % (u64)(hi - lo + 1));
+    }
+    // BoundedSeq([term : SmokeNat, value : Value], n) (Smokeraft.tla:4-6): uniform over
+    // the whole set of sequences of length 0..n; encoded as (len, e0, e1, ...).
+    std::vector<int> seq(std::mt19937_64& g, int n) const {
+        const u64 E = (u64)(nat + 1) * (u64)V;
+        u64 total = 0, p = 1;
+        for (int m = 0; m <= n; ++m, p *= E) total += p;
+        u64 r = g() % total;
+        int len = 0;
+        p = 1;
+        while (r >= p) { r -= p; p *= E; ++len; }
+        std::vector<int> s{len};
+        for (int x = 0; x < len; ++x) {
+            const u64 e = r % E;
+            r /= E;
+            s.push_back((int)(e / (u64)V));  // term
+            s.push_back((int)(e % (u64)V));  // value
+        }
+        return s;
+    }
+};
+
+// One message of SmokeMessageType (Smokeraft.tla:24-62) as a canonical int vector.
+std::vector<int> smoke_msg(const SmokeDomains& D, int type, std::mt19937_64& g) {
+    std::vector<int> v{type, D.uni(g, 0, D.nat), D.uni(g, 0, D.S - 1), D.uni(g, 0, D.S - 1)};
+    if (type == RVQ) { v.push_back(D.uni(g, 0, D.nat)); v.push_back(D.uni(g, 0, D.nat)); }
+    if (type == AEQ) {
+        v.push_back(D.uni(g, -1, 1));              // mprevLogIndex \in SmokeInt
+        v.push_back(D.uni(g, 0, D.nat));           // mprevLogTerm
+        const auto e = D.seq(g, 1);                // mentries \in SmokeSeq(...)
+        v.insert(v.end(), e.begin(), e.end());
+        v.push_back(D.uni(g, 0, D.nat));           // mcommitIndex
+    }
+    if (type == RVP) {
+        v.push_back(D.uni(g, 0, 1));               // mvoteGranted \in BOOLEAN
+        const auto e = D.seq(g, 1);                // mlog \in SmokeSeq(...)
+        v.insert(v.end(), e.begin(), e.end());
+    }
+    if (type == AEP) { v.push_back(D.uni(g, 0, 1)); v.push_back(D.uni(g, 0, D.nat)); }
+    return v;
+}
+
+void msg_to_view(const std::vector<int>& v, rmc_msg_view* m) {
+    memset(m, 0, sizeof *m);
+    m->mtype = v[0];
+    m->mterm = v[1];
+    m->msource = v[2];
+    m->mdest = v[3];
+    m->count = 1;
+    size_t p = 4;
+    auto seq = [&](rmc_entry* out, int32_t* len) {
+        *len = v[p++];
+        for (int x = 0; x < *len; ++x) { out[x].term = v[p++]; out[x].value = v[p++]; }
+    };
+    if (v[0] == RVQ) { m->mlastLogTerm = v[p++]; m->mlastLogIndex = v[p++]; }
+    if (v[0] == AEQ) { m->mprevLogIndex = v[p++]; m->mprevLogTerm = v[p++]; seq(m->mentries, &m->mentries_len); m->mcommitIndex = v[p++]; }
+    if (v[0] == RVP) { m->mvoteGranted = v[p++]; seq(m->mlog, &m->mlog_len); }
+    if (v[0] == AEP) { m->msuccess = v[p++]; m->mmatchIndex = v[p++]; }
+}
+
+// SmokeInit (Smokeraft.tla:64-76): k choices for each of the 9 per-server
+// variables, all k^9 combinations, each with the same bag of k messages drawn as
+// [RandomSubset(k, SmokeMessageType) -> {1}].
+int smoke_init(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<u32>* packed, std::string* why) {
+    const int S = c->sh.S, k = sc.smoke_k;
+    SmokeDomains D{S, c->cfg.n_values, sc.smoke_nat > 0 ? sc.smoke_nat : 2};
+    if (D.nat > 3) { *why = "smoke_nat > 3 exceeds the packed index range"; return RMC_E_INVAL; }
+    if (k > c->sh.K) { *why = "smoke_k messages exceed the bag capacity (set MaxMsgs >= k)"; return RMC_E_INVAL; }
+    std::mt19937_64 g(sc.seed ^ 0x5350AC3ull);
+    using V = std::vector<int>;
+    auto fn = [&](auto elem) { return [&, elem](std::mt19937_64& gg) { V v; for (int i = 0; i < S; ++i) { auto e = elem(gg); v.insert(v.end(), e.begin(), e.end()); } return v; }; };
+    auto one = [&](int lo, int hi) { return [&D, lo, hi](std::mt19937_64& gg) { return V{D.uni(gg, lo, hi)}; }; };
+    const auto ct = random_subset<V>(k, fn(one(0, D.nat)), g);                               // :67
+    const auto st = random_subset<V>(k, fn(one(0, 2)), g);                                   // :68
+    const auto vf = random_subset<V>(k, fn(one(-1, S - 1)), g);                              // :69 (Nil = -1)
+    const auto lg = random_subset<V>(k, fn([&](std::mt19937_64& gg) { return D.seq(gg, 3); }), g);  // :70
+    const auto ci = random_subset<V>(k, fn(one(0, D.nat)), g);                               // :71
+    const auto vr = random_subset<V>(k, fn(one(0, (1 << S) - 1)), g);                        // :72
+    const auto vg = random_subset<V>(k, fn(one(0, (1 << S) - 1)), g);                        // :73
+    auto row = [&](int lo, int hi) { return [&, lo, hi](std::mt19937_64& gg) { V v; for (int j = 0; j < S; ++j) v.push_back(D.uni(gg, lo, hi)); return v; }; };
+    const auto ni = random_subset<V>(k, fn(row(1, D.nat)), g);                               // :74
+    const auto mi = random_subset<V>(k, fn(row(0, D.nat)), g);                               // :75
+    std::vector<V> mtype_union;                                                              // :58-62
+    for (int t : {RVQ, AEQ, RVP, AEP}) {
+        auto part = random_subset<V>(k, [&, t](std::mt19937_64& gg) { return smoke_msg(D, t, gg); }, g);
+        mtype_union.insert(mtype_union.end(), part.begin(), part.end());
+    }
+    const auto msgs = random_subset<V>(k, [&](std::mt19937_64& gg) { return mtype_union[gg() % mtype_union.size()]; }, g);  // :76
+    for (const auto* vec : {&ct, &st, &vf, &lg, &ci, &vr, &vg, &ni, &mi})
+        if ((int)vec->size() != k) { *why = "RandomSubset could not draw k distinct elements"; return RMC_E_INVAL; }
+    u64 n = 1;
+    for (int x = 0; x < 9; ++x) n *= (u64)k;
+    packed->assign(n * (u64)c->NW, 0u);
+    for (u64 idx = 0; idx < n; ++idx) {
+        int dg[9];
+        u64 r = idx;
+        for (int x = 0; x < 9; ++x) { dg[x] = (int)(r % (u64)k); r /= (u64)k; }
+        rmc_state_view v;
+        memset(&v, 0, sizeof v);
+        v.n_servers = S;
+        size_t lp = 0;
+        for (int i = 0; i < S; ++i) {
+            v.currentTerm[i] = ct[dg[0]][i];
+            v.state[i] = st[dg[1]][i];
+            v.votedFor[i] = vf[dg[2]][i];
+            v.commitIndex[i] = ci[dg[4]][i];
+            v.votesResponded[i] = (uint32_t)vr[dg[5]][i];
+            v.votesGranted[i] = (uint32_t)vg[dg[6]][i];
+            for (int j = 0; j < S; ++j) {
+                v.nextIndex[i][j] = ni[dg[7]][i * S + j];
+                v.matchIndex[i][j] = mi[dg[8]][i * S + j];
+            }
+        }
+        const V& L = lg[dg[3]];
+        for (int i = 0; i < S; ++i) {
+            v.log_len[i] = L[lp++];
+            for (int x = 0; x < v.log_len[i]; ++x) { v.log[i][x].term = L[lp++]; v.log[i][x].value = L[lp++]; }
+        }
+        v.n_msgs = (int)msgs.size();
+        for (size_t q = 0; q < msgs.size(); ++q) msg_to_view(msgs[q], &v.msgs[q]);
+        if (int rc = encode_view(c, v, packed->data() + idx * (u64)c->NW, why)) return rc;
+    }
+    return 0;
+}
+
+int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_beh, std::vector<u32>* rec) {
+    if (!c || !sc || !out || sc->behaviours == 0 || sc->depth < 1) return RMC_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<u32> inits;
+    std::string why;
+    if (sc->smoke_k > 0) {
+        if (int rc = smoke_init(c, *sc, &inits, &why)) return fail(c, rc, why);
+    } else {
+        rmc_state_view iv;
+        init_view(c->cfg, &iv);
+        inits.assign((size_t)c->NW, 0u);
+        if (int rc = encode_view(c, iv, inits.data(), &why)) return fail(c, rc, why);
+    }
+    const u64 n_init = inits.size() / (u64)c->NW;
+    Params P = c->P;  // no CONSTRAINT in simulation: only the packed capacity bounds
+    P.max_term = 15;
+    P.max_log = LOG_CAP;
+    P.max_msgs = c->sh.K;
+    P.max_dup = 3;
+    u32 *d_init = nullptr, *d_rec = nullptr;
+    SimCounters* d_out = nullptr;
+    HIPCHK(c, hipMalloc(&d_init, inits.size() * 4));
+    HIPCHK(c, hipMalloc(&d_out, sizeof(SimCounters)));
+    if (rec) HIPCHK(c, hipMalloc(&d_rec, (size_t)sc->depth * c->NW * 4));
+    SimCounters h{};
+    h.viol = ~0ull;
+    HIPCHK(c, hipMemcpy(d_init, inits.data(), inits.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d_out, &h, sizeof h, hipMemcpyHostToDevice));
+    HIPCHK(c, hipEventRecord(c->ev0, c->st));
+    HIPCHK(c, launch_sim(c->sh, P, d_init, n_init, sc->behaviours, sc->depth, sc->seed, d_out, rec_beh, d_rec, c->st));
+    HIPCHK(c, hipEventRecord(c->ev1, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    HIPCHK(c, hipMemcpy(&h, d_out, sizeof h, hipMemcpyDeviceToHost));
+    if (rec) {
+        rec->assign((size_t)(h.steps + 1) * c->NW, 0u);
+        HIPCHK(c, hipMemcpy(rec->data(), d_rec, rec->size() * 4, hipMemcpyDeviceToHost));
+    }
+    (void)hipFree(d_init);
+    (void)hipFree(d_out);
+    (void)hipFree(d_rec);
+    memset(out, 0, sizeof *out);
+    out->behaviours = rec ? 1 : sc->behaviours;
+    out->steps = h.steps;
+    out->init_states = n_init;
+    out->truncated = h.truncated;
+    out->deadlocked = h.deadlocked;
+    if (h.viol != ~0ull) {
+        out->violated_inv = 1 << (int)((h.viol >> 40) & 3);
+        out->violation_depth = (int32_t)(h.viol >> 42);
+        out->violation_behaviour = h.viol & ((1ull << 40) - 1);
+    }
+    out->kernel_seconds = 1e-3 * ms;
+    out->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rmc_simulate(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out) { return run_sim(c, sc, out, -1, nullptr); }
+
+int rmc_sim_replay(rmc_ctx* c, const rmc_sim_config* sc, uint64_t behaviour, rmc_state_view* states, size_t cap,
+                   size_t* len) {
+    if (!c || !sc || !len || behaviour >= sc->behaviours) return RMC_E_INVAL;
+    rmc_sim_result r;
+    std::vector<u32> rec;
+    if (int rc = run_sim(c, sc, &r, (i64)behaviour, &rec)) return rc;
+    *len = rec.size() / (size_t)c->NW;
+    for (size_t q = 0; q < *len && q < cap; ++q) decode_state(c, rec.data() + q * c->NW, &states[q]);
     return 0;
 }
 
@@ -568,6 +797,7 @@ int rmc_dist_start(rmc_ctx* c) {
     c->level_start.clear();
     c->have_target = 0;
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     HIPCHK(c, hipMemsetAsync(c->B.sent, 0, c->sent_slots * 8, c->st));
     if (int rc = reset_counters(c, false)) return rc;
     rmc_state_view iv;

@@ -53,6 +53,18 @@ struct Shape {
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 
+// Simulation counters (k_simulate).
+typedef int64_t i64;
+struct SimCounters {
+    u64 steps, truncated, deadlocked;
+    u64 viol;  // min over violations of (depth << 42 | invariant << 40 | behaviour), ~0 = none
+};
+hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
+                      SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
+
+// Fingerprint salt for the kernels of this device (0 = default hash).
+hipError_t set_fp_salt(u64 seed, hipStream_t st);
+
 // Random-probe microbenchmark over table[mask + 1] (mode 0 loads, 1 CAS).
 hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st);
 

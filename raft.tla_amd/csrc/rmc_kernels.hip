@@ -616,7 +616,101 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
     }
 }
 
+// ---- simulation (TLC -simulate; Smokeraft.cfg) -------------
+// One thread per behaviour: a random initial state from `inits`, then up to
+// depth-1 steps, each choosing uniformly among ALL enabled successors (one
+// reservoir pass over the lanes).  A chosen successor outside the packed
+// capacity (term 16, Len(log) 4, 9 messages, count 4) ends the behaviour as
+// "truncated"; no enabled lane ends it as "deadlocked" (Smokeraft.cfg:48
+// turns deadlock checking off).  Invariants are checked on every state.
+// rec_beh >= 0: that behaviour also writes its states to rec (replay).
+__device__ __forceinline__ u64 sim_rand(u64& x) {  // splitmix64 stream
+    x += 0x9E3779B97F4A7C15ull;
+    return mix64(x);
+}
+
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* inits, u64 n_init, u64 n_beh, int depth,
+                                                  u64 seed, SimCounters* out, i64 rec_beh, u32* rec) {
+    constexpr int NW = 2 * S + K;
+    u64 steps = 0, trunc = 0, dead = 0;
+    for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n_beh; t += (u64)gridDim.x * 256ull) {
+        if (rec_beh >= 0 && (i64)t != rec_beh) continue;  // replay of one behaviour
+        u64 rs = mix64(seed ^ (t * 0xD1B54A32D192ED03ull));
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(inits + (sim_rand(rs) % n_init) * (u64)NW, w, m);
+        const bool record = (i64)t == rec_beh;
+        if (record) store_state<S, K>(rec, w, m);
+        int v = check_invariants<S, K>(w, m, P);
+        if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 42) | ((u64)(v - 1) << 40) | t));
+        for (int dd = 2; dd <= depth && !v; ++dd) {
+            u32 cnt = 0;
+            int pick = -1;
+            for (int lane = 0; lane < P.off[10]; ++lane) {
+                Delta d;
+                lane_delta<S, K>(w, m, lane, P, d);
+                if (!d.en) continue;
+                ++cnt;
+                if (sim_rand(rs) % cnt == 0) pick = lane;  // reservoir: uniform over enabled lanes
+            }
+            if (cnt == 0) {
+                ++dead;
+                break;
+            }
+            Delta d;
+            lane_delta<S, K>(w, m, pick, P, d);
+            u64 hh;
+            if (!delta_fp<S, K>(w, m, 0ull, d, P, &hh)) {
+                ++trunc;
+                break;
+            }
+            u64 wo[S];
+            u32 mo[K];
+            materialise<S, K>(w, m, d, wo, mo);
+#pragma unroll
+            for (int i = 0; i < S; ++i) w[i] = wo[i];
+#pragma unroll
+            for (int q = 0; q < K; ++q) m[q] = mo[q];
+            ++steps;
+            if (record) store_state<S, K>(rec + (u64)(dd - 1) * NW, w, m);
+            v = check_invariants<S, K>(w, m, P);
+            if (v)
+                atomicMin((unsigned long long*)&out->viol,
+                          (unsigned long long)(((u64)dd << 42) | ((u64)(v - 1) << 40) | t));
+        }
+    }
+    atomicAdd((unsigned long long*)&out->steps, (unsigned long long)steps);
+    if (trunc) atomicAdd((unsigned long long*)&out->truncated, (unsigned long long)trunc);
+    if (dead) atomicAdd((unsigned long long*)&out->deadlocked, (unsigned long long)dead);
+}
+
+template <int S, int K>
+static hipError_t launch_sim_t(const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
+                               SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
+    const u64 blocks = (n_beh + 255) / 256;
+    const u64 g = blocks < 4096 ? blocks : 4096;
+    hipLaunchKernelGGL((k_simulate<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, inits, n_init, n_beh, depth, seed,
+                       out, rec_beh, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
+                      SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
+#define RMC_SCASE(SS, KK) \
+    if (sh.S == SS && sh.K == KK) return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, out, rec_beh, rec, st);
+    RMC_SCASE(2, 4) RMC_SCASE(2, 8) RMC_SCASE(3, 4) RMC_SCASE(3, 8) RMC_SCASE(4, 4) RMC_SCASE(4, 8) RMC_SCASE(5, 4)
+    RMC_SCASE(5, 8)
+#undef RMC_SCASE
+    return hipErrorInvalidValue;
+}
+
 // ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
+hipError_t set_fp_salt(u64 seed, hipStream_t st) {
+    const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &salt, sizeof salt, 0, hipMemcpyHostToDevice, st);
+}
+
 static const u64 kExpandGrid = 2048;
 
 // Probes in flight per thread: 8 (measured best of 4/8 on MI355X).

@@ -80,13 +80,26 @@ class SuccView(C.Structure):
                 ("state", StateView)]
 
 
+class SimConfig(C.Structure):
+    _fields_ = [("behaviours", C.c_uint64), ("depth", C.c_int32), ("smoke_k", C.c_int32),
+                ("smoke_nat", C.c_int32), ("pad", C.c_int32), ("seed", C.c_uint64)]
+
+
+class SimResult(C.Structure):
+    _fields_ = [("behaviours", C.c_uint64), ("steps", C.c_uint64), ("init_states", C.c_uint64),
+                ("truncated", C.c_uint64), ("deadlocked", C.c_uint64), ("violated_inv", C.c_int32),
+                ("violation_depth", C.c_int32), ("violation_behaviour", C.c_uint64),
+                ("seconds", C.c_double), ("kernel_seconds", C.c_double)]
+
+
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.POINTER(LevelStats), C.c_void_p)
 
 # Every symbol include/rmc.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_run_bfs",
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
            "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
-           "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level")
+           "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level",
+           "rmc_set_seed", "rmc_simulate", "rmc_sim_replay")
 
 _lib = None
 
@@ -137,6 +150,13 @@ def native():
         lib.rmc_dist_insert.restype = C.c_int
         lib.rmc_dist_end_level.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         lib.rmc_dist_end_level.restype = C.c_int
+        lib.rmc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
+        lib.rmc_set_seed.restype = C.c_int
+        lib.rmc_simulate.argtypes = [C.c_void_p, C.POINTER(SimConfig), C.POINTER(SimResult)]
+        lib.rmc_simulate.restype = C.c_int
+        lib.rmc_sim_replay.argtypes = [C.c_void_p, C.POINTER(SimConfig), C.c_uint64,
+                                       C.POINTER(StateView), C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.rmc_sim_replay.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -217,6 +237,25 @@ class Checker:
         self._check(self.lib.rmc_get_result(self.ctx, C.byref(res)))
         self.levels = levels
         return res
+
+    def simulate(self, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0) -> SimResult:
+        """TLC -simulate over Smokeraft-style initial states (rmc_simulate)."""
+        sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, 0, seed)
+        out = SimResult()
+        self._check(self.lib.rmc_simulate(self.ctx, C.byref(sc), C.byref(out)))
+        return out
+
+    def sim_replay(self, behaviour, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0):
+        """States of one behaviour of the same simulation (rmc_sim_replay)."""
+        sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, 0, seed)
+        st = (StateView * depth)()
+        n = C.c_size_t()
+        self._check(self.lib.rmc_sim_replay(self.ctx, C.byref(sc), behaviour, st, depth, C.byref(n)))
+        return [st[k] for k in range(min(n.value, depth))]
+
+    def set_seed(self, seed: int):
+        """Fingerprint salt for the next run (rmc_set_seed)."""
+        self._check(self.lib.rmc_set_seed(self.ctx, seed))
 
     def result(self) -> Result:
         res = Result()

@@ -117,8 +117,8 @@ def random_state(model, rng: random.Random):
             return R.rec(mlastLogTerm=rng.randint(0, T), mlastLogIndex=rng.randint(0, L), **c)
         if t == R.RVP:
             return R.rec(mvoteGranted=rng.random() < 0.5, mlog=lg(), **c)
-        if t == R.AEQ:
-            return R.rec(mprevLogIndex=rng.randint(0, L), mprevLogTerm=rng.randint(0, T),
+        if t == R.AEQ:  # SmokeInt = -1..1 (Smokeraft.tla:14-15, :35): -1 included
+            return R.rec(mprevLogIndex=rng.randint(-1, L), mprevLogTerm=rng.randint(0, T),
                          mentries=tuple(ent() for _ in range(rng.randint(0, 1))),
                          mcommitIndex=rng.randint(0, L), **c)
         return R.rec(msuccess=rng.random() < 0.5, mmatchIndex=rng.randint(0, L), **c)

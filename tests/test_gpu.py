@@ -65,6 +65,17 @@ def test_bfs_matches_oracle(name):
     assert res.violated_inv == 0 and res.deadlock == 0
 
 
+def test_fingerprint_salt_does_not_change_counts():
+    """Another member of the fingerprint family (rmc_config.seed) must give the
+    same exact counts: evidence against fingerprint collisions at full size."""
+    g = GOLDEN["bounded_full"]
+    cfg = cfg_from(g["params"], capacity=int(g["distinct"] * 1.25))
+    cfg.seed = 0xC0FFEE
+    res, levels, _ = run(cfg)
+    assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+    assert levels == g["level_new"]
+
+
 @pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both"])
 def test_bug_variant_violation_and_trace(name):
     g = GOLDEN[name]

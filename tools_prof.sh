@@ -1,5 +1,6 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-for om in 2; do
-RMC_OWNER=$om timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 2957$om tests/dist_worker.py --cfg specs/MCraftBounded.cfg --out gpurun_out/balance8_owner$om.json --device 0 --backend gloo --chunk 2097152 --cap-per-dest 4194304 --capacity 30000000 --rerun 0 > gpurun_out/balance8_owner$om.log 2>&1 || exit 1
+timeout -k 10 500 python -u -m pytest tests/test_gpu.py tests/test_dist.py -x -q --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
+for kc in 1 0 1; do
+RMC_KEY_CACHE=$kc timeout -k 10 300 python -u bench.py --no-cpu --no-probe-ceiling > gpurun_out/bench_kc$kc.json 2> gpurun_out/bench_kc$kc.err || exit 1
 done
