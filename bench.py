@@ -34,8 +34,10 @@ def parse():
                     help="state capacity per GPU (0 = 1.5e9 / world * 1.3 for the bench model)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK (one GPU per rank)")
-    ap.add_argument("--chunk", type=int, default=1 << 21, help="frontier states per exchange")
-    ap.add_argument("--cap-per-dest", type=int, default=1 << 23, help="outbox records per rank")
+    ap.add_argument("--chunk", type=int, default=1 << 24, help="frontier states per exchange")
+    ap.add_argument("--cap-per-dest", type=int, default=1 << 24, help="outbox records per rank")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the sharded path even at one rank (measures its overhead)")
     ap.add_argument("--no-probe-ceiling", action="store_true",
                     help="skip the random-probe microbenchmark (roofline ceiling)")
     ap.add_argument("--cpu-levels", type=int, default=22,
@@ -76,19 +78,30 @@ def pmc_traffic(config_path):
 
 def main():
     a = parse()
+    # The JSON line is the only thing on stdout: libraries that print banners
+    # there (RCCL prints its version block at communicator init) are sent to
+    # stderr by pointing fd 1 at fd 2 for the rest of the run.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    sharded = world > 1 or a.force_dist
+    if sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         import torch
         import torch.distributed as dist
         dev = a.device if a.device >= 0 else local
         torch.cuda.set_device(dev)
         dist.init_process_group(a.dist_backend, init_method="env://")
     cfg = rmc.config_from_files(a.config)
-    cfg.device = (a.device if a.device >= 0 else local) if world > 1 else max(a.device, 0)
-    cfg.state_capacity = a.capacity or int(1.5e9 / world * (1.3 if world > 1 else 1.0))
+    cfg.device = (a.device if a.device >= 0 else local) if sharded else max(a.device, 0)
+    cfg.state_capacity = a.capacity or int(1.5e9 / world * (1.3 if sharded else 1.0))
     W = rmc.native().rmc_state_bytes(cfg)
     # roofline ceiling of the fingerprint set: random 8-B probes over 64 GB
     r_max = None
@@ -99,18 +112,18 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    last_dist = [None]
+
     def one_run(ck, first):
-        if world == 1:
+        if not sharded:
             r = ck.run()
             return r.distinct, r.generated, r.depth, r.probes, r.expand_kernel_seconds, r.expand_launches
         from rmc import dist as rdist
-        k0 = ck.result().expand_kernel_seconds if not first else 0.0
-        l0 = ck.result().expand_launches if not first else 0
         r = rdist.run(ck, chunk_states=a.chunk, cap_per_dest=a.cap_per_dest, sent_cache_slots=1 << 27,
                       init=first)
-        cr = ck.result()
-        return (r.distinct, r.generated, r.depth, r.probes, cr.expand_kernel_seconds - k0,
-                cr.expand_launches - l0)
+        cr = ck.result()  # rmc_dist_start resets the per-run counters
+        last_dist[0] = r
+        return (r.distinct, r.generated, r.depth, r.probes, cr.expand_kernel_seconds, cr.expand_launches)
 
     with rmc.Checker(cfg) as ck:
         first = True
@@ -132,7 +145,7 @@ def main():
         barrier()
         dt = time.perf_counter() - t0
         salt_check = None
-        if world == 1:  # untimed: same search under another fingerprint salt
+        if not sharded:  # untimed: same search under another fingerprint salt
             ck.set_seed(0x5A17ED)
             r2 = ck.run()
             ck.set_seed(0)
@@ -152,7 +165,7 @@ def main():
     ks = kern / a.steps
     nlaunch = max(1, launches // a.steps)
     achieved = b_alg / ks / 1e9 if ks > 0 else 0.0
-    traffic, tsrc = pmc_traffic(a.config) if world == 1 else (None, None)
+    traffic, tsrc = pmc_traffic(a.config) if not sharded else (None, None)
     out = {
         "metric": METRIC,
         "value": D / per_step,
@@ -172,13 +185,13 @@ def main():
                         f"{cfg.max_log_len} MaxMsgs={cfg.max_msgs} MaxDup={cfg.max_dup}, BFS to fixpoint",
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
-            "parallelism": f"fingerprint-sharded x{world} (RCCL all-to-all)" if world > 1 else "single GPU",
+            "parallelism": f"fingerprint-sharded x{world} (RCCL all-to-all)" if sharded else "single GPU",
             "fp_salt_crosscheck": salt_check,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-            "kernel": "k_expand", "kernel_ms_per_step": ks * 1e3 if world == 1 else None,
+            "kernel": "k_expand", "kernel_ms_per_step": ks * 1e3,
             "launches_per_step": nlaunch, "alg_bytes_per_launch": b_alg / nlaunch,
             "alg_bytes_per_step": b_alg, "probes_per_step": NP,
             "probe_rate_per_s": NP / ks if ks > 0 else 0.0,
@@ -186,14 +199,18 @@ def main():
             "frac_of_probe_ceiling": (NP / ks / r_max) if (ks > 0 and r_max) else None,
         },
     }
-    if world > 1:
+    if sharded:
+        ld = last_dist[0]
+        out["sharded"] = {"chunks_per_step": ld.chunks, "records_sent_rank0": ld.records_sent,
+                          "phase_s_rank0": {k: round(v, 6) for k, v in ld.phase.items()},
+                          "chunk_states": a.chunk, "cap_per_dest": a.cap_per_dest}
         out["roofline"]["note"] = "per-rank kernel time of rank 0; achieved is rank 0's share"
         out["roofline"]["achieved"] = (b_alg / world) / ks / 1e9 if ks > 0 else 0.0
         out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
     if rank == 0 and not a.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_levels)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

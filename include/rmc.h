@@ -49,6 +49,10 @@ extern "C" {
 #define RMC_FLAG_CHECK_DEADLOCK (1u << 1)  /* CHECK_DEADLOCK TRUE (TLC default)         */
 #define RMC_FLAG_BUG_QUORUM (1u << 2)      /* BecomeLeader guard raft.tla:197 weakened  */
                                            /* to votesGranted[i] /= {} (config 5)       */
+#define RMC_FLAG_VERIFY_STATES (1u << 3)   /* full-state verification: every fingerprint */
+                                           /* hit is compared with the stored state;    */
+                                           /* differences = collisions (no TLC analog;  */
+                                           /* single GPU, no SYMMETRY)                  */
 
 /* rmc_config.invariants — the INVARIANT names the engine knows (fused checks). */
 #define RMC_INV_TYPEOK (1u << 0)           /* raft.tla:482-492                          */
@@ -92,6 +96,9 @@ typedef struct rmc_result {
                                   /* the ctx stream (sum over levels)                    */
     uint64_t expand_launches;  /* expansion kernel launches (levels are split in chunks) */
     uint64_t probes;           /* fingerprint-set probes (successors that reached the set) */
+    uint64_t collisions;       /* RMC_FLAG_VERIFY_STATES: fingerprint hits whose stored state */
+                               /* differs (0 = the counts are exact, not probabilistic)   */
+    uint64_t verified;         /* RMC_FLAG_VERIFY_STATES: hits compared state by state    */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */
@@ -171,6 +178,10 @@ int rmc_run_bfs(rmc_ctx* ctx, rmc_progress_fn cb, void* user);
 /* Changes rmc_config.seed (fingerprint salt) for the next run on this ctx. */
 int rmc_set_seed(rmc_ctx* ctx, uint64_t seed);
 int rmc_get_result(const rmc_ctx* ctx, rmc_result* out);
+/* Test hook of the verification mode: keep only the low `bits` fingerprint
+ * bits (1..64), so collisions happen and must be reported.  Needs
+ * RMC_FLAG_VERIFY_STATES. */
+int rmc_set_fp_bits(rmc_ctx* ctx, int32_t bits);
 
 /* Counterexample: the states from an initial state to the violating (or
  * deadlocked) state, in order, with the action family and lane of the step
@@ -229,8 +240,9 @@ int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, r
  *          host all-to-all of counts and records (torch.distributed / RCCL);
  *          rmc_dist_insert(received records) } until every rank's frontier is done;
  *   rmc_dist_end_level -> local stats; host all-reduce; stop when no rank has new states.
- * A record is rmc_dist_record_words() u32: the packed successor, its
- * fingerprint, the global parent ref (rank << 48 | index) and the lane.
+ * A record is rmc_dist_record_words() u32: the packed successor and its
+ * global parent ref (rank << 48 | lane << 40 | index); the owner recomputes
+ * the fingerprint from the state.
  * The outbox is caller-owned device memory: [world][cap_per_dest][record]. */
 int rmc_dist_init(rmc_ctx* ctx, int32_t rank, int32_t world, uint64_t sent_cache_slots);
 size_t rmc_dist_record_words(const rmc_ctx* ctx);

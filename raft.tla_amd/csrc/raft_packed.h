@@ -118,6 +118,8 @@ RMC_HD u32 owner_of(u64 key, u32 world) { return (u32)(((key >> 32) * (u64)world
 struct Params {
     int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;
     int off[11];  // family lane offsets (= Lanes<S,K>::off, for host code)
+    u64 fp_mask;  // full-state verification mode: fingerprint bits kept (~0 = all; fewer only
+                  // to provoke collisions in tests, rmc_set_fp_bits)
 };
 
 // Lane table: Restart S, Timeout S, RequestVote S^2,

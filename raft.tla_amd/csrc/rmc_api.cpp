@@ -76,6 +76,8 @@ int validate(const rmc_config* c, std::string* why) {
     if ((c->flags & RMC_FLAG_SYMMETRY) && c->n_servers > 4)
         return bad("SYMMETRY is supported for up to 4 servers");
     if (c->invariants & ~7u) return bad("unknown invariant bit");
+    if ((c->flags & RMC_FLAG_VERIFY_STATES) && (c->flags & RMC_FLAG_SYMMETRY))
+        return bad("full-state verification is not supported with SYMMETRY");
     return 0;
 }
 
@@ -84,6 +86,7 @@ void fill_params(rmc_ctx* c) {
     c->sh.S = g.n_servers;
     c->sh.K = kcap_for(g.max_msgs);
     c->sh.sym = (g.flags & RMC_FLAG_SYMMETRY) != 0;
+    c->sh.verify = (g.flags & RMC_FLAG_VERIFY_STATES) != 0;
     c->NW = 2 * c->sh.S + c->sh.K;
     Params& P = c->P;
     P.V = g.n_values;
@@ -94,6 +97,7 @@ void fill_params(rmc_ctx* c) {
     P.bug_quorum = (g.flags & RMC_FLAG_BUG_QUORUM) ? 1 : 0;
     P.inv_mask = (int)g.invariants;
     P.symmetry = c->sh.sym ? 1 : 0;
+    P.fp_mask = ~0ull;
     const int S = c->sh.S, K = c->sh.K;
     const int sizes[10] = {S, S, S * S, S, S * VMAX, S, S * S, K, K, K};  // = Lanes<S,K>
     P.off[0] = 0;
@@ -377,6 +381,13 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         return bail(RMC_E_NOMEM);
     }
     memset(c->h_ctr, 0, sizeof(Counters));
+    if (c->sh.verify) {  // slot -> store index (8 B per slot) + deferred-hit buffer (16 B per record)
+        c->B.vcap = 1ull << 26;
+        if (hipMalloc(&c->B.sidx, slots * 8) != hipSuccess || hipMalloc(&c->B.vbuf, c->B.vcap * 16) != hipSuccess) {
+            c->err = "device allocation failed (verification buffers)";
+            return bail(RMC_E_NOMEM);
+        }
+    }
     c->B.rank = 0;
     c->B.world = 1;
     c->B.ref_tag = 0;
@@ -395,6 +406,8 @@ void rmc_destroy(rmc_ctx* c) {
     (void)hipFree(c->d_staged);
     (void)hipFree(c->B.sent);
     (void)hipFree(c->B.ocount);
+    (void)hipFree(c->B.sidx);
+    (void)hipFree(c->B.vbuf);
     if (c->h_ocount) (void)hipHostFree(c->h_ocount);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -412,6 +425,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->level_start.clear();
     c->have_target = 0;
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     if (int rc = reset_counters(c, false)) return rc;
 
@@ -427,6 +441,8 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.generated = 1;
     c->level_start.push_back(0);
     c->level_start.push_back(c->h_ctr->count);
+    if (c->sh.verify)
+        HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
     int depth = c->h_ctr->count ? 1 : 0;
     if (c->h_ctr->viol != ~0ull) {
         c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 3);
@@ -444,10 +460,24 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         }
         if (int rc = reset_counters(c, true)) return rc;
         HIPCHK(c, hipEventRecord(c->ev0, c->st));
-        for (u64 a = lo; a < hi; a += CHUNK) {
-            const u64 b = std::min(hi, a + CHUNK);
+        // verification mode: smaller launches, each followed by publishing its
+        // new states (k_publish) and checking its deferred hits (k_verify)
+        const u64 chunk = c->sh.verify ? (1ull << 20) : CHUNK;
+        for (u64 a = lo; a < hi; a += chunk) {
+            const u64 b = std::min(hi, a + chunk);
             HIPCHK(c, launch(c->sh, 0, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
             c->res.expand_launches += 1;
+            if (c->sh.verify) {
+                const u64 before = c->h_ctr->count;
+                if (int rc = read_counters(c)) return rc;
+                if (c->h_ctr->overflow) break;
+                HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, before, c->h_ctr->count, nullptr, nullptr, 0, nullptr,
+                                 c->st));
+                HIPCHK(c, launch(c->sh, 6, c->P, c->PT, c->B, c->h_ctr->vcount, 0, nullptr, nullptr, 0, nullptr,
+                                 c->st));
+                HIPCHK(c, hipMemsetAsync(&c->B.ctr->vcount, 0, 8, c->st));
+                c->h_ctr->vcount = 0;
+            }
         }
         HIPCHK(c, hipEventRecord(c->ev1, c->st));
         if (int rc = read_counters(c)) return rc;
@@ -456,6 +486,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         c->res.expand_kernel_seconds += 1e-3 * ms;
         const Counters& k = *c->h_ctr;
         if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
+        if (k.overflow & 4u) return fail(c, RMC_E_CAPACITY, "verification buffer full");
+        if (k.overflow & 8u) return fail(c, RMC_E_HIP, "verification: a stored state has no fingerprint slot");
+        c->res.collisions += k.collisions;
+        c->res.verified += k.vchecked;
         if (k.overflow) {
             return fail(c, RMC_E_CAPACITY, "state store full (capacity " + std::to_string(c->B.cap) +
                                                 " states); raise rmc_config.state_capacity");
@@ -504,6 +538,13 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
 int rmc_set_seed(rmc_ctx* c, uint64_t seed) {
     if (!c) return RMC_E_INVAL;
     c->cfg.seed = seed;
+    return 0;
+}
+
+int rmc_set_fp_bits(rmc_ctx* c, int32_t bits) {
+    if (!c || bits < 1 || bits > 64) return RMC_E_INVAL;
+    if (!c->sh.verify) return fail(c, RMC_E_INVAL, "rmc_set_fp_bits needs RMC_FLAG_VERIFY_STATES");
+    c->P.fp_mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
     return 0;
 }
 
@@ -764,12 +805,15 @@ int rmc_sim_replay(rmc_ctx* c, const rmc_sim_config* sc, uint64_t behaviour, rmc
 // ---- sharded BFS (one process per GPU; the host driver does the all-to-all) ----
 int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_slots) {
     if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return RMC_E_INVAL;
+    if (c->sh.verify) return fail(c, RMC_E_INVAL, "sharded mode does not support full-state verification yet");
     if (c->sh.sym) return fail(c, RMC_E_INVAL, "sharded mode does not support SYMMETRY yet");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     u64 slots = 1;
     while (slots < std::max<u64>(sent_cache_slots, 1024)) slots <<= 1;
     (void)hipFree(c->B.sent);
     (void)hipFree(c->B.ocount);
+    (void)hipFree(c->B.sidx);
+    (void)hipFree(c->B.vbuf);
     if (c->h_ocount) (void)hipHostFree(c->h_ocount);
     c->B.sent = nullptr;
     c->B.ocount = nullptr;
@@ -783,12 +827,12 @@ int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_s
     c->B.world = (u32)world;
     c->B.ref_tag = (u64)rank << 48;
     const char* om = getenv("RMC_OWNER");  // partition: 0 fingerprint, 1 server-0 word, 2 servers 0+1
-    c->B.owner_mode = om ? (u32)std::min(2, std::max(0, atoi(om))) : 1u;
+    c->B.owner_mode = om ? (u32)std::min(2, std::max(0, atoi(om))) : 2u;
     c->dist = 1;
     return 0;
 }
 
-size_t rmc_dist_record_words(const rmc_ctx* c) { return c ? (size_t)c->NW + 6 : 0; }
+size_t rmc_dist_record_words(const rmc_ctx* c) { return c ? (size_t)c->NW + 2 : 0; }
 
 int rmc_dist_start(rmc_ctx* c) {
     if (!c || !c->dist) return RMC_E_STATE;

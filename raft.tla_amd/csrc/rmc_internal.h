@@ -16,6 +16,10 @@ struct Counters {
     u32 overflow;   // state store full
     u32 table_full; // fingerprint set full
     u64 probes;     // fingerprint-set probes issued by k_expand
+    // full-state verification mode (RMC_FLAG_VERIFY_STATES)
+    u64 collisions; // fingerprint hits whose stored state differs from the successor
+    u64 vchecked;   // fingerprint hits compared state against state
+    u64 vcount;     // deferred hits in vbuf (stored twin not yet published)
 };
 
 struct DevBufs {
@@ -28,13 +32,19 @@ struct DevBufs {
     Counters* ctr;
     // sharded mode (rank/world > 1 GPU processes; single mode: rank 0, world 1)
     u32 rank, world;
-    u32 owner_mode;            // 0: owner by fingerprint, 1: by server 0's word
+    u32 owner_mode;            // 0: by fingerprint, 1: by server 0 word, 2: by servers 0+1 words (default)
     u64 ref_tag;               // (rank << 48): parent refs are global (rank, index)
     u64* sent;                 // lossy cache of fingerprints already shipped to their owner
     u64 smask;                 // sent-cache slots - 1
     u32* outbox;               // [world][ocap][NW + 6] records, caller-owned
     u64 ocap;                  // records per destination
     unsigned long long* ocount;  // [world] records written per destination
+    // full-state verification mode: store index of the state owning each
+    // fingerprint-set slot (~0 = not yet published; published between launches
+    // by k_publish) and the deferred hits {parent index, slot | lane << 56}
+    u64* sidx;
+    u64* vbuf;
+    u64 vcap;                  // records in vbuf
 };
 
 struct PermTable {
@@ -44,12 +54,15 @@ struct PermTable {
 struct Shape {
     int S, K;
     bool sym;
+    bool verify;  // full-state verification (no symmetry, single GPU)
 };
 
 // which: 0 = k_expand over store[a, b); 1 = k_seed of `a` staged states `in`;
 //        2 = k_list of `a` states `in` into `out` (cap records, *count);
 //        3 = sharded k_expand over store[a, b) (outbox in B);
-//        4 = k_insert_remote of `a` received records `in`.
+//        4 = k_insert_remote of `a` received records `in`;
+//        5 = k_publish over store[a, b) (verification: slot -> store index);
+//        6 = k_verify of `a` deferred hits in B.vbuf.
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 

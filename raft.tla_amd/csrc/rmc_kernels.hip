@@ -45,6 +45,24 @@ __device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 
     return 0;
 }
 
+// fp_insert that also reports the slot holding the key (verification mode).
+__device__ __forceinline__ int fp_insert_at(u64* __restrict__ table, u64 mask, u64 key, u32* full, u64* at) {
+    u64 s = key & mask;
+    for (u64 n = 0; n <= mask; ++n) {
+        const u64 cur = table[s];
+        if (cur == key) { *at = s; return 0; }
+        if (cur == 0) {
+            const u64 prev = atomicCAS((unsigned long long*)&table[s], 0ull, (unsigned long long)key);
+            if (prev == 0) { *at = s; return 1; }
+            if (prev == key) { *at = s; return 0; }
+        }
+        s = (s + 1) & mask;
+    }
+    atomicOr(full, 1u);
+    *at = ~0ull;
+    return 0;
+}
+
 // Same protocol, given the already-loaded content `cur` of the first slot.
 __device__ __forceinline__ int fp_resolve(u64* __restrict__ table, u64 mask, u64 key, u64 cur, u32* full) {
     if (cur == key) return 0;
@@ -213,16 +231,126 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
     wave_sync_lds();
 }
 
+// ---- full-state verification (RMC_FLAG_VERIFY_STATES) ---------------------------
+// TLC trusts its 64-bit fingerprints; this mode checks them.  Every successor
+// whose fingerprint is already in the set is compared, field for field, with
+// the stored state that owns that fingerprint.  A difference is a fingerprint
+// collision (a distinct state the search would silently drop) and is counted.
+// The slot -> store-index map (sidx) is published between launches
+// (k_publish), so a hit on a state of a completed launch is checked inline
+// and a hit on a state found in the same launch is deferred to k_verify.
+template <int S, int K>
+__device__ __forceinline__ bool same_state(const u64 (&w)[S], const u32 (&m)[K], const u32* __restrict__ st) {
+    u64 w2[S];
+    u32 m2[K];
+    load_state<S, K>(st, w2, m2);
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < S; ++i) eq &= w[i] == w2[i];
+#pragma unroll
+    for (int q = 0; q < K; ++q) eq &= m[q] == m2[q];
+    return eq;
+}
+
+template <int S, int K>
+__device__ __noinline__ void verify_hit(const u64 (&w)[S], const u32 (&m)[K], u64 parent, int lane, u64 slot,
+                                        const Params& P, const DevBufs& B) {
+    constexpr int NW = 2 * S + K;
+    const u64 ix = slot == ~0ull ? ~0ull : B.sidx[slot];
+    if (slot == ~0ull) return;  // table full (flagged by the insert)
+    if (ix == ~0ull) {          // owner found in this launch: check after it
+        const u64 q = atomicAdd((unsigned long long*)&B.ctr->vcount, 1ull);
+        if (q < B.vcap) {
+            B.vbuf[2 * q] = parent;
+            B.vbuf[2 * q + 1] = slot | ((u64)lane << 56);
+        } else {
+            atomicOr(&B.ctr->overflow, 4u);
+        }
+        return;
+    }
+    Delta d;
+    lane_delta<S, K>(w, m, lane, P, d);
+    u64 wo[S];
+    u32 mo[K];
+    materialise<S, K>(w, m, d, wo, mo);
+    atomicAdd((unsigned long long*)&B.ctr->vchecked, 1ull);
+    if (!same_state<S, K>(wo, mo, B.store + ix * (u64)NW))
+        atomicAdd((unsigned long long*)&B.ctr->collisions, 1ull);
+}
+
+template <int S, int K>
+__device__ __forceinline__ u64 verify_key(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
+    const u64 k = state_fp<S, K>(w, m) & P.fp_mask;
+    return k ? k : 1ull;
+}
+
+// sidx[slot of state i's fingerprint] = i for the stored states [lo, hi).
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_publish(const Params P, const DevBufs B, u64 lo, u64 hi) {
+    constexpr int NW = 2 * S + K;
+    for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + i * (u64)NW, w, m);
+        const u64 key = verify_key<S, K>(w, m, P);
+        u64 s = key & B.tmask;
+        u64 n = 0;
+        while (B.table[s] != key && n <= B.tmask) { s = (s + 1) & B.tmask; ++n; }
+        if (n > B.tmask) atomicOr(&B.ctr->overflow, 8u);  // a stored state without its key
+        else B.sidx[s] = i;
+    }
+}
+
+// The deferred hits of the last launch, now that their owners are published.
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_verify(const Params P, const DevBufs B, u64 n) {
+    constexpr int NW = 2 * S + K;
+    for (u64 q = (u64)blockIdx.x * 256ull + threadIdx.x; q < n; q += (u64)gridDim.x * 256ull) {
+        const u64 parent = B.vbuf[2 * q], sl = B.vbuf[2 * q + 1];
+        const u64 slot = sl & ((1ull << 56) - 1);
+        const int lane = (int)(sl >> 56);
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + parent * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, d, wo, mo);
+        const u64 ix = B.sidx[slot];
+        if (ix == ~0ull) {
+            atomicOr(&B.ctr->overflow, 8u);
+            continue;
+        }
+        atomicAdd((unsigned long long*)&B.ctr->vchecked, 1ull);
+        if (!same_state<S, K>(wo, mo, B.store + ix * (u64)NW))
+            atomicAdd((unsigned long long*)&B.ctr->collisions, 1ull);
+    }
+}
+
 // Owner rank of a state in sharded mode.  Mode 0: by fingerprint.  Mode 1: by
 // server 0's word — a successor that does not touch server 0 (bag-only
 // actions, actions of the other servers) stays on its parent's rank, so far
 // fewer successors cross GPUs; balance relies on server 0's many word values.
 // Mode 2: by the words of servers 0 and 1 (more distinct values: better
 // balance, successors of two servers cross).
+constexpr u64 OWN_C0 = 0x6a09e667f3bcc909ull, OWN_C1 = 0xbb67ae8584caa73bull;
+__device__ __forceinline__ u64 own_h0(u64 w0, const DevBufs& B) { return B.owner_mode ? mix64(w0 ^ OWN_C0) : 0ull; }
+__device__ __forceinline__ u64 own_h1(u64 w1, const DevBufs& B) { return B.owner_mode == 2 ? mix64(w1 ^ OWN_C1) : 0ull; }
 __device__ __forceinline__ u32 owner_state(u64 key, u64 w0, u64 w1, const DevBufs& B) {
-    if (B.owner_mode == 1) return owner_of(mix64(w0 ^ 0x6a09e667f3bcc909ull), B.world);
-    if (B.owner_mode == 2) return owner_of(mix64(w0 ^ 0x6a09e667f3bcc909ull) + mix64(w1 ^ 0xbb67ae8584caa73bull), B.world);
-    return owner_of(key, B.world);
+    if (B.owner_mode == 0) return owner_of(key, B.world);
+    return owner_of(own_h0(w0, B) + own_h1(w1, B), B.world);
+}
+// Owner of a successor: a lane that leaves servers 0 and 1 alone (mode 2; mode 1:
+// server 0) keeps its parent's owner — this rank, since a state is stored by
+// its owner — so only the other lanes mix their words.
+template <int S>
+__device__ __forceinline__ u32 owner_succ(u64 key, const Delta& d, const u64 (&w)[S], const DevBufs& B) {
+    if (B.world == 1) return 0;
+    if (B.owner_mode == 0) return owner_of(key, B.world);
+    if (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2))
+        return owner_state(key, d.srv == 0 ? d.w_new : w[0], d.srv == 1 ? d.w_new : w[1], B);
+    return B.rank;
 }
 
 template <int S, int K>
@@ -239,24 +367,37 @@ __device__ __forceinline__ u64 fp_of_materialised(const u64 (&w)[S], const u32 (
 template <int S, int K>
 __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
                                            const uint8_t* l_lane, const uint8_t* l_dest, u32 n) {
-    constexpr int NW = 2 * S + K, RW = NW + 6;
+    constexpr int NW = 2 * S + K, RW = NW + 2;
     wave_sync_lds();
     const int me = (int)__lane_id();
     const u64 lt = (1ull << me) - 1ull;
+    // Reserve every destination's slots for the whole list with ONE atomic per
+    // destination: lane dd (world <= 64) counts destination dd's entries, adds
+    // them to dd's counter, then hands out consecutive slots round by round.
+    u64 mine = 0;  // lane dd: entries for destination dd, then its next slot
+    for (u32 e0 = 0; e0 < n; e0 += 64) {
+        const u32 e = e0 + (u32)me;
+        const u32 dest = e < n ? l_dest[e] : 0xFFu;
+        for (u32 dd = 0; dd < B.world; ++dd) {
+            const u64 bal = __ballot(dest == dd);
+            if ((u32)me == dd) mine += (u64)__popcll(bal);
+        }
+    }
+    if ((u32)me < B.world && mine) {
+        unsigned long long* ctr = (u32)me == B.rank ? (unsigned long long*)&B.ctr->count : &B.ocount[me];
+        mine = atomicAdd(ctr, (unsigned long long)mine);
+    }
     for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
         const u32 e = e0 + (u32)me;
         const bool valid = e < n;
         const u32 dest = valid ? l_dest[e] : 0xFFu;
         u64 slot = ~0ull;
         for (u32 dd = 0; dd < B.world; ++dd) {
-            const u64 bal = __ballot(valid && dest == dd);
+            const u64 bal = __ballot(dest == dd);
             if (!bal) continue;
-            const int leader = __ffsll((long long)bal) - 1;
-            u64 base = 0;
-            unsigned long long* ctr = dd == B.rank ? (unsigned long long*)&B.ctr->count : &B.ocount[dd];
-            if (me == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(bal));
-            base = bcast64(base, leader);
-            if (valid && dest == dd) slot = base + (u64)__popcll(bal & lt);
+            const u64 base = bcast64(mine, (int)dd);
+            if (dest == dd) slot = base + (u64)__popcll(bal & lt);
+            if ((u32)me == dd) mine += (u64)__popcll(bal);
         }
         if (!valid) continue;
         const u64 rel = l_rel[e];
@@ -286,11 +427,10 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
             }
             u32* r = B.outbox + ((u64)dest * B.ocap + slot) * (u64)RW;
             store_state<S, K>(r, wo, mo);
-            const u64 key = fp_of_materialised<S, K>(wo, mo, P);
-            const u64 ref = B.ref_tag | (lo + rel);
-            r[NW] = (u32)key; r[NW + 1] = (u32)(key >> 32);
-            r[NW + 2] = (u32)ref; r[NW + 3] = (u32)(ref >> 32);
-            r[NW + 4] = (u32)lane; r[NW + 5] = 0;
+            // global parent ref with the lane in bits 40-47 (the owner
+            // recomputes the fingerprint from the state: 8 B less per record)
+            const u64 ref = B.ref_tag | ((u64)lane << 40) | (lo + rel);
+            r[NW] = (u32)ref; r[NW + 1] = (u32)(ref >> 32);
         }
     }
     wave_sync_lds();
@@ -302,13 +442,17 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // DIST: sharded mode — successors owned by another rank are looked up in the
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
-template <int S, int K, bool SYM, int BATCH, bool DIST>
+template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false>
 __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr int NP = SYM ? NPerm<S>::v : 1;
-    __shared__ u32 s_rel[4][WCAP];
-    __shared__ uint8_t s_lane[4][WCAP];
-    __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? WCAP : 1];
+    // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
+    // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
+    // single-GPU kernel (VGPR-bound there).
+    constexpr int LCAP = DIST ? 320 : WCAP;
+    __shared__ u32 s_rel[4][LCAP];
+    __shared__ uint8_t s_lane[4][LCAP];
+    __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? LCAP : 1];
     __shared__ u64 s_key[BATCH][256];
     __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
     const int wv = (int)(threadIdx.x >> 6);
@@ -353,10 +497,9 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                     if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
                         key = h;
                         if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
+                        if constexpr (VERIFY) key &= P.fp_mask;
                         key = key ? key : 1ull;
-                        if constexpr (DIST)
-                            s_own[b][threadIdx.x] = (uint8_t)owner_state(key, d.srv == 0 ? d.w_new : w[0],
-                                                                         d.srv == 1 ? d.w_new : w[1], B);
+                        if constexpr (DIST) s_own[b][threadIdx.x] = (uint8_t)owner_succ<S>(key, d, w, B);
                     }
                 }
                 s_key[b][threadIdx.x] = key;
@@ -379,7 +522,11 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
             u32 newbits = 0, slowbits = 0;
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
-                if (!key[b] || cur[b] == key[b]) continue;
+                if (!key[b]) continue;
+                if (cur[b] == key[b]) {
+                    if constexpr (VERIFY) verify_hit<S, K>(w, m, lo + rel, lane0 + b, key[b] & B.tmask, P, B);
+                    continue;
+                }
                 if constexpr (DIST) {
                     if (s_own[b][threadIdx.x] != B.rank) {  // not sent before (lossy cache): ship it
                         B.sent[(key[b] >> 8) & B.smask] = key[b];
@@ -392,6 +539,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                                                (unsigned long long)key[b]);
                     if (prev == 0) newbits |= 1u << b;
                     else if (prev != key[b]) slowbits |= 1u << b;
+                    else if constexpr (VERIFY) verify_hit<S, K>(w, m, lo + rel, lane0 + b, key[b] & B.tmask, P, B);
                 } else {
                     slowbits |= 1u << b;
                 }
@@ -399,7 +547,15 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
             while (slowbits) {  // rare: linear probing past an occupied first slot
                 const int b = __builtin_ctz(slowbits);
                 slowbits &= slowbits - 1;
-                if (fp_insert(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full)) newbits |= 1u << b;
+                if constexpr (VERIFY) {
+                    u64 at = 0;
+                    if (fp_insert_at(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full, &at))
+                        newbits |= 1u << b;
+                    else
+                        verify_hit<S, K>(w, m, lo + rel, lane0 + b, at, P, B);
+                } else if (fp_insert(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full)) {
+                    newbits |= 1u << b;
+                }
             }
             // (d) list the winners (wave-aggregated, no global atomics)
             for (int b = 0; b < BATCH; ++b) {
@@ -413,7 +569,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                         if constexpr (DIST) l_dest[pos] = s_own[b][threadIdx.x];
                     }
                     n += (u32)__popcll(bal);
-                    if (n > (u32)(WCAP - 64)) {
+                    if (n > (u32)(LCAP - 64)) {
                         if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
@@ -444,7 +600,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 template <int S, int K>
 __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, const u32* inbox, const u32* l_idx,
                                              u32 n) {
-    constexpr int NW = 2 * S + K, RW = NW + 6;
+    constexpr int NW = 2 * S + K, RW = NW + 2;
     wave_sync_lds();
     const int me = (int)__lane_id();
     u64 base = 0;
@@ -461,8 +617,9 @@ __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, 
         u32 m[K];
         load_state<S, K>(r, w, m);
         store_state<S, K>(B.store + ni * (u64)NW, w, m);
-        B.parent[ni] = (u64)r[NW + 2] | ((u64)r[NW + 3] << 32);
-        B.act[ni] = (uint8_t)r[NW + 4];
+        const u64 ref = (u64)r[NW] | ((u64)r[NW + 1] << 32);
+        B.parent[ni] = ref & ~(0xFFull << 40);
+        B.act[ni] = (uint8_t)(ref >> 40);
         const int v = check_invariants<S, K>(w, m, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
     }
@@ -471,7 +628,7 @@ __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, 
 
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_insert_remote(const Params P, const DevBufs B, const u32* inbox, u64 n) {
-    constexpr int NW = 2 * S + K, RW = NW + 6;
+    constexpr int NW = 2 * S + K, RW = NW + 2;
     __shared__ u32 s_idx[4][WCAP];
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
@@ -484,9 +641,10 @@ __global__ __launch_bounds__(256) void k_insert_remote(const Params P, const Dev
         const bool live = t < n;
         int is_new = 0;
         if (live) {
-            const u32* r = inbox + t * (u64)RW;
-            const u64 key = (u64)r[NW] | ((u64)r[NW + 1] << 32);
-            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+            u64 w[S];
+            u32 m[K];
+            load_state<S, K>(inbox + t * (u64)RW, w, m);
+            is_new = fp_insert(B.table, B.tmask, fp_of_materialised<S, K>(w, m, P), &B.ctr->table_full);
         }
         pr += (u64)__popcll(__ballot(live));
         const u64 bal = __ballot(is_new);
@@ -559,6 +717,7 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
 #pragma unroll
             for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
         }
+        key &= P.fp_mask;  // ~0 unless a verification test weakens the fingerprint
         key = key ? key : 1ull;
         // sharded mode: only the owner of an initial state stores it
         if (owner_state(key, w[0], w[1], B) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
@@ -717,22 +876,35 @@ static const u64 kExpandGrid = 2048;
 constexpr int kBatch = 8;
 
 template <int S, int K, bool SYM>
-static hipError_t launch_t(int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
-                           const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-    const u64 n = (which == 0 || which == 3) ? (b - a) : a;
+static hipError_t launch_t(int which, bool verify, const Params& P, const PermTable& PT, const DevBufs& B, u64 a,
+                           u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
+    const u64 n = (which == 0 || which == 3 || which == 5) ? (b - a) : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs
     const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
     if (which == 0) {
-        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        if constexpr (SYM) {
+            if (verify) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        } else if (verify) {
+            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+                               B, a, b);
+        } else {
+            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                               b);
+        }
     } else if (which == 3) {
         if constexpr (SYM) return hipErrorInvalidValue;  // sharded mode: no symmetry yet
         else hipLaunchKernelGGL((k_expand<S, K, false, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 4) {
         if constexpr (SYM) return hipErrorInvalidValue;
         else hipLaunchKernelGGL((k_insert_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, in, a);
+    } else if (which == 5) {
+        hipLaunchKernelGGL((k_publish<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
+    } else if (which == 6) {
+        hipLaunchKernelGGL((k_verify<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a);
     } else if (which == 1) {
         hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
     } else {
@@ -743,20 +915,22 @@ static hipError_t launch_t(int which, const Params& P, const PermTable& PT, cons
 }
 
 template <int S, int K>
-static hipError_t launch_sk(bool sym, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
-                            const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
+static hipError_t launch_sk(bool sym, bool verify, int which, const Params& P, const PermTable& PT, const DevBufs& B,
+                            u64 a, u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count,
+                            hipStream_t st) {
     if constexpr (S <= 4) {
-        if (sym) return launch_t<S, K, true>(which, P, PT, B, a, b, in, out, cap, count, st);
+        if (sym) return launch_t<S, K, true>(which, verify, P, PT, B, a, b, in, out, cap, count, st);
     } else {
         if (sym) return hipErrorInvalidValue;
     }
-    return launch_t<S, K, false>(which, P, PT, B, a, b, in, out, cap, count, st);
+    return launch_t<S, K, false>(which, verify, P, PT, B, a, b, in, out, cap, count, st);
 }
 
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-#define RMC_CASE(SS, KK) \
-    if (sh.S == SS && sh.K == KK) return launch_sk<SS, KK>(sh.sym, which, P, PT, B, a, b, in, out, cap, count, st);
+#define RMC_CASE(SS, KK)                                                                                      \
+    if (sh.S == SS && sh.K == KK)                                                                             \
+        return launch_sk<SS, KK>(sh.sym, sh.verify, which, P, PT, B, a, b, in, out, cap, count, st);
     RMC_CASE(2, 4) RMC_CASE(2, 8) RMC_CASE(3, 4) RMC_CASE(3, 8) RMC_CASE(4, 4) RMC_CASE(4, 8) RMC_CASE(5, 4)
     RMC_CASE(5, 8)
 #undef RMC_CASE

@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
 
 MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8
-FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM = 1, 2, 4
+FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES = 1, 2, 4, 8
 INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING = 1, 2, 4
 INV_NAMES = {INV_TYPEOK: "TypeOK", INV_ONE_LEADER: "OneLeaderPerTerm",
              INV_LOG_MATCHING: "LogMatching"}
@@ -40,7 +40,8 @@ class Result(C.Structure):
                 ("depth", C.c_int32), ("violated_inv", C.c_int32), ("violation_depth", C.c_int32),
                 ("deadlock", C.c_int32), ("collision_probability", C.c_double),
                 ("seconds", C.c_double), ("expand_kernel_seconds", C.c_double),
-                ("expand_launches", C.c_uint64), ("probes", C.c_uint64)]
+                ("expand_launches", C.c_uint64), ("probes", C.c_uint64),
+                ("collisions", C.c_uint64), ("verified", C.c_uint64)]
 
 
 class LevelStats(C.Structure):
@@ -99,7 +100,7 @@ EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_ru
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
            "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
            "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level",
-           "rmc_set_seed", "rmc_simulate", "rmc_sim_replay")
+           "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits")
 
 _lib = None
 
@@ -152,6 +153,8 @@ def native():
         lib.rmc_dist_end_level.restype = C.c_int
         lib.rmc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
         lib.rmc_set_seed.restype = C.c_int
+        lib.rmc_set_fp_bits.argtypes = [C.c_void_p, C.c_int32]
+        lib.rmc_set_fp_bits.restype = C.c_int
         lib.rmc_simulate.argtypes = [C.c_void_p, C.POINTER(SimConfig), C.POINTER(SimResult)]
         lib.rmc_simulate.restype = C.c_int
         lib.rmc_sim_replay.argtypes = [C.c_void_p, C.POINTER(SimConfig), C.c_uint64,
@@ -169,9 +172,9 @@ class RmcError(RuntimeError):
 
 def make_config(n_servers=3, n_values=2, max_term=2, max_log_len=1, max_msgs=2, max_dup=1,
                 symmetry=False, bug_quorum=False, invariants=INV_TYPEOK, check_deadlock=True,
-                device=0, max_depth=0, state_capacity=0):
+                device=0, max_depth=0, state_capacity=0, verify_states=False):
     flags = (FLAG_SYMMETRY if symmetry else 0) | (FLAG_BUG_QUORUM if bug_quorum else 0) | \
-        (FLAG_CHECK_DEADLOCK if check_deadlock else 0)
+        (FLAG_CHECK_DEADLOCK if check_deadlock else 0) | (FLAG_VERIFY_STATES if verify_states else 0)
     return Config(n_servers, n_values, max_term, max_log_len, max_msgs, max_dup, flags,
                   invariants, device, max_depth, state_capacity, 0)
 
@@ -252,6 +255,10 @@ class Checker:
         n = C.c_size_t()
         self._check(self.lib.rmc_sim_replay(self.ctx, C.byref(sc), behaviour, st, depth, C.byref(n)))
         return [st[k] for k in range(min(n.value, depth))]
+
+    def set_fp_bits(self, bits: int):
+        """Verification-mode test hook: keep only `bits` fingerprint bits (rmc_set_fp_bits)."""
+        self._check(self.lib.rmc_set_fp_bits(self.ctx, bits))
 
     def set_seed(self, seed: int):
         """Fingerprint salt for the next run (rmc_set_seed)."""

@@ -32,33 +32,65 @@ class DistResult:
     seconds: float = 0.0
     expand_kernel_seconds: float = 0.0
     records_sent: int = 0
+    chunks: int = 0
     levels: list = field(default_factory=list)
+    # host wall time per phase (s): expand (kernel + count readback), exchange
+    # (both all-to-alls), insert (kernel + readback), level (end-of-level stats)
+    phase: dict = field(default_factory=lambda: dict(expand=0.0, exchange=0.0, insert=0.0, level=0.0))
 
 
-def exchange(outbox: torch.Tensor, send_counts, group=None):
+def exchange(outbox: torch.Tensor, send_counts, group=None, more=None):
     """All-to-all of the first send_counts[d] records of outbox[d] to rank d
     (all_to_all_single with split sizes: one RCCL alltoallv).  Returns
-    (records received, contiguous in source-rank order; per-source counts).
-    On a gloo group the tensors travel through host memory."""
+    (records received, contiguous in source-rank order; per-source counts;
+    per-source `more` flags).  `more` (this rank still has frontier to expand)
+    rides along with the counts, so the chunk loop needs no extra collective
+    to agree on termination.  On a gloo group the tensors travel through host
+    memory.  On RCCL the received tensor is complete on return: the current
+    stream is synchronised, because librmc consumes it on its own stream."""
     world = dist.get_world_size(group)
     dev = outbox.device
     cpu = dist.get_backend(group) == "gloo"
     send = [int(x) for x in send_counts]
-    sc = torch.tensor(send, dtype=torch.int64)
+    flag = 1 if more is None else int(bool(more))
+    # per destination: [records for it, my `more` flag, my total records]; the
+    # totals tell every rank whether ANY rank sends, so all skip the payload
+    # collective together (a collective skipped by some ranks only deadlocks)
+    sc = torch.tensor([[c, flag, sum(send)] for c in send], dtype=torch.int64)
     rc = torch.empty_like(sc)
     if not cpu:
         sc, rc = sc.to(dev), rc.to(dev)
     dist.all_to_all_single(rc, sc, group=group)
-    rc = rc.cpu().tolist()
+    rcl = rc.cpu().tolist()
+    recv = [x[0] for x in rcl]
+    flags = [x[1] for x in rcl]
     rw = outbox.shape[-1]
+    if sum(x[2] for x in rcl) == 0:
+        return outbox.new_empty((0, rw)), recv, flags
     flat = torch.cat([outbox[d, :send[d]] for d in range(world)])
-    out = torch.empty((sum(rc), rw), dtype=outbox.dtype, device="cpu" if cpu else dev)
+    out = torch.empty((sum(recv), rw), dtype=outbox.dtype, device="cpu" if cpu else dev)
     if cpu:
         flat = flat.cpu()
-    dist.all_to_all_single(out, flat, output_split_sizes=rc, input_split_sizes=send, group=group)
-    if cpu and out.device != dev:
-        out = out.to(dev)
-    return out, rc
+    dist.all_to_all_single(out, flat, output_split_sizes=recv, input_split_sizes=send, group=group)
+    if cpu:
+        if out.device != dev:
+            out = out.to(dev)
+    else:
+        torch.cuda.current_stream(dev).synchronize()
+    return out, recv, flags
+
+
+def _allgather(vals, dev, cpu, group):
+    """One collective for a rank's small stats vector: returns [world][len]
+    (an all-reduce of a zero matrix holding this rank's row: gloo has no
+    all_gather_into_tensor)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    t = torch.zeros((world, len(vals)), dtype=torch.int64)
+    t[rank] = torch.tensor(vals, dtype=torch.int64)
+    if not cpu:
+        t = t.to(dev)
+    dist.all_reduce(t, group=group)
+    return t.cpu().tolist()
 
 
 def _allreduce(vals, op, dev, cpu, group):
@@ -92,21 +124,33 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
     done = C.c_int32()
     out5 = (C.c_uint64 * 5)()
     while True:
-        # ---- expand this level's frontier chunk by chunk, exchanging each chunk
+        # ---- expand this level's frontier chunk by chunk, exchanging each chunk;
+        # the chunk loop ends when no rank has frontier left (flags ride on the
+        # counts all-to-all)
+        ph = res.phase
         while True:
+            t1 = time.perf_counter()
             chk(lib.rmc_dist_expand(ctx, chunk_states, C.c_void_p(outbox.data_ptr()), cap_per_dest,
                                     send, C.byref(done)))
+            t2 = time.perf_counter()
             res.records_sent += sum(send)
-            received, rc = exchange(outbox, list(send), group)
+            res.chunks += 1
+            received, _rc, flags = exchange(outbox, list(send), group, more=not done.value)
+            t3 = time.perf_counter()
             if received.shape[0]:
                 chk(lib.rmc_dist_insert(ctx, C.c_void_p(received.data_ptr()), received.shape[0]))
-            more = _allreduce([0 if done.value else 1], dist.ReduceOp.SUM, dev, cpu, group)[0]
-            if more == 0:
+            t4 = time.perf_counter()
+            ph["expand"] += t2 - t1
+            ph["exchange"] += t3 - t2
+            ph["insert"] += t4 - t3
+            if not any(flags):
                 break
+        t1 = time.perf_counter()
         chk(lib.rmc_dist_end_level(ctx, out5))
-        new, gen, probes = _allreduce([out5[0], out5[1], out5[2]], dist.ReduceOp.SUM, dev, cpu,
-                                      group)
-        viol = _allreduce([out5[4]], dist.ReduceOp.MAX, dev, cpu, group)[0]
+        stats = _allgather([out5[0], out5[1], out5[2], out5[4]], dev, cpu, group)
+        ph["level"] += time.perf_counter() - t1
+        new, gen, probes = (sum(r[k] for r in stats) for k in range(3))
+        viol = max(r[3] for r in stats)
         res.generated += gen
         res.probes += probes
         res.levels.append(new)

@@ -33,9 +33,12 @@ def main():
     ap.add_argument("--capacity", type=int, default=0)
     ap.add_argument("--rerun", type=int, default=1)
     args = ap.parse_args()
+    dev = args.device if args.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "nccl":
+        import torch
+        torch.cuda.set_device(dev)
     dist.init_process_group(args.backend, init_method="env://")
     rank, world = dist.get_rank(), dist.get_world_size()
-    dev = args.device if args.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
     if args.case:
         g = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))[args.case]
         p = g["params"]
@@ -64,7 +67,7 @@ def main():
                        levels=r.levels, violated_inv=r.violated_inv,
                        violation_depth=r.violation_depth, records_sent=r.records_sent,
                        per_rank=per_rank, wall_s=wall,
-                       owner_mode=os.environ.get("RMC_OWNER", "1"),
+                       owner_mode=os.environ.get("RMC_OWNER", "2"),
                        rerun=[[x.distinct, x.generated, x.depth] for x in reruns]),
                   open(args.out, "w"))
     dist.destroy_process_group()

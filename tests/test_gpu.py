@@ -76,6 +76,40 @@ def test_fingerprint_salt_does_not_change_counts():
     assert levels == g["level_new"]
 
 
+@pytest.mark.parametrize("name", ["small", "s5_prefix9", "bug_log_matching", "bounded_full"])
+def test_full_state_verification_is_exact(name):
+    """RMC_FLAG_VERIFY_STATES: every fingerprint hit is compared with the stored
+    state; with 64-bit fingerprints no hit differs, so the counts are certified
+    exact (and equal the oracle's exact-state counts)."""
+    g = GOLDEN[name]
+    cfg = cfg_from(g["params"], capacity=max(1 << 22, int(g["distinct"] * 1.25)))
+    cfg.flags |= rmc.FLAG_VERIFY_STATES
+    res, levels, _ = run(cfg)
+    assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+    assert levels == g["level_new"]
+    assert res.collisions == 0
+    # every probe either inserted a new state or hit an existing one, and
+    # every hit was compared (initial state: inserted by the seed kernel)
+    assert res.verified == res.probes - (res.distinct - 1)
+
+
+@pytest.mark.parametrize("bits", [16, 20])
+def test_full_state_verification_reports_collisions(bits):
+    """A fingerprint cut to `bits` bits must collide on a 2.5 M-state model: the
+    search loses states (as TLC would, silently) and the verification reports
+    the colliding hits."""
+    g = GOLDEN["small"]
+    cfg = cfg_from(g["params"], capacity=1 << 22)
+    cfg.flags |= rmc.FLAG_VERIFY_STATES
+    with rmc.Checker(cfg) as ck:
+        ck.set_fp_bits(bits)
+        res = ck.run()
+    assert res.distinct <= 1 << bits
+    assert res.distinct < g["distinct"]
+    assert res.collisions > 0
+    assert res.verified == res.probes - (res.distinct - 1)
+
+
 @pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both"])
 def test_bug_variant_violation_and_trace(name):
     g = GOLDEN[name]
