@@ -360,8 +360,9 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         size_t fr = 0, tot = 0;
         (void)hipMemGetInfo(&fr, &tot);
         const u64 budget = (u64)((double)fr * 0.80);
-        cap = budget / (per_state + 32);  // table <= 4 slots per state after pow2 rounding
-        cap = std::min<u64>(cap, 1ull << 31);
+        // table <= 4 slots per state after pow2 rounding (+ as many sidx words when verifying)
+        cap = budget / (per_state + (c->sh.verify ? 64 : 32));
+        cap = std::min<u64>(cap, 1ull << 36);
     }
     cap = std::max<u64>(cap, 1024);
     u64 slots = 1;

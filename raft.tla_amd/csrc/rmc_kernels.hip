@@ -252,30 +252,30 @@ __device__ __forceinline__ bool same_state(const u64 (&w)[S], const u32 (&m)[K],
     return eq;
 }
 
+// Check one fingerprint hit: 0 = the stored state equals the successor,
+// 1 = it differs (a collision), 2 = the owner is not published yet (defer),
+// 3 = no slot (table full, flagged by the insert).  Counting and deferral are
+// aggregated by the caller (one atomic per wave, not per hit).
 template <int S, int K>
-__device__ __noinline__ void verify_hit(const u64 (&w)[S], const u32 (&m)[K], u64 parent, int lane, u64 slot,
-                                        const Params& P, const DevBufs& B) {
+__device__ __forceinline__ int verify_hit(const u64 (&w)[S], const u32 (&m)[K], int lane, u64 slot, const Params& P,
+                                       const DevBufs& B) {
     constexpr int NW = 2 * S + K;
-    const u64 ix = slot == ~0ull ? ~0ull : B.sidx[slot];
-    if (slot == ~0ull) return;  // table full (flagged by the insert)
-    if (ix == ~0ull) {          // owner found in this launch: check after it
-        const u64 q = atomicAdd((unsigned long long*)&B.ctr->vcount, 1ull);
-        if (q < B.vcap) {
-            B.vbuf[2 * q] = parent;
-            B.vbuf[2 * q + 1] = slot | ((u64)lane << 56);
-        } else {
-            atomicOr(&B.ctr->overflow, 4u);
-        }
-        return;
-    }
+    if (slot == ~0ull) return 3;
+    const u64 ix = B.sidx[slot];
+    if (ix == ~0ull) return 2;  // owner found in this launch: check after it
     Delta d;
     lane_delta<S, K>(w, m, lane, P, d);
     u64 wo[S];
     u32 mo[K];
     materialise<S, K>(w, m, d, wo, mo);
-    atomicAdd((unsigned long long*)&B.ctr->vchecked, 1ull);
-    if (!same_state<S, K>(wo, mo, B.store + ix * (u64)NW))
-        atomicAdd((unsigned long long*)&B.ctr->collisions, 1ull);
+    return same_state<S, K>(wo, mo, B.store + ix * (u64)NW) ? 0 : 1;
+}
+
+__device__ __forceinline__ u64 wave_sum64(u64 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v += (u64)(u32)__shfl_xor((int)(u32)v, off) | ((u64)(u32)__shfl_xor((int)(u32)(v >> 32), off) << 32);
+    return v;
 }
 
 template <int S, int K>
@@ -305,6 +305,7 @@ __global__ __launch_bounds__(256) void k_publish(const Params P, const DevBufs B
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_verify(const Params P, const DevBufs B, u64 n) {
     constexpr int NW = 2 * S + K;
+    u64 vchk = 0, vcol = 0;
     for (u64 q = (u64)blockIdx.x * 256ull + threadIdx.x; q < n; q += (u64)gridDim.x * 256ull) {
         const u64 parent = B.vbuf[2 * q], sl = B.vbuf[2 * q + 1];
         const u64 slot = sl & ((1ull << 56) - 1);
@@ -322,10 +323,13 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const DevBufs B,
             atomicOr(&B.ctr->overflow, 8u);
             continue;
         }
-        atomicAdd((unsigned long long*)&B.ctr->vchecked, 1ull);
-        if (!same_state<S, K>(wo, mo, B.store + ix * (u64)NW))
-            atomicAdd((unsigned long long*)&B.ctr->collisions, 1ull);
+        ++vchk;
+        vcol += same_state<S, K>(wo, mo, B.store + ix * (u64)NW) ? 0u : 1u;
     }
+    vchk = wave_sum64(vchk);
+    vcol = wave_sum64(vcol);
+    if (__lane_id() == 0 && vchk) atomicAdd((unsigned long long*)&B.ctr->vchecked, (unsigned long long)vchk);
+    if (__lane_id() == 0 && vcol) atomicAdd((unsigned long long*)&B.ctr->collisions, (unsigned long long)vcol);
 }
 
 // Owner rank of a state in sharded mode.  Mode 0: by fingerprint.  Mode 1: by
@@ -463,6 +467,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
     uint8_t* l_dest = s_dest[DIST ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u64 gen = 0;
+    u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
     const u64 nf = hi - lo;
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
@@ -520,11 +525,15 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
             for (int b = 0; b < BATCH; ++b) pr += (u64)__popcll(__ballot(key[b] != 0));  // wave-uniform
             // (c) resolve: hit -> duplicate; empty -> CAS; mismatch -> slow path
             u32 newbits = 0, slowbits = 0;
+            u32 hitbits = 0;  // verification: probes that found their key (slot parked in s_key)
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
                 if (!key[b]) continue;
                 if (cur[b] == key[b]) {
-                    if constexpr (VERIFY) verify_hit<S, K>(w, m, lo + rel, lane0 + b, key[b] & B.tmask, P, B);
+                    if constexpr (VERIFY) {
+                        hitbits |= 1u << b;
+                        s_key[b][threadIdx.x] = key[b] & B.tmask;  // the slot that holds the key
+                    }
                     continue;
                 }
                 if constexpr (DIST) {
@@ -539,7 +548,10 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                                                (unsigned long long)key[b]);
                     if (prev == 0) newbits |= 1u << b;
                     else if (prev != key[b]) slowbits |= 1u << b;
-                    else if constexpr (VERIFY) verify_hit<S, K>(w, m, lo + rel, lane0 + b, key[b] & B.tmask, P, B);
+                    else if constexpr (VERIFY) {
+                        hitbits |= 1u << b;
+                        s_key[b][threadIdx.x] = key[b] & B.tmask;
+                    }
                 } else {
                     slowbits |= 1u << b;
                 }
@@ -549,12 +561,44 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
                 slowbits &= slowbits - 1;
                 if constexpr (VERIFY) {
                     u64 at = 0;
-                    if (fp_insert_at(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full, &at))
+                    if (fp_insert_at(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full, &at)) {
                         newbits |= 1u << b;
-                    else
-                        verify_hit<S, K>(w, m, lo + rel, lane0 + b, at, P, B);
+                    } else {
+                        hitbits |= 1u << b;
+                        s_key[b][threadIdx.x] = at;  // the slot that holds the key
+                    }
                 } else if (fp_insert(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full)) {
                     newbits |= 1u << b;
+                }
+            }
+            if constexpr (VERIFY) {
+                // compare each hit with the stored owner of its slot (parked in s_key)
+                u32 defbits = 0;
+                for (int b = 0; b < BATCH; ++b) {  // rolled: one inlined copy of the check
+                    if (!((hitbits >> b) & 1u)) continue;
+                    const int r = verify_hit<S, K>(w, m, lane0 + b, s_key[b][threadIdx.x], P, B);
+                    vchk += (u64)(r <= 1);
+                    vcol += (u64)(r == 1);
+                    defbits |= (u32)(r == 2) << b;
+                }
+                // defer hits on owners not yet published (one atomic per wave and probe batch)
+                for (int b = 0; b < BATCH; ++b) {
+                    const bool def = (defbits >> b) & 1u;
+                    const u64 bal = __ballot(def);
+                    if (!bal) continue;
+                    const int leader = __ffsll((long long)bal) - 1;
+                    u64 q0 = 0;
+                    if (me == leader) q0 = atomicAdd((unsigned long long*)&B.ctr->vcount, (unsigned long long)__popcll(bal));
+                    q0 = bcast64(q0, leader);
+                    if (def) {
+                        const u64 q = q0 + (u64)__popcll(bal & lt_mask);
+                        if (q < B.vcap) {
+                            B.vbuf[2 * q] = lo + rel;
+                            B.vbuf[2 * q + 1] = s_key[b][threadIdx.x] | ((u64)(lane0 + b) << 56);
+                        } else {
+                            atomicOr(&B.ctr->overflow, 4u);
+                        }
+                    }
                 }
             }
             // (d) list the winners (wave-aggregated, no global atomics)
@@ -591,6 +635,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
         gs += (u64)(u32)__shfl_xor((int)(u32)gs, off) | ((u64)(u32)__shfl_xor((int)(u32)(gs >> 32), off) << 32);
     if (me == 0 && gs) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)gs);
     if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+    if constexpr (VERIFY) {
+        vchk = wave_sum64(vchk);
+        vcol = wave_sum64(vcol);
+        if (me == 0 && vchk) atomicAdd((unsigned long long*)&B.ctr->vchecked, (unsigned long long)vchk);
+        if (me == 0 && vcol) atomicAdd((unsigned long long*)&B.ctr->collisions, (unsigned long long)vcol);
+    }
 }
 
 // Sharded mode, owner side: insert the n records received from other ranks
