@@ -233,8 +233,10 @@ int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, r
 
 /* ---- sharded BFS over several GPUs (one process per GPU) --------------------
  * Replaces TLC's distributed mode (TLCServer/TLCWorker with a partitioned
- * FPSet).  Fingerprints are owned by rank
- * ((fp >> 32) * world) >> 32; each rank stores and expands the states it owns.
+ * FPSet).  A state is owned by the rank given by a hash
+ * of its servers 0 and 1 words (RMC_OWNER=2, default; 1: server 0's word only;
+ * 0: by fingerprint, ((fp >> 32) * world) >> 32); each rank stores and expands
+ * the states it owns.
  * Per level, every rank runs:
  *   loop { rmc_dist_expand(chunk) -> per-destination record counts;
  *          host all-to-all of counts and records (torch.distributed / RCCL);
@@ -251,6 +253,14 @@ int rmc_dist_expand(rmc_ctx* ctx, uint64_t max_states, uint32_t* outbox, uint64_
                     uint64_t* send_counts, int32_t* frontier_done);
 int rmc_dist_insert(rmc_ctx* ctx, const uint32_t* inbox, uint64_t n_records);
 int rmc_dist_end_level(rmc_ctx* ctx, uint64_t* out5);
+/* Trace reconstruction across ranks (TLC's distributed mode rebuilds the
+ * counterexample from the workers' parent fingerprints): the state this rank
+ * stores at `index`, the action family and lane of the step into it (-1 for an
+ * initial state) and its parent's global reference (rank << 48 | index on that
+ * rank; ~0 for an initial state).  out5[3] of rmc_dist_end_level is 1 + the
+ * index of a violating state.  The host walks the chain rank by rank. */
+int rmc_dist_state(rmc_ctx* ctx, uint64_t index, rmc_state_view* state, int32_t* family,
+                   int32_t* instance, uint64_t* parent_ref);
 
 /* ---- roofline microbenchmark -----------------------------------------------
  * Random 8-byte accesses into a table of table_bytes on `device`, 8 in flight

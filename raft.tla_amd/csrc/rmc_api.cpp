@@ -904,6 +904,25 @@ int rmc_dist_insert(rmc_ctx* c, const uint32_t* inbox, uint64_t n_records) {
     return 0;
 }
 
+int rmc_dist_state(rmc_ctx* c, uint64_t index, rmc_state_view* state, int32_t* family, int32_t* instance,
+                   uint64_t* parent_ref) {
+    if (!c || !c->dist) return RMC_E_INVAL;
+    if (c->level_start.empty() || index >= c->level_start.back())
+        return fail(c, RMC_E_INVAL, "rmc_dist_state: index beyond the stored states");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    std::vector<u32> buf((size_t)c->NW);
+    u64 p = 0;
+    uint8_t a = 0;
+    HIPCHK(c, hipMemcpy(buf.data(), c->B.store + index * (u64)c->NW, buf.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&p, c->B.parent + index, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&a, c->B.act + index, 1, hipMemcpyDeviceToHost));
+    if (state) decode_state(c, buf.data(), state);
+    if (family) *family = family_of(c->P, a);
+    if (instance) *instance = a == 255 ? -1 : a;
+    if (parent_ref) *parent_ref = p;
+    return 0;
+}
+
 // Closes the current level on this rank.  out[0..4] = new states stored here
 // (the next local frontier), successors generated here, probes, 1 + index of
 // a violating state (0 = none), violated invariant bit.

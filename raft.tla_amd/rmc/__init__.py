@@ -99,7 +99,7 @@ PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.POINTER(LevelStats), C.c_void_p)
 EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_run_bfs",
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
            "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
-           "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level",
+           "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level", "rmc_dist_state",
            "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits")
 
 _lib = None
@@ -151,6 +151,9 @@ def native():
         lib.rmc_dist_insert.restype = C.c_int
         lib.rmc_dist_end_level.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         lib.rmc_dist_end_level.restype = C.c_int
+        lib.rmc_dist_state.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(StateView), C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+        lib.rmc_dist_state.restype = C.c_int
         lib.rmc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
         lib.rmc_set_seed.restype = C.c_int
         lib.rmc_set_fp_bits.argtypes = [C.c_void_p, C.c_int32]

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
-from . import Checker, RmcError
+from . import Checker, RmcError, StateView
 
 
 @dataclass
@@ -34,6 +34,9 @@ class DistResult:
     records_sent: int = 0
     chunks: int = 0
     levels: list = field(default_factory=list)
+    # counterexample on a violation: [(family, lane, StateView)] from Init to the
+    # violating state, gathered across ranks (identical on every rank)
+    trace: list = field(default_factory=list)
     # host wall time per phase (s): expand (kernel + count readback), exchange
     # (both all-to-alls), insert (kernel + readback), level (end-of-level stats)
     phase: dict = field(default_factory=lambda: dict(expand=0.0, exchange=0.0, insert=0.0, level=0.0))
@@ -99,6 +102,48 @@ def _allreduce(vals, op, dev, cpu, group):
     return t.cpu().tolist()
 
 
+def trace(ck: Checker, rank0: int, index0: int, group=None) -> list:
+    """Collective: the chain of parents from state `index0` on rank `rank0`
+    back to an initial state.  Each step, the rank holding the current state
+    broadcasts it (decoded view, family, lane, parent's global ref); the
+    parent ref names the next rank.  Returns [(family, lane, StateView)] in
+    behaviour order, on every rank."""
+    lib, ctx = ck.lib, ck.ctx
+    rank = dist.get_rank(group)
+    cpu = dist.get_backend(group) == "gloo"
+    dev = torch.device("cuda", ck.cfg.device)
+    nb = C.sizeof(StateView)
+    hdr = 3  # family, lane, parent ref (int64 each)
+    nwords = hdr + (nb + 7) // 8
+    chain = []
+    owner, idx = rank0, index0
+    for _ in range(1 << 16):
+        t = torch.zeros(nwords, dtype=torch.int64)
+        if rank == owner:
+            sv = StateView()
+            fam, inst, pref = C.c_int32(), C.c_int32(), C.c_uint64()
+            rc = lib.rmc_dist_state(ctx, idx, C.byref(sv), C.byref(fam), C.byref(inst), C.byref(pref))
+            if rc:
+                raise RmcError(rc, lib.rmc_last_error(ctx).decode())
+            t[0], t[1] = fam.value, inst.value
+            t[2] = pref.value - (1 << 64) if pref.value >= 1 << 63 else pref.value
+            raw = bytearray(nb + (-nb) % 8)
+            C.memmove((C.c_char * nb).from_buffer(raw), C.byref(sv), nb)
+            t[hdr:] = torch.frombuffer(raw, dtype=torch.int64)
+        if not cpu:
+            t = t.to(dev)
+        dist.broadcast(t, src=dist.get_global_rank(group, owner) if group is not None else owner, group=group)
+        t = t.cpu()
+        sv = StateView.from_buffer_copy(t[hdr:].numpy().tobytes()[:nb])
+        chain.append((int(t[0]), int(t[1]), sv))
+        pref = int(t[2]) & 0xFFFFFFFFFFFFFFFF
+        if pref == 0xFFFFFFFFFFFFFFFF:
+            break
+        owner, idx = pref >> 48, pref & ((1 << 48) - 1)
+    chain.reverse()
+    return chain
+
+
 def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slots=1 << 26,
         group=None, init=True) -> DistResult:
     """Collective: every rank calls it with its own Checker (one GPU each)."""
@@ -147,7 +192,7 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
                 break
         t1 = time.perf_counter()
         chk(lib.rmc_dist_end_level(ctx, out5))
-        stats = _allgather([out5[0], out5[1], out5[2], out5[4]], dev, cpu, group)
+        stats = _allgather([out5[0], out5[1], out5[2], out5[4], out5[3]], dev, cpu, group)
         ph["level"] += time.perf_counter() - t1
         new, gen, probes = (sum(r[k] for r in stats) for k in range(3))
         viol = max(r[3] for r in stats)
@@ -157,8 +202,12 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
         if new:
             depth += 1
         if viol:
-            res.violated_inv = viol
+            # every violating state of this level has the minimal depth: trace the
+            # one of the lowest rank that found one
+            vr = min(q for q, r in enumerate(stats) if r[3])
+            res.violated_inv = stats[vr][3]
             res.violation_depth = depth
+            res.trace = trace(ck, vr, stats[vr][4] - 1, group)
             break
         if new == 0:
             break

@@ -138,3 +138,20 @@ def random_state(model, rng: random.Random):
         nextIndex=tuple(tuple(rng.randint(1, L + 1) for _ in range(S)) for _ in range(S)),
         matchIndex=tuple(tuple(rng.randint(0, L) for _ in range(S)) for _ in range(S)),
     )
+
+
+def check_trace(model, trace, violated_inv, violation_depth):
+    """A counterexample [(family, lane, StateView)] must be a behaviour of the
+    spec (Python restatement) from Init to a state violating `violated_inv`,
+    every earlier state satisfying it, of length `violation_depth`."""
+    import rmc
+    assert len(trace) == violation_depth
+    states = [from_view(v) for _f, _i, v in trace]
+    assert states[0] == R.init_state(model) and trace[0][0] == -1
+    for a, b, (fam, _inst, _v) in zip(states, states[1:], trace[1:]):
+        succ = {(f, t) for f, _p, t in R.successors(model, a)}
+        assert (rmc.FAMILIES[fam], b) in succ
+        assert R.in_constraint(model, b)
+    inv = {rmc.INV_ONE_LEADER: R.one_leader_per_term, rmc.INV_LOG_MATCHING: R.log_matching}
+    assert not inv[violated_inv](model, states[-1])
+    assert all(inv[violated_inv](model, s) for s in states[:-1])

@@ -59,6 +59,13 @@ def main():
         local = ck.result()
         reruns = [rdist.run(ck, chunk_states=args.chunk, cap_per_dest=args.cap_per_dest, init=False)
                   for _ in range(args.rerun)]
+        # the trace is identical on every rank (it is broadcast step by step)
+        if r.trace:
+            mine = [[f, i, bytes(v).hex()] for f, i, v in r.trace]
+            allt = [None] * world
+            dist.all_gather_object(allt, mine)
+            assert all(t == mine for t in allt), "ranks disagree on the trace"
+
     per_rank = [None] * world
     dist.all_gather_object(per_rank, dict(rank=rank, distinct=local.distinct,
                                           records_sent=r.records_sent))
@@ -67,6 +74,7 @@ def main():
                        levels=r.levels, violated_inv=r.violated_inv,
                        violation_depth=r.violation_depth, records_sent=r.records_sent,
                        per_rank=per_rank, wall_s=wall,
+                       trace=[[f, i, bytes(v).hex()] for f, i, v in r.trace],
                        owner_mode=os.environ.get("RMC_OWNER", "2"),
                        rerun=[[x.distinct, x.generated, x.depth] for x in reruns]),
                   open(args.out, "w"))

@@ -12,6 +12,10 @@ import sys
 
 import pytest
 
+import rmc
+from oracle import raft_spec as R
+from tests.convert import check_trace
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))
 
@@ -81,3 +85,27 @@ def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
     assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
     assert res["records_sent"] > 0 or nproc == 1
     assert sum(p["distinct"] for p in res["per_rank"]) == g["distinct"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,nproc", [("bug_one_leader", 2), ("bug_log_matching", 3), ("bug_both", 2)])
+def test_sharded_violation_and_trace(case, nproc, tmp_path):
+    """Bug variant (config 5) on N ranks: the violation, its minimal depth and the
+    counts at the stopping level equal the oracle's, and the counterexample,
+    gathered rank by rank through the global parent refs, is a behaviour of the
+    spec ending in a violating state (SURVEY.md §8e "Trace")."""
+    g = GOLDEN[case]
+    p = g["params"]
+    out = tmp_path / "r.json"
+    r = _torchrun(nproc, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out",
+                          str(out), "--device", "0", "--backend", "gloo"], 29640 + nproc)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert res["violated_inv"] == g["violated_inv"]
+    assert res["violation_depth"] == g["violation_depth"]
+    assert res["distinct"] == g["distinct"] and res["generated"] == g["generated"]
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
+                    bug_quorum=True)
+    trace = [(f, i, rmc.StateView.from_buffer_copy(bytes.fromhex(h))) for f, i, h in res["trace"]]
+    check_trace(model, trace, res["violated_inv"], res["violation_depth"])

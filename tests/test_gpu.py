@@ -12,7 +12,7 @@ import pytest
 
 import rmc
 from oracle import raft_spec as R
-from tests.convert import from_view, random_state, to_view
+from tests.convert import check_trace, from_view, random_state, to_view
 
 pytestmark = pytest.mark.gpu
 
@@ -122,16 +122,7 @@ def test_bug_variant_violation_and_trace(name):
     model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
                     max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
                     bug_quorum=True)
-    assert len(trace) == res.violation_depth
-    states = [from_view(v) for _f, _i, v in trace]
-    assert states[0] == R.init_state(model) and trace[0][0] == -1
-    for a, b, (fam, _inst, _v) in zip(states, states[1:], trace[1:]):
-        succ = {(f, t) for f, _p, t in R.successors(model, a)}
-        assert (rmc.FAMILIES[fam], b) in succ
-        assert R.in_constraint(model, b)
-    inv = {rmc.INV_ONE_LEADER: R.one_leader_per_term, rmc.INV_LOG_MATCHING: R.log_matching}
-    assert not inv[res.violated_inv](model, states[-1])
-    assert all(inv[res.violated_inv](model, s) for s in states[:-1])
+    check_trace(model, trace, res.violated_inv, res.violation_depth)
 
 
 FUZZ = [
