@@ -807,7 +807,6 @@ int rmc_sim_replay(rmc_ctx* c, const rmc_sim_config* sc, uint64_t behaviour, rmc
 int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_slots) {
     if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return RMC_E_INVAL;
     if (c->sh.verify) return fail(c, RMC_E_INVAL, "sharded mode does not support full-state verification yet");
-    if (c->sh.sym) return fail(c, RMC_E_INVAL, "sharded mode does not support SYMMETRY yet");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     u64 slots = 1;
     while (slots < std::max<u64>(sent_cache_slots, 1024)) slots <<= 1;
@@ -829,6 +828,9 @@ int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_s
     c->B.ref_tag = (u64)rank << 48;
     const char* om = getenv("RMC_OWNER");  // partition: 0 fingerprint, 1 server-0 word, 2 servers 0+1
     c->B.owner_mode = om ? (u32)std::min(2, std::max(0, atoi(om))) : 2u;
+    // SYMMETRY: the states of one orbit must meet at one owner, so the owner is
+    // a function of the canonical fingerprint (server words differ across the orbit)
+    if (c->sh.sym) c->B.owner_mode = 0;
     c->dist = 1;
     return 0;
 }

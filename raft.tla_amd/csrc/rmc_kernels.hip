@@ -676,9 +676,12 @@ __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, 
     wave_sync_lds();
 }
 
-template <int S, int K>
-__global__ __launch_bounds__(256) void k_insert_remote(const Params P, const DevBufs B, const u32* inbox, u64 n) {
+// SYM: the key is the canonical (least permuted) fingerprint, as k_expand's.
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_insert_remote(const Params P, const PermTable PT, const DevBufs B,
+                                                       const u32* inbox, u64 n) {
     constexpr int NW = 2 * S + K, RW = NW + 2;
+    constexpr int NP = SYM ? NPerm<S>::v : 1;
     __shared__ u32 s_idx[4][WCAP];
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
@@ -694,7 +697,16 @@ __global__ __launch_bounds__(256) void k_insert_remote(const Params P, const Dev
             u64 w[S];
             u32 m[K];
             load_state<S, K>(inbox + t * (u64)RW, w, m);
-            is_new = fp_insert(B.table, B.tmask, fp_of_materialised<S, K>(w, m, P), &B.ctr->table_full);
+            u64 key = fp_of_materialised<S, K>(w, m, P);
+            if constexpr (SYM) {
+                u64 hp[NP];
+                perm_fps<S, K, NP>(w, m, PT, hp);
+                key = ~0ull;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
+                key = key ? key : 1ull;
+            }
+            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
         }
         pr += (u64)__popcll(__ballot(live));
         const u64 bal = __ballot(is_new);
@@ -946,11 +958,9 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                b);
         }
     } else if (which == 3) {
-        if constexpr (SYM) return hipErrorInvalidValue;  // sharded mode: no symmetry yet
-        else hipLaunchKernelGGL((k_expand<S, K, false, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 4) {
-        if constexpr (SYM) return hipErrorInvalidValue;
-        else hipLaunchKernelGGL((k_insert_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, in, a);
+        hipLaunchKernelGGL((k_insert_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
     } else if (which == 5) {
         hipLaunchKernelGGL((k_publish<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
     } else if (which == 6) {

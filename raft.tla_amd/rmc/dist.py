@@ -31,6 +31,7 @@ class DistResult:
     violation_depth: int = 0
     seconds: float = 0.0
     expand_kernel_seconds: float = 0.0
+    left_on_queue: int = 0
     records_sent: int = 0
     chunks: int = 0
     levels: list = field(default_factory=list)
@@ -168,7 +169,11 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
     send = (C.c_uint64 * world)()
     done = C.c_int32()
     out5 = (C.c_uint64 * 5)()
+    max_depth = ck.cfg.max_depth
     while True:
+        if max_depth > 0 and depth >= max_depth:  # level `depth` stays unexpanded (rmc_run_bfs)
+            res.left_on_queue = res.levels[-1] if res.levels else 1
+            break
         # ---- expand this level's frontier chunk by chunk, exchanging each chunk;
         # the chunk loop ends when no rank has frontier left (flags ride on the
         # counts all-to-all)

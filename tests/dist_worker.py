@@ -45,7 +45,8 @@ def main():
         cfg = rmc.make_config(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
                               max_log_len=p["max_log_len"], max_msgs=p["max_msgs"],
                               max_dup=p["max_dup"], bug_quorum=bool(p["bug_quorum"]),
-                              invariants=p["invariants"], device=dev,
+                              invariants=p["invariants"], device=dev, symmetry=bool(p["symmetry"]),
+                              max_depth=p["max_depth"],
                               state_capacity=args.capacity or max(1 << 20, g["distinct"]))
     else:
         cfg = rmc.config_from_files(args.cfg)
@@ -71,6 +72,7 @@ def main():
                                           records_sent=r.records_sent))
     if rank == 0:
         json.dump(dict(distinct=r.distinct, generated=r.generated, depth=r.depth,
+                       left_on_queue=r.left_on_queue,
                        levels=r.levels, violated_inv=r.violated_inv,
                        violation_depth=r.violation_depth, records_sent=r.records_sent,
                        per_rank=per_rank, wall_s=wall,

@@ -66,13 +66,15 @@ def test_exchange_protocol_gloo_world2(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,nproc,backend", [("tiny2_v2", 2, "gloo"), ("small", 2, "gloo"),
                                                 ("small", 4, "gloo"), ("s5_prefix9", 2, "gloo"),
+                                                ("small_sym", 2, "gloo"), ("bounded_sym_prefix16", 3, "gloo"),
+                                                ("msgs5_dup2_prefix9", 2, "gloo"), ("s4_prefix10", 3, "gloo"),
                                                 ("small", 1, "nccl")])
 def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
     """gloo: N ranks share the box's one GPU.  nccl: one rank through RCCL, the
-    code path of the driver's multi-GPU bench (device tensors, stream sync)."""
+    code path of the driver's multi-GPU bench (device tensors, stream sync).
+    SYMMETRY cases route by the canonical fingerprint; depth-bounded cases stop
+    with the last level unexpanded, as rmc_run_bfs."""
     g = GOLDEN[case]
-    if g["params"]["max_depth"]:
-        pytest.skip("sharded runs go to fixpoint")
     out = tmp_path / "r.json"
     r = _torchrun(nproc, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out",
                           str(out), "--device", "0", "--backend", backend], 29620 + nproc)
@@ -81,6 +83,7 @@ def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
     assert res["distinct"] == g["distinct"]
     assert res["generated"] == g["generated"]
     assert res["depth"] == g["depth"]
+    assert res["left_on_queue"] == g["left_on_queue"]
     assert [1] + [x for x in res["levels"] if x] == g["level_new"]
     assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
     assert res["records_sent"] > 0 or nproc == 1
