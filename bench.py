@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK (one GPU per rank)")
     ap.add_argument("--chunk", type=int, default=1 << 24, help="frontier states per exchange")
-    ap.add_argument("--cap-per-dest", type=int, default=1 << 24, help="outbox records per rank")
+    ap.add_argument("--cap-per-dest", type=int, default=1 << 25, help="outbox records per destination rank")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the sharded path even at one rank (measures its overhead)")
     ap.add_argument("--no-probe-ceiling", action="store_true",
@@ -202,6 +202,7 @@ def main():
     if sharded:
         ld = last_dist[0]
         out["sharded"] = {"chunks_per_step": ld.chunks, "records_sent_rank0": ld.records_sent,
+                          "max_records_per_dest_per_state": round(ld.max_dest_per_state, 4),
                           "phase_s_rank0": {k: round(v, 6) for k, v in ld.phase.items()},
                           "chunk_states": a.chunk, "cap_per_dest": a.cap_per_dest}
         out["roofline"]["note"] = "per-rank kernel time of rank 0; achieved is rank 0's share"

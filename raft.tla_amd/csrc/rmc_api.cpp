@@ -856,6 +856,7 @@ int rmc_dist_start(rmc_ctx* c) {
     HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
     if (int rc = read_counters(c)) return rc;
     c->res.generated = c->B.rank == 0 ? 1 : 0;  // the initial state is counted once, globally
+    c->res.distinct = c->h_ctr->count;         // initial states stored on this rank (its first frontier)
     c->level_start.push_back(0);
     c->level_start.push_back(c->h_ctr->count);
     c->cursor = 0;

@@ -33,6 +33,7 @@ class DistResult:
     expand_kernel_seconds: float = 0.0
     left_on_queue: int = 0
     records_sent: int = 0
+    max_dest_per_state: float = 0.0  # most records for one destination per expanded state
     chunks: int = 0
     levels: list = field(default_factory=list)
     # counterexample on a violation: [(family, lane, StateView)] from Init to the
@@ -43,45 +44,62 @@ class DistResult:
     phase: dict = field(default_factory=lambda: dict(expand=0.0, exchange=0.0, insert=0.0, level=0.0))
 
 
-def exchange(outbox: torch.Tensor, send_counts, group=None, more=None):
-    """All-to-all of the first send_counts[d] records of outbox[d] to rank d
-    (all_to_all_single with split sizes: one RCCL alltoallv).  Returns
-    (records received, contiguous in source-rank order; per-source counts;
-    per-source `more` flags).  `more` (this rank still has frontier to expand)
-    rides along with the counts, so the chunk loop needs no extra collective
-    to agree on termination.  On a gloo group the tensors travel through host
-    memory.  On RCCL the received tensor is complete on return: the current
-    stream is synchronised, because librmc consumes it on its own stream."""
-    world = dist.get_world_size(group)
-    dev = outbox.device
-    cpu = dist.get_backend(group) == "gloo"
-    send = [int(x) for x in send_counts]
-    flag = 1 if more is None else int(bool(more))
-    # per destination: [records for it, my `more` flag, my total records]; the
-    # totals tell every rank whether ANY rank sends, so all skip the payload
-    # collective together (a collective skipped by some ranks only deadlocks)
-    sc = torch.tensor([[c, flag, sum(send)] for c in send], dtype=torch.int64)
+def exchange_counts(send, more, dev, cpu, group=None):
+    """All-to-all of the per-destination record counts.  Per destination d the
+    row is [records for d, my `more` flag, my total records]: `more` (this rank
+    still has frontier to expand) rides along so the chunk loop needs no extra
+    collective to agree on termination, and the totals tell every rank whether
+    ANY rank sends, so all skip the payload collective together (a collective
+    skipped by some ranks only deadlocks).  Returns (recv counts, flags, any)."""
+    sc = torch.tensor([[c, int(bool(more)), sum(send)] for c in send], dtype=torch.int64)
     rc = torch.empty_like(sc)
     if not cpu:
         sc, rc = sc.to(dev), rc.to(dev)
     dist.all_to_all_single(rc, sc, group=group)
     rcl = rc.cpu().tolist()
-    recv = [x[0] for x in rcl]
-    flags = [x[1] for x in rcl]
+    return [x[0] for x in rcl], [x[1] for x in rcl], sum(x[2] for x in rcl) > 0
+
+
+def payload_start(outbox: torch.Tensor, send, recv, cpu, group=None):
+    """Start the all-to-all of the first send[d] records of outbox[d] to rank d
+    (all_to_all_single with split sizes: one RCCL alltoallv).  On RCCL the
+    collective is asynchronous, so the caller can expand the next chunk into
+    the other outbox meanwhile.  Returns a handle for payload_finish."""
+    world = outbox.shape[0]
     rw = outbox.shape[-1]
-    if sum(x[2] for x in rcl) == 0:
-        return outbox.new_empty((0, rw)), recv, flags
     flat = torch.cat([outbox[d, :send[d]] for d in range(world)])
-    out = torch.empty((sum(recv), rw), dtype=outbox.dtype, device="cpu" if cpu else dev)
-    if cpu:
-        flat = flat.cpu()
-    dist.all_to_all_single(out, flat, output_split_sizes=recv, input_split_sizes=send, group=group)
-    if cpu:
-        if out.device != dev:
-            out = out.to(dev)
-    else:
-        torch.cuda.current_stream(dev).synchronize()
-    return out, recv, flags
+    out = torch.empty((sum(recv), rw), dtype=outbox.dtype, device="cpu" if cpu else outbox.device)
+    if cpu:  # gloo: through host memory, synchronously
+        dist.all_to_all_single(out, flat.cpu(), output_split_sizes=recv, input_split_sizes=list(send),
+                               group=group)
+        return (None, out.to(outbox.device), flat)
+    work = dist.all_to_all_single(out, flat, output_split_sizes=recv, input_split_sizes=list(send),
+                                  group=group, async_op=True)
+    return (work, out, flat)
+
+
+def payload_finish(handle):
+    """Wait for payload_start's collective.  On RCCL the received tensor is
+    complete on return: the current stream is synchronised, because librmc
+    consumes it on its own stream."""
+    work, out, _flat = handle
+    if work is not None:
+        work.wait()
+        torch.cuda.current_stream(out.device).synchronize()
+    return out
+
+
+def exchange(outbox: torch.Tensor, send_counts, group=None, more=None):
+    """One synchronous exchange (counts, then records); returns (records
+    received, contiguous in source-rank order; per-source counts; per-source
+    `more` flags).  The BFS loop uses the split, pipelined form."""
+    dev = outbox.device
+    cpu = dist.get_backend(group) == "gloo"
+    send = [int(x) for x in send_counts]
+    recv, flags, anyone = exchange_counts(send, True if more is None else more, dev, cpu, group)
+    if not anyone:
+        return outbox.new_empty((0, outbox.shape[-1])), recv, flags
+    return payload_finish(payload_start(outbox, send, recv, cpu, group)), recv, flags
 
 
 def _allgather(vals, dev, cpu, group):
@@ -160,7 +178,9 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
     if init:
         chk(lib.rmc_dist_init(ctx, rank, world, sent_cache_slots))
     rw = lib.rmc_dist_record_words(ctx)
-    outbox = torch.empty((world, cap_per_dest, rw), dtype=torch.int32, device=dev)
+    # two outboxes: chunk k+1 is expanded into one while chunk k's records
+    # leave from the other (RCCL all-to-all overlapped with k_expand)
+    outboxes = [torch.empty((world, cap_per_dest, rw), dtype=torch.int32, device=dev) for _ in range(2)]
     res = DistResult()
     t0 = time.perf_counter()
     chk(lib.rmc_dist_start(ctx))
@@ -170,33 +190,64 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
     done = C.c_int32()
     out5 = (C.c_uint64 * 5)()
     max_depth = ck.cfg.max_depth
+    # adaptive chunk (states per expansion): start where even one record per
+    # state for one destination fits, then track the observed ratio
+    cur_chunk = int(min(chunk_states, cap_per_dest // 2))
+    # this rank's share of the first level: the initial state lives on its owner
+    local_frontier, consumed = int(ck.result().distinct), 0
+    ph = res.phase
+
+    def expand(ob):
+        """Expand this rank's next chunk into outbox `ob`; returns the send counts."""
+        nonlocal consumed, cur_chunk
+        t1 = time.perf_counter()
+        n_exp = min(cur_chunk, local_frontier - consumed)
+        chk(lib.rmc_dist_expand(ctx, cur_chunk, C.c_void_p(outboxes[ob].data_ptr()), cap_per_dest,
+                                send, C.byref(done)))
+        ph["expand"] += time.perf_counter() - t1
+        snd = [int(x) for x in send]
+        consumed += max(n_exp, 0)
+        res.records_sent += sum(snd)
+        res.chunks += 1
+        if n_exp > 0:
+            # keep the fullest outbox at <= half its capacity (an overflow is an
+            # error: dropped records would be lost states)
+            rho = max(max(snd), 1) / n_exp
+            res.max_dest_per_state = max(res.max_dest_per_state, rho)
+            cur_chunk = int(min(chunk_states, max(1 << 14, cap_per_dest / (2.0 * rho))))
+        return snd
+
     while True:
         if max_depth > 0 and depth >= max_depth:  # level `depth` stays unexpanded (rmc_run_bfs)
             res.left_on_queue = res.levels[-1] if res.levels else 1
             break
-        # ---- expand this level's frontier chunk by chunk, exchanging each chunk;
-        # the chunk loop ends when no rank has frontier left (flags ride on the
-        # counts all-to-all)
-        ph = res.phase
+        # ---- expand this level's frontier chunk by chunk; chunk k's records
+        # travel while chunk k+1 is expanded; the loop ends when no rank has
+        # frontier left (flags ride on the counts all-to-all)
+        ob = 0
+        snd = expand(ob)
         while True:
-            t1 = time.perf_counter()
-            chk(lib.rmc_dist_expand(ctx, chunk_states, C.c_void_p(outbox.data_ptr()), cap_per_dest,
-                                    send, C.byref(done)))
             t2 = time.perf_counter()
-            res.records_sent += sum(send)
-            res.chunks += 1
-            received, _rc, flags = exchange(outbox, list(send), group, more=not done.value)
+            recv, flags, anyone = exchange_counts(snd, consumed < local_frontier, dev, cpu, group)
+            handle = payload_start(outboxes[ob], snd, recv, cpu, group) if anyone else None
+            ph["exchange"] += time.perf_counter() - t2
+            more = any(flags)
+            if more:  # every rank expands its next chunk (possibly empty) meanwhile
+                ob ^= 1
+                snd = expand(ob)
             t3 = time.perf_counter()
-            if received.shape[0]:
-                chk(lib.rmc_dist_insert(ctx, C.c_void_p(received.data_ptr()), received.shape[0]))
-            t4 = time.perf_counter()
-            ph["expand"] += t2 - t1
-            ph["exchange"] += t3 - t2
-            ph["insert"] += t4 - t3
-            if not any(flags):
+            if handle is not None:
+                received = payload_finish(handle)
+                t4 = time.perf_counter()
+                ph["exchange"] += t4 - t3
+                if received.shape[0]:
+                    chk(lib.rmc_dist_insert(ctx, C.c_void_p(received.data_ptr()), received.shape[0]))
+                ph["insert"] += time.perf_counter() - t4
+            if not more:
                 break
         t1 = time.perf_counter()
         chk(lib.rmc_dist_end_level(ctx, out5))
+        local_frontier, consumed = int(out5[0]), 0
         stats = _allgather([out5[0], out5[1], out5[2], out5[4], out5[3]], dev, cpu, group)
         ph["level"] += time.perf_counter() - t1
         new, gen, probes = (sum(r[k] for r in stats) for k in range(3))
