@@ -207,15 +207,20 @@ int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_vi
  * (Smokeraft.tla:64-76: one RandomSubset(k, .) per variable, k^9 states, over
  * SmokeNat = 0..smoke_nat, SmokeInt = -1..1, BoundedSeq(.,3)/(.,1) logs);
  * smoke_k = 0 starts from Init.  TLC's StopAfter (a 1-s budget,
- * Smokeraft.tla:88-92) is replaced by an explicit behaviour count.  A step
- * whose chosen successor exceeds the packed capacity ends that behaviour and is
- * counted in `truncated`. */
+ * Smokeraft.tla:88-92) is replaced by an explicit behaviour count.  The packed
+ * state holds terms <= 15, logs <= 3 entries, <= K distinct messages, counts <= 3:
+ * RMC_SIM_WITHIN_CAPACITY draws each step uniformly among the enabled
+ * successors that fit (the capacity acts as a state constraint, so behaviours
+ * run to `depth`); RMC_SIM_TRUNCATE draws among all enabled successors and a
+ * draw beyond the capacity ends that behaviour (counted in `truncated`). */
+#define RMC_SIM_WITHIN_CAPACITY 0
+#define RMC_SIM_TRUNCATE 1
 typedef struct rmc_sim_config {
     uint64_t behaviours;       /* random behaviours to run                        */
     int32_t depth;             /* states per behaviour (TLC -depth, default 100)  */
     int32_t smoke_k;           /* SmokeInit RandomSubset size k; 0 = Init         */
     int32_t smoke_nat;         /* SmokeNat = 0..smoke_nat (default 2)             */
-    int32_t pad;
+    int32_t mode;              /* RMC_SIM_WITHIN_CAPACITY (0) or RMC_SIM_TRUNCATE */
     uint64_t seed;             /* RNG seed for the SmokeInit draws and the walks  */
 } rmc_sim_config;
 typedef struct rmc_sim_result {
@@ -278,6 +283,13 @@ int rmc_probe_bench(int device, uint64_t table_bytes, uint64_t accesses, int mod
  * same stem is used).  Errors name the unsupported construct in err. */
 int rmc_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* cfg,
                           char* err, size_t err_cap);
+/* The same for a simulation model (TLC -simulate on Smokeraft.tla/.cfg):
+ * `Init <- SmokeInit` sets sim->smoke_k from `k ==` and sim->smoke_nat from
+ * `SmokeNat == 0..N` (Smokeraft.tla:10-19); a CONSTRAINT that is not a state
+ * bound (StopAfter, Smokeraft.tla:84-92) is accepted and replaced by
+ * sim->behaviours; sim->depth defaults to 100 (TLC -depth). */
+int rmc_sim_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* cfg,
+                              rmc_sim_config* sim, char* err, size_t err_cap);
 
 #ifdef __cplusplus
 }

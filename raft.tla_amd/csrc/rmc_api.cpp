@@ -728,7 +728,9 @@ int smoke_init(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<u32>* pac
 }
 
 int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_beh, std::vector<u32>* rec) {
-    if (!c || !sc || !out || sc->behaviours == 0 || sc->depth < 1) return RMC_E_INVAL;
+    if (!c || !sc || !out || sc->behaviours == 0 || sc->depth < 1 ||
+        (sc->mode != RMC_SIM_WITHIN_CAPACITY && sc->mode != RMC_SIM_TRUNCATE))
+        return RMC_E_INVAL;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<u32> inits;
@@ -757,7 +759,7 @@ int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_b
     HIPCHK(c, hipMemcpy(d_init, inits.data(), inits.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(d_out, &h, sizeof h, hipMemcpyHostToDevice));
     HIPCHK(c, hipEventRecord(c->ev0, c->st));
-    HIPCHK(c, launch_sim(c->sh, P, d_init, n_init, sc->behaviours, sc->depth, sc->seed, d_out, rec_beh, d_rec, c->st));
+    HIPCHK(c, launch_sim(c->sh, P, d_init, n_init, sc->behaviours, sc->depth, sc->seed, sc->mode, d_out, rec_beh, d_rec, c->st));
     HIPCHK(c, hipEventRecord(c->ev1, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
     float ms = 0.f;

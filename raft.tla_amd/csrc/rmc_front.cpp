@@ -102,7 +102,11 @@ bool load_module(const std::string& dir, const std::string& name, std::map<std::
     }
     for (size_t k = 0; k < starts.size(); ++k) {
         const size_t end = k + 1 < starts.size() ? starts[k + 1].first : text.size();
-        M.defs[starts[k].second] = trim(text.substr(body_at[k], end - body_at[k]));
+        std::string body = text.substr(body_at[k], end - body_at[k]);
+        // a separator line (4+ dashes, MCraft.tla:6,11,16,21) ends a definition
+        std::smatch sm;
+        if (std::regex_search(body, sm, std::regex("\n[ \t]*-{4,}"))) body = body.substr(0, (size_t)sm.position(0));
+        M.defs[starts[k].second] = trim(body);
     }
     mods[name] = M;
     for (const auto& e : M.extends)
@@ -189,8 +193,12 @@ int count_set(const std::string& body) {  // "{r1, r2, r3}" -> 3
 
 }  // namespace
 
-extern "C" int rmc_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* out, char* err,
-                                     size_t err_cap) {
+// sim != nullptr: a simulation model (Smokeraft.cfg:43-48): `Init <- SmokeInit`
+// with `k` and `SmokeNat` from the modules (Smokeraft.tla:10-19), a StopAfter-
+// style CONSTRAINT that is not a state bound (replaced by an explicit behaviour
+// count), no state bounds required (only the packed capacity limits a walk).
+static int parse_model(const char* cfg_path, const char* tla_path, rmc_config* out, rmc_sim_config* sim,
+                       char* err, size_t err_cap) {
     std::string e;
     auto fail = [&](const std::string& m) {
         if (err && err_cap) snprintf(err, err_cap, "%s", m.c_str());
@@ -274,8 +282,33 @@ extern "C" int rmc_config_from_files(const char* cfg_path, const char* tla_path,
     }
     if (!C.init.empty() && C.init != "Init") return fail("INIT " + C.init + " is not supported by BFS mode");
     if (!C.next.empty() && C.next != "Next") return fail("NEXT " + C.next + " is not supported");
-    if (C.subst.count("Init") || C.subst.count("Next"))
-        return fail("Init/Next overrides (e.g. Smokeraft's SmokeInit) are simulation-mode models");
+    if (C.subst.count("Next")) return fail("Next override is not supported");
+    if (sim) {
+        memset(sim, 0, sizeof *sim);
+        sim->behaviours = 1ull << 20;
+        sim->depth = 100;  // TLC -simulate default depth
+        sim->smoke_nat = 2;
+        auto it = C.subst.find("Init");
+        if (it != C.subst.end()) {
+            std::string b;
+            if (it->second != "SmokeInit" || !def("SmokeInit", &b))
+                return fail("Init <- " + it->second + ": only Smokeraft's SmokeInit is compiled in");
+            int kk = 0;
+            if (!int_of("k", &kk) || kk < 1) return fail("SmokeInit needs `k == <number>` (Smokeraft.tla:17-19)");
+            sim->smoke_k = kk;
+            std::string nat;
+            if (def("SmokeNat", &nat)) {
+                std::smatch m;
+                std::string nn;
+                for (char ch : nat) if (!isspace((unsigned char)ch)) nn += ch;
+                if (!std::regex_match(nn, m, std::regex("0\\.\\.([0-9]+)")))
+                    return fail("SmokeNat must be 0..N (Smokeraft.tla:10-11)");
+                sim->smoke_nat = atoi(m[1].str().c_str());
+            }
+        }
+    } else if (C.subst.count("Init")) {
+        return fail("Init overrides (e.g. Smokeraft's SmokeInit) are simulation-mode models (rmc-tlc -simulate)");
+    }
     if (!C.props.empty()) return fail("PROPERTY " + C.props[0] + " (liveness) is out of scope");
     if (!C.unknown.empty()) return fail("cfg section " + C.unknown[0] + " is not supported");
     // BecomeLeader override (config 5 bug variant)
@@ -292,6 +325,7 @@ extern "C" int rmc_config_from_files(const char* cfg_path, const char* tla_path,
     }
     for (auto& kv : C.subst) {
         if (kv.first == "Server" || kv.first == "Value" || kv.first == "BecomeLeader") continue;
+        if (sim && kv.first == "Init") continue;  // SmokeInit, resolved above
         std::string b;
         if (!def(kv.second, &b)) return fail("override " + kv.first + " <- " + kv.second + ": not found");
         int tmp;
@@ -321,7 +355,14 @@ extern "C" int rmc_config_from_files(const char* cfg_path, const char* tla_path,
                 ++hits;
             }
         }
+        if (!hits && sim) continue;  // e.g. StopAfter (Smokeraft.tla:84-92): a run budget, not a bound
         if (!hits) return fail("CONSTRAINT " + cn + " is not a recognised raft state bound");
+    }
+    if (sim) {  // unbounded fields: the packed capacity (rmc_simulate truncates beyond it)
+        if (g.max_term < 0) g.max_term = 14;
+        if (g.max_log_len < 0) g.max_log_len = 3;
+        if (g.max_msgs < 0) g.max_msgs = 8;
+        if (g.max_dup < 0) g.max_dup = 3;
     }
     if (g.max_term < 0 || g.max_log_len < 0 || g.max_msgs < 0 || g.max_dup < 0)
         return fail("the model is infinite without a CONSTRAINT bounding currentTerm, Len(log), "
@@ -344,4 +385,18 @@ extern "C" int rmc_config_from_files(const char* cfg_path, const char* tla_path,
     *out = g;
     if (err && err_cap) err[0] = 0;
     return 0;
+}
+
+extern "C" int rmc_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* out, char* err,
+                                     size_t err_cap) {
+    return parse_model(cfg_path, tla_path, out, nullptr, err, err_cap);
+}
+
+extern "C" int rmc_sim_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* out,
+                                         rmc_sim_config* sim, char* err, size_t err_cap) {
+    if (!sim) {
+        if (err && err_cap) snprintf(err, err_cap, "null argument");
+        return RMC_E_PARSE;
+    }
+    return parse_model(cfg_path, tla_path, out, sim, err, err_cap);
 }

@@ -73,7 +73,7 @@ struct SimCounters {
     u64 viol;  // min over violations of (depth << 42 | invariant << 40 | behaviour), ~0 = none
 };
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
-                      SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
+                      int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
 
 // Fingerprint salt for the kernels of this device (0 = default hash).
 hipError_t set_fp_salt(u64 seed, hipStream_t st);

@@ -839,11 +839,13 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
 
 // ---- simulation (TLC -simulate; Smokeraft.cfg) -------------
 // One thread per behaviour: a random initial state from `inits`, then up to
-// depth-1 steps, each choosing uniformly among ALL enabled successors (one
-// reservoir pass over the lanes).  A chosen successor outside the packed
-// capacity (term 16, Len(log) 4, 9 messages, count 4) ends the behaviour as
-// "truncated"; no enabled lane ends it as "deadlocked" (Smokeraft.cfg:48
-// turns deadlock checking off).  Invariants are checked on every state.
+// depth-1 steps, each choosing uniformly (one reservoir pass over the lanes)
+// among the enabled successors — mode 0: those within the packed capacity
+// (term <= 15, Len(log) <= 3, <= K messages, count <= 3; P carries these
+// bounds), mode 1: all of them, a chosen successor beyond the capacity ending
+// the behaviour as "truncated".  No candidate ends it as "deadlocked"
+// (Smokeraft.cfg:48 turns deadlock checking off).  Invariants are checked on
+// every state.
 // rec_beh >= 0: that behaviour also writes its states to rec (replay).
 __device__ __forceinline__ u64 sim_rand(u64& x) {  // splitmix64 stream
     x += 0x9E3779B97F4A7C15ull;
@@ -852,7 +854,7 @@ __device__ __forceinline__ u64 sim_rand(u64& x) {  // splitmix64 stream
 
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* inits, u64 n_init, u64 n_beh, int depth,
-                                                  u64 seed, SimCounters* out, i64 rec_beh, u32* rec) {
+                                                  u64 seed, int mode, SimCounters* out, i64 rec_beh, u32* rec) {
     constexpr int NW = 2 * S + K;
     u64 steps = 0, trunc = 0, dead = 0;
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n_beh; t += (u64)gridDim.x * 256ull) {
@@ -872,6 +874,8 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
                 Delta d;
                 lane_delta<S, K>(w, m, lane, P, d);
                 if (!d.en) continue;
+                u64 hh;
+                if (mode == 0 && !delta_fp<S, K>(w, m, 0ull, d, P, &hh)) continue;  // beyond the capacity
                 ++cnt;
                 if (sim_rand(rs) % cnt == 0) pick = lane;  // reservoir: uniform over enabled lanes
             }
@@ -908,18 +912,19 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
 
 template <int S, int K>
 static hipError_t launch_sim_t(const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
-                               SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
+                               int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
     const u64 blocks = (n_beh + 255) / 256;
     const u64 g = blocks < 4096 ? blocks : 4096;
     hipLaunchKernelGGL((k_simulate<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, inits, n_init, n_beh, depth, seed,
-                       out, rec_beh, rec);
+                       mode, out, rec_beh, rec);
     return hipGetLastError();
 }
 
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
-                      SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
+                      int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
 #define RMC_SCASE(SS, KK) \
-    if (sh.S == SS && sh.K == KK) return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, out, rec_beh, rec, st);
+    if (sh.S == SS && sh.K == KK)   \
+        return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, st);
     RMC_SCASE(2, 4) RMC_SCASE(2, 8) RMC_SCASE(3, 4) RMC_SCASE(3, 8) RMC_SCASE(4, 4) RMC_SCASE(4, 8) RMC_SCASE(5, 4)
     RMC_SCASE(5, 8)
 #undef RMC_SCASE

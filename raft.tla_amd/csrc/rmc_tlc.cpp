@@ -114,15 +114,74 @@ int progress(const rmc_level_stats* s, void*) {
 }
 
 int usage() {
-    fprintf(stderr, "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N] X.tla\n");
+    fprintf(stderr,
+            "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N]\n"
+            "               [-verify] [-fpseed S] [-simulate [num=N]] [-seed S] X.tla\n"
+            "  -depth N   stop after N BFS levels (level N is left on the queue)\n"
+            "  -verify    full-state verification: compare every fingerprint hit with the stored state\n"
+            "  -fpseed S  fingerprint salt (TLC -fp: another member of the fingerprint family)\n"
+            "  -simulate  random simulation (TLC -simulate; num=N behaviours, default 2^20;\n"
+            "             -depth = states per behaviour, default 100; -seed = RNG seed)\n");
     return 2;
+}
+
+// TLC -simulate: random behaviours with the invariants checked on every state
+// (Smokeraft.cfg:43-48 through rmc_sim_config_from_files).
+int run_simulation(const std::string& cfg, const std::string& tla, int device, int depth, unsigned long long num,
+                   unsigned long long seed) {
+    rmc_config c;
+    rmc_sim_config sc;
+    char err[512];
+    int rc = rmc_sim_config_from_files(cfg.c_str(), tla.c_str(), &c, &sc, err, sizeof err);
+    if (rc) { printf("Error: %s\n", err); return 1; }
+    c.device = device;
+    c.state_capacity = 1 << 12;  // no state store needed for walks
+    if (depth > 0) sc.depth = depth;
+    if (num > 0) sc.behaviours = num;
+    sc.seed = seed;
+    printf("Running Random Simulation with seed %llu: %llu behaviours of up to %d states, %s.\n",
+           (unsigned long long)seed, (unsigned long long)sc.behaviours, sc.depth,
+           sc.smoke_k ? "initial states from SmokeInit" : "initial state from Init");
+    rmc_ctx* ctx = nullptr;
+    rc = rmc_create(&c, &ctx);
+    if (rc) { printf("Error: rmc_create failed (%d)\n", rc); return 1; }
+    rmc_sim_result r;
+    rc = rmc_simulate(ctx, &sc, &r);
+    if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
+    if (sc.smoke_k) printf("SmokeInit: %llu initial states (k = %d).\n", (unsigned long long)r.init_states, sc.smoke_k);
+    int exitcode = 0;
+    if (r.violated_inv) {
+        printf("Error: Invariant %s is violated.\n", inv_name(r.violated_inv));
+        printf("Error: The behavior up to this point is:\n");
+        std::vector<rmc_state_view> st((size_t)sc.depth);
+        size_t len = 0;
+        rmc_sim_replay(ctx, &sc, r.violation_behaviour, st.data(), st.size(), &len);
+        for (size_t k = 0; k < len && k < st.size(); ++k) {
+            printf("State %zu:\n", k + 1);
+            print_state(st[k]);
+            printf("\n");
+        }
+        exitcode = 12;
+    } else {
+        printf("No error has been found in %llu behaviours.\n", (unsigned long long)r.behaviours);
+    }
+    printf("%llu states generated (%llu steps), %llu behaviours truncated at the packed capacity, "
+           "%llu deadlocked (no successor within the capacity).\n",
+           (unsigned long long)(r.steps + r.behaviours), (unsigned long long)r.steps,
+           (unsigned long long)r.truncated, (unsigned long long)r.deadlocked);
+    printf("Finished in %.0fms (%.3g behaviours/s, %.3g steps/s on the device)\n", r.seconds * 1e3,
+           r.behaviours / (r.kernel_seconds > 0 ? r.kernel_seconds : 1), r.steps / (r.kernel_seconds > 0 ? r.kernel_seconds : 1));
+    rmc_destroy(ctx);
+    return exitcode;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
     std::string cfg, tla;
-    int depth = 0, device = 0, nodeadlock = 0;
+    int depth = 0, device = 0, nodeadlock = 0, verify = 0;
+    unsigned long long fpseed = 0, seed = 0, num = 0;
+    int simulate = 0;
     unsigned long long capacity = 0;
     for (int a = 1; a < argc; ++a) {
         std::string s = argv[a];
@@ -133,12 +192,20 @@ int main(int argc, char** argv) {
         else if (s == "-device") { const char* v = next(); if (!v) return usage(); device = atoi(v); }
         else if (s == "-capacity") { const char* v = next(); if (!v) return usage(); capacity = strtoull(v, nullptr, 10); }
         else if (s == "-workers") { if (!next()) return usage(); }  // accepted for compatibility
+        else if (s == "-verify") verify = 1;
+        else if (s == "-simulate") {
+            simulate = 1;
+            if (a + 1 < argc && strncmp(argv[a + 1], "num=", 4) == 0) num = strtoull(argv[++a] + 4, nullptr, 10);
+        }
+        else if (s == "-seed") { const char* v = next(); if (!v) return usage(); seed = strtoull(v, nullptr, 0); }
+        else if (s == "-fpseed" || s == "-fp") { const char* v = next(); if (!v) return usage(); fpseed = strtoull(v, nullptr, 0); }
         else if (s[0] == '-') { fprintf(stderr, "unsupported option %s\n", s.c_str()); return usage(); }
         else tla = s;
     }
     if (tla.empty()) return usage();
     if (cfg.empty()) cfg = (tla.size() > 4 && tla.substr(tla.size() - 4) == ".tla" ? tla.substr(0, tla.size() - 4) : tla) + ".cfg";
     printf("rmc-tlc: %s\n", rmc_version());
+    if (simulate) return run_simulation(cfg, tla, device, depth, num, seed);
     rmc_config c;
     char err[512];
     int rc = rmc_config_from_files(cfg.c_str(), tla.c_str(), &c, err, sizeof err);
@@ -147,6 +214,8 @@ int main(int argc, char** argv) {
     c.max_depth = depth;
     c.state_capacity = capacity;
     if (nodeadlock) c.flags &= ~RMC_FLAG_CHECK_DEADLOCK;
+    if (verify) c.flags |= RMC_FLAG_VERIFY_STATES;
+    c.seed = fpseed;
     printf("Model: %d servers, %d values, CONSTRAINT MaxTerm=%d MaxLogLen=%d MaxMsgs=%d MaxDup=%d%s%s\n",
            c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,
            (c.flags & RMC_FLAG_SYMMETRY) ? ", SYMMETRY Permutations(Server)" : "",
@@ -182,6 +251,9 @@ int main(int argc, char** argv) {
                "  because two distinct states had the same fingerprint:\n"
                "  calculated (optimistic):  val = %.1E\n", r.collision_probability);
     }
+    if (verify)
+        printf("Full-state verification: %llu fingerprint hits compared state by state, %llu collisions.\n",
+               (unsigned long long)r.verified, (unsigned long long)r.collisions);
     printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
            (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
     printf("The depth of the complete state graph search is %d.\n", r.depth);

@@ -83,7 +83,7 @@ class SuccView(C.Structure):
 
 class SimConfig(C.Structure):
     _fields_ = [("behaviours", C.c_uint64), ("depth", C.c_int32), ("smoke_k", C.c_int32),
-                ("smoke_nat", C.c_int32), ("pad", C.c_int32), ("seed", C.c_uint64)]
+                ("smoke_nat", C.c_int32), ("mode", C.c_int32), ("seed", C.c_uint64)]
 
 
 class SimResult(C.Structure):
@@ -100,7 +100,8 @@ EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_ru
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
            "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
            "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level", "rmc_dist_state",
-           "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits")
+           "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits",
+           "rmc_sim_config_from_files")
 
 _lib = None
 
@@ -135,6 +136,9 @@ def native():
         lib.rmc_config_from_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Config),
                                               C.c_char_p, C.c_size_t]
         lib.rmc_config_from_files.restype = C.c_int
+        lib.rmc_sim_config_from_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Config),
+                                                  C.POINTER(SimConfig), C.c_char_p, C.c_size_t]
+        lib.rmc_sim_config_from_files.restype = C.c_int
         lib.rmc_probe_bench.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int,
                                         C.POINTER(C.c_double)]
         lib.rmc_probe_bench.restype = C.c_int
@@ -193,6 +197,18 @@ def config_from_files(cfg_path, tla_path=None):
     return cfg
 
 
+def sim_config_from_files(cfg_path, tla_path=None):
+    """(Config, SimConfig) of a simulation model (Smokeraft.cfg: Init <- SmokeInit)."""
+    lib = native()
+    cfg, sc = Config(), SimConfig()
+    err = C.create_string_buffer(512)
+    rc = lib.rmc_sim_config_from_files(cfg_path.encode(), tla_path.encode() if tla_path else None,
+                                       C.byref(cfg), C.byref(sc), err, 512)
+    if rc:
+        raise RmcError(rc, err.value.decode())
+    return cfg, sc
+
+
 def probe_bench(device=0, table_bytes=64 << 30, accesses=1 << 31, mode=0):
     """Random 8-byte probe (mode 0) / CAS (mode 1) rate over a table of
     table_bytes: the roofline ceiling R_max of the fingerprint set."""
@@ -244,16 +260,17 @@ class Checker:
         self.levels = levels
         return res
 
-    def simulate(self, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0) -> SimResult:
-        """TLC -simulate over Smokeraft-style initial states (rmc_simulate)."""
-        sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, 0, seed)
+    def simulate(self, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0, mode=0) -> SimResult:
+        """TLC -simulate over Smokeraft-style initial states (rmc_simulate);
+        mode 0 = RMC_SIM_WITHIN_CAPACITY, 1 = RMC_SIM_TRUNCATE."""
+        sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, mode, seed)
         out = SimResult()
         self._check(self.lib.rmc_simulate(self.ctx, C.byref(sc), C.byref(out)))
         return out
 
-    def sim_replay(self, behaviour, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0):
+    def sim_replay(self, behaviour, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0, mode=0):
         """States of one behaviour of the same simulation (rmc_sim_replay)."""
-        sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, 0, seed)
+        sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, mode, seed)
         st = (StateView * depth)()
         n = C.c_size_t()
         self._check(self.lib.rmc_sim_replay(self.ctx, C.byref(sc), behaviour, st, depth, C.byref(n)))

@@ -166,3 +166,32 @@ def test_expand_matches_oracle_on_fuzzed_states(k):
                 ora_in[(f, t)] += 1
         assert gpu_gen[idx] == ora_gen, (idx, s)
         assert gpu_in[idx] == ora_in, (idx, s)
+
+
+CLI = os.path.join(os.path.dirname(os.path.dirname(__file__)), "raft.tla_amd", "bin", "rmc-tlc")
+SPECS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "specs")
+MODELS = os.path.join(os.path.dirname(__file__), "golden", "models")
+
+
+def test_cli_bfs_summary_with_verification():
+    """rmc-tlc prints TLC's summary lines; -verify adds the collision count."""
+    import subprocess
+    g = GOLDEN["tiny2"]
+    r = subprocess.run([CLI, "-verify", "-config", os.path.join(SPECS, "MCraftTiny2.cfg"),
+                        os.path.join(SPECS, "MCraftTiny2.tla")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"{g['generated']} states generated, {g['distinct']} distinct states found, 0 states left on queue." \
+        in r.stdout
+    assert f"The depth of the complete state graph search is {g['depth']}." in r.stdout
+    assert ", 0 collisions." in r.stdout
+
+
+def test_cli_simulation_mode():
+    """rmc-tlc -simulate on a SmokeInit model (k = 3: 3^9 initial states, as
+    Smokeraft.tla:17-19 lists); TypeOK holds on every state."""
+    import subprocess
+    r = subprocess.run([CLI, "-simulate", "num=65536", "-seed", "3", os.path.join(MODELS, "SmokeFixture.tla")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "SmokeInit: 19683 initial states (k = 3)." in r.stdout
+    assert "No error has been found in 65536 behaviours." in r.stdout

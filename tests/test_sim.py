@@ -59,12 +59,26 @@ def test_replayed_behaviours_are_behaviours_of_the_spec():
 
 
 def test_simulation_runs_at_scale():
+    """Default mode: draws among the successors within the packed capacity, so
+    behaviours run to depth 100 (TLC -simulate's default depth)."""
     with rmc.Checker(smoke_cfg()) as ck:
         r = ck.simulate(behaviours=1 << 18, depth=100, smoke_k=2, seed=3)
     assert r.behaviours == 1 << 18
     assert r.violated_inv == 0  # TypeOK holds (Smokeraft.cfg:38-39)
-    assert r.steps > (1 << 18) * 50
-    assert r.truncated < (1 << 18) // 2
+    assert r.truncated == 0
+    assert r.steps + 100 * r.deadlocked >= (1 << 18) * 99
+
+
+def test_simulation_truncate_mode_counts_capacity_exits():
+    """RMC_SIM_TRUNCATE draws among all enabled successors (TLC's distribution
+    while the state fits) and ends a behaviour whose draw exceeds the packed
+    capacity; such behaviours are counted, never silently dropped."""
+    with rmc.Checker(smoke_cfg()) as ck:
+        r = ck.simulate(behaviours=1 << 16, depth=100, smoke_k=2, seed=3, mode=1)
+    assert r.violated_inv == 0
+    assert r.truncated > 0
+    assert r.steps < (1 << 16) * 99
+    assert r.truncated + r.deadlocked <= 1 << 16
 
 
 def test_simulation_finds_the_injected_bug():
