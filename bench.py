@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK (one GPU per rank)")
     ap.add_argument("--chunk", type=int, default=1 << 24, help="frontier states per exchange")
     ap.add_argument("--cap-per-dest", type=int, default=1 << 25, help="outbox records per destination rank")
+    ap.add_argument("--sent-cache", type=int, default=1 << 30,
+                    help="sharded mode: slots of the per-rank cache of fingerprints already sent")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the sharded path even at one rank (measures its overhead)")
     ap.add_argument("--no-probe-ceiling", action="store_true",
@@ -119,7 +121,7 @@ def main():
             r = ck.run()
             return r.distinct, r.generated, r.depth, r.probes, r.expand_kernel_seconds, r.expand_launches
         from rmc import dist as rdist
-        r = rdist.run(ck, chunk_states=a.chunk, cap_per_dest=a.cap_per_dest, sent_cache_slots=1 << 27,
+        r = rdist.run(ck, chunk_states=a.chunk, cap_per_dest=a.cap_per_dest, sent_cache_slots=a.sent_cache,
                       init=first)
         cr = ck.result()  # rmc_dist_start resets the per-run counters
         last_dist[0] = r

@@ -164,8 +164,11 @@ def trace(ck: Checker, rank0: int, index0: int, group=None) -> list:
 
 
 def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slots=1 << 26,
-        group=None, init=True) -> DistResult:
-    """Collective: every rank calls it with its own Checker (one GPU each)."""
+        group=None, init=True, pipeline_chunks=4, min_chunk=1 << 20) -> DistResult:
+    """Collective: every rank calls it with its own Checker (one GPU each).
+    A level's local frontier is expanded in about `pipeline_chunks` chunks (of
+    at least `min_chunk` states, at most `chunk_states`), so the exchange of
+    one chunk overlaps the expansion of the next."""
     lib, ctx = ck.lib, ck.ctx
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     cpu = dist.get_backend(group) == "gloo"
@@ -192,7 +195,8 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
     max_depth = ck.cfg.max_depth
     # adaptive chunk (states per expansion): start where even one record per
     # state for one destination fits, then track the observed ratio
-    cur_chunk = int(min(chunk_states, cap_per_dest // 2))
+    cap_bound = int(min(chunk_states, cap_per_dest // 2))  # outbox-fill bound on the chunk
+    cur_chunk = cap_bound
     # this rank's share of the first level: the initial state lives on its owner
     local_frontier, consumed = int(ck.result().distinct), 0
     ph = res.phase
@@ -214,7 +218,8 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
             # error: dropped records would be lost states)
             rho = max(max(snd), 1) / n_exp
             res.max_dest_per_state = max(res.max_dest_per_state, rho)
-            cur_chunk = int(min(chunk_states, max(1 << 14, cap_per_dest / (2.0 * rho))))
+            cap_bound = int(min(chunk_states, max(1 << 14, cap_per_dest / (2.0 * rho))))
+            cur_chunk = min(cur_chunk, cap_bound)
         return snd
 
     while True:
@@ -225,6 +230,8 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
         # travel while chunk k+1 is expanded; the loop ends when no rank has
         # frontier left (flags ride on the counts all-to-all)
         ob = 0
+        # about pipeline_chunks chunks per level (each bounded by the outbox fill)
+        cur_chunk = min(cap_bound, max(min_chunk, -(-local_frontier // max(1, pipeline_chunks))))
         snd = expand(ob)
         while True:
             t2 = time.perf_counter()
