@@ -447,7 +447,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false>
-__global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+__device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr int NP = SYM ? NPerm<S>::v : 1;
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
@@ -641,6 +641,19 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
         if (me == 0 && vchk) atomicAdd((unsigned long long*)&B.ctr->vchecked, (unsigned long long)vchk);
         if (me == 0 && vcol) atomicAdd((unsigned long long*)&B.ctr->collisions, (unsigned long long)vcol);
     }
+}
+
+template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false>
+__global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    expand_body<S, K, SYM, BATCH, DIST, VERIFY>(P, PT, B, lo, hi);
+}
+
+// The sharded expansion at 6 waves/SIMD (its owner bookkeeping takes 82 VGPRs
+// unconstrained: 5 waves): the register budget is capped for this variant only.
+template <int S, int K, int BATCH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_expand_dist(
+    const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
 
 // Sharded mode, owner side: insert the n records received from other ranks
@@ -963,7 +976,10 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                b);
         }
     } else if (which == 3) {
-        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        if constexpr (SYM)
+            hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        else
+            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 4) {
         hipLaunchKernelGGL((k_insert_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
     } else if (which == 5) {
