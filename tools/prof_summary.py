@@ -1,0 +1,68 @@
+"""Summarise the rocprofv3 databases of tools_prof.sh into profiles/<round>/:
+
+  kernel_stats_<cfg>.csv     per-kernel calls / total / average (kernel-trace pass)
+  pmc_traffic_<cfg>.json     HBM bytes per k_expand launch (FETCH_SIZE and
+                             WRITE_SIZE passes, one counter per pass)
+
+    python tools/prof_summary.py gpurun_out/prof r01 MCraftBench
+"""
+import csv
+import glob
+import json
+import os
+import sqlite3
+import sys
+
+
+def one_db(d):
+    files = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
+    if len(files) != 1:
+        raise SystemExit(f"expected one .db under {d}, found {files}")
+    return sqlite3.connect(files[0])
+
+
+def main():
+    src, rnd, stem = sys.argv[1:4]
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", rnd)
+    os.makedirs(out, exist_ok=True)
+    kt = one_db(os.path.join(src, "kt"))
+    rows = kt.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    with open(os.path.join(out, f"kernel_stats_{stem}.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "TotalDurationUs", "AverageUs", "Percentage"])
+        for r in rows:
+            w.writerow(r)
+    expand = [r for r in rows if "k_expand<" in r[0]]
+    name, calls, total_us, avg_us, _pct = max(expand, key=lambda r: r[2])
+
+    def counter(db, cname):
+        vals = db.execute("select value from counters_collection where counter_name = ? and kernel_name = ?",
+                          (cname, name)).fetchall()
+        return [v[0] for v in vals]
+
+    fetch = counter(one_db(os.path.join(src, "fetch")), "FETCH_SIZE")
+    write = counter(one_db(os.path.join(src, "write")), "WRITE_SIZE")
+    n = len(fetch)
+    rec = {
+        "command": "tools_prof.sh: rocprofv3 --kernel-trace --stats | --pmc FETCH_SIZE | --pmc WRITE_SIZE "
+                   "(separate passes) -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-probe-ceiling",
+        "workload": f"specs/{stem}.cfg, BFS to fixpoint (bench step + the untimed fingerprint-salt re-run)",
+        "kernel": name,
+        "launches": calls,
+        "kernel_total_us": total_us,
+        "kernel_avg_us": avg_us,
+        "pmc_launches": n,
+        "fetch_size_kb_total": sum(fetch),
+        "write_size_kb_total": sum(write),
+        "hbm_bytes_total": (sum(fetch) + sum(write)) * 1024.0,
+        "hbm_bytes_per_launch": (sum(fetch) + sum(write)) * 1024.0 / max(1, n),
+        "note": "FETCH_SIZE/WRITE_SIZE in KiB. The accesses are 8-B random probes (one 64-B granule each), "
+                "CAS and 40-B state stores, not 16-B/lane streams, so the gfx950 2x FETCH_SIZE correction "
+                "for wide streaming reads (MI355X_MICROARCH.md, HBM) is not applied.",
+    }
+    json.dump(rec, open(os.path.join(out, f"pmc_traffic_{stem}.json"), "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()

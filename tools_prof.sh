@@ -1,4 +1,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests/test_gpu.py tests/test_sim.py tests/test_dist.py -x -v --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
-timeout -k 10 300 python -u bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || exit 1
+A="--steps 1 --warmup 0 --no-cpu --no-probe-ceiling"
+mkdir -p gpurun_out/prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt -o kt -- python3 bench.py $A > gpurun_out/prof/kt.json 2> gpurun_out/prof/kt.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/fetch -o fetch -- python3 bench.py $A > gpurun_out/prof/fetch.json 2> gpurun_out/prof/fetch.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/write -o write -- python3 bench.py $A > gpurun_out/prof/write.json 2> gpurun_out/prof/write.err || exit 1
