@@ -43,6 +43,7 @@ extern "C" {
 #define RMC_E_NOGPU (-19)      /* no usable gfx950 device */
 #define RMC_E_PARSE (-74)      /* .cfg / .tla front-end could not recognise the model */
 #define RMC_E_STATE (-71)      /* call out of order (e.g. rmc_trace before a violation) */
+#define RMC_E_IO (-61)         /* checkpoint file missing, unreadable or of another model */
 
 /* rmc_config.flags */
 #define RMC_FLAG_SYMMETRY (1u << 0)        /* SYMMETRY Permutations(Server)            */
@@ -190,6 +191,17 @@ int rmc_set_fp_bits(rmc_ctx* ctx, int32_t bits);
  * *len receives the trace length even if it exceeds cap. */
 int rmc_trace(rmc_ctx* ctx, rmc_state_view* states, int32_t* families, int32_t* instances,
               size_t cap, size_t* len);
+
+/* ---- checkpoint / recovery (TLC -checkpoint / -recover) ----------------------
+ * rmc_checkpoint: after rmc_run_bfs stopped at a level boundary (max_depth or
+ * the progress callback), write the stored levels (states, parent refs, lanes),
+ * the level table and the counters to `path`.  rmc_recover: on a ctx of the
+ * same model (constants, bounds, flags, seed; capacity >= the checkpoint's
+ * states), load them and rebuild the fingerprint set from the states; the next
+ * rmc_run_bfs continues from the first unexpanded level, with cumulative
+ * counts.  Single-GPU contexts. */
+int rmc_checkpoint(rmc_ctx* ctx, const char* path);
+int rmc_recover(rmc_ctx* ctx, const char* path);
 
 /* ---- codec and successor enumeration (tests, Java driver printing) -------
  * rmc_state_bytes: bytes of one packed state for this config.

@@ -44,6 +44,9 @@ struct rmc_ctx {
     u64* h_ocount = nullptr;  // pinned [world]
     u64 cursor = 0;           // next unexpanded state of the current local frontier
     int depth = 0;
+    // recovery (rmc_recover): the next rmc_run_bfs continues from this level
+    int resume = 0;
+    int resume_depth = 0;
 };
 
 namespace {
@@ -422,9 +425,20 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     HIPCHK(c, hipSetDevice(c->cfg.device));
     const auto t0 = std::chrono::steady_clock::now();
     auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    const bool resume = c->resume != 0;  // rmc_recover restored store, set and counters
+    c->resume = 0;
+    c->have_target = 0;
+    int depth = 0;
+    if (resume) {
+        c->res.left_on_queue = 0;
+        c->res.seconds = 0;
+        HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
+        c->h_ctr->count = c->level_start.back();
+        if (int rc = reset_counters(c, true)) return rc;
+        depth = c->resume_depth;
+    } else {
     c->res = rmc_result{};
     c->level_start.clear();
-    c->have_target = 0;
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
@@ -444,13 +458,14 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->level_start.push_back(c->h_ctr->count);
     if (c->sh.verify)
         HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
-    int depth = c->h_ctr->count ? 1 : 0;
+    depth = c->h_ctr->count ? 1 : 0;
     if (c->h_ctr->viol != ~0ull) {
         c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 3);
         c->res.violation_depth = 1;
         c->have_target = 1;
         c->target_idx = c->h_ctr->viol >> 2;
     }
+    }  // !resume
     const u64 CHUNK = 1ull << 26;
     while (!c->have_target) {
         const u64 lo = c->level_start[depth - 1], hi = c->level_start[depth];
@@ -552,6 +567,120 @@ int rmc_set_fp_bits(rmc_ctx* c, int32_t bits) {
 int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
     if (!c || !out) return RMC_E_INVAL;
     *out = c->res;
+    return 0;
+}
+
+// ---- checkpoint / recovery (TLC -checkpoint / -recover) ------------------------
+// File: header, level boundaries, then the stored states, parent refs and lanes
+// of levels 1..depth.  The fingerprint set is not written: rmc_recover rebuilds
+// it from the states (k_rehash), one pass over the store.
+namespace {
+struct CkptHeader {
+    char magic[8];
+    uint32_t version, nw;
+    rmc_config cfg;
+    uint64_t count, nlevels;
+    int32_t depth, pad;
+    rmc_result res;
+};
+const char kCkptMagic[8] = {'R', 'M', 'C', 'C', 'K', 'P', 'T', '1'};
+
+bool same_model(const rmc_config& a, const rmc_config& b) {
+    return a.n_servers == b.n_servers && a.n_values == b.n_values && a.max_term == b.max_term &&
+           a.max_log_len == b.max_log_len && a.max_msgs == b.max_msgs && a.max_dup == b.max_dup &&
+           a.flags == b.flags && a.invariants == b.invariants && a.seed == b.seed;
+}
+
+// Copy n bytes between a device buffer and a file through a pinned bounce buffer.
+int move_file(rmc_ctx* c, FILE* f, void* dev, u64 n, bool to_file) {
+    const u64 B = 64ull << 20;
+    void* h = nullptr;
+    HIPCHK(c, hipHostMalloc(&h, B, hipHostMallocDefault));
+    int rc = 0;
+    for (u64 off = 0; off < n && !rc; off += B) {
+        const u64 k = std::min(B, n - off);
+        char* d = (char*)dev + off;
+        if (to_file) {
+            if (hipMemcpy(h, d, k, hipMemcpyDeviceToHost) != hipSuccess) rc = RMC_E_HIP;
+            else if (fwrite(h, 1, k, f) != k) rc = fail(c, RMC_E_IO, "checkpoint write failed");
+        } else {
+            if (fread(h, 1, k, f) != k) rc = fail(c, RMC_E_IO, "checkpoint file truncated");
+            else if (hipMemcpy(d, h, k, hipMemcpyHostToDevice) != hipSuccess) rc = RMC_E_HIP;
+        }
+    }
+    (void)hipHostFree(h);
+    if (rc == RMC_E_HIP) return fail(c, rc, "checkpoint copy failed");
+    return rc;
+}
+}  // namespace
+
+int rmc_checkpoint(rmc_ctx* c, const char* path) {
+    if (!c || !path) return RMC_E_INVAL;
+    if (c->dist) return fail(c, RMC_E_INVAL, "checkpoint: single-GPU runs only");
+    if (c->level_start.size() < 2 || c->have_target)
+        return fail(c, RMC_E_STATE, "checkpoint: needs a BFS stopped at a level boundary without a violation");
+    if (c->res.left_on_queue == 0) return fail(c, RMC_E_STATE, "checkpoint: the search is complete");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    FILE* f = fopen(path, "wb");
+    if (!f) return fail(c, RMC_E_IO, std::string("checkpoint: cannot create ") + path);
+    CkptHeader h{};
+    memcpy(h.magic, kCkptMagic, 8);
+    h.version = 1;
+    h.nw = (uint32_t)c->NW;
+    h.cfg = c->cfg;
+    h.count = c->level_start.back();
+    h.nlevels = c->level_start.size();
+    h.depth = c->res.depth;
+    h.res = c->res;
+    int rc = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(c->level_start.data(), 8, h.nlevels, f) == h.nlevels
+                 ? 0 : fail(c, RMC_E_IO, "checkpoint write failed");
+    if (!rc) rc = move_file(c, f, c->B.store, h.count * (u64)c->NW * 4, true);
+    if (!rc) rc = move_file(c, f, c->B.parent, h.count * 8, true);
+    if (!rc) rc = move_file(c, f, c->B.act, h.count, true);
+    if (fclose(f) != 0 && !rc) rc = fail(c, RMC_E_IO, "checkpoint close failed");
+    return rc;
+}
+
+int rmc_recover(rmc_ctx* c, const char* path) {
+    if (!c || !path) return RMC_E_INVAL;
+    if (c->dist) return fail(c, RMC_E_INVAL, "recover: single-GPU runs only");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(c, RMC_E_IO, std::string("recover: cannot open ") + path);
+    CkptHeader h{};
+    int rc = 0;
+    std::vector<u64> ls;
+    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 1)
+        rc = fail(c, RMC_E_IO, "recover: not an rmc checkpoint");
+    else if (h.nw != (uint32_t)c->NW || !same_model(h.cfg, c->cfg))
+        rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another model (constants, bounds, flags or seed)");
+    else if (h.count > c->B.cap)
+        rc = fail(c, RMC_E_CAPACITY, "recover: the checkpoint holds more states than this ctx's capacity");
+    else {
+        ls.resize(h.nlevels);
+        if (h.nlevels < 2 || fread(ls.data(), 8, h.nlevels, f) != h.nlevels || ls.back() != h.count)
+            rc = fail(c, RMC_E_IO, "recover: corrupt level table");
+    }
+    if (!rc) rc = move_file(c, f, c->B.store, h.count * (u64)c->NW * 4, false);
+    if (!rc) rc = move_file(c, f, c->B.parent, h.count * 8, false);
+    if (!rc) rc = move_file(c, f, c->B.act, h.count, false);
+    fclose(f);
+    if (rc) return rc;
+    // rebuild the fingerprint set (and the verification slot map) from the states
+    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
+    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
+    if (int r2 = reset_counters(c, false)) return r2;
+    HIPCHK(c, launch(c->sh, 7, c->P, c->PT, c->B, 0, h.count, nullptr, nullptr, 0, nullptr, c->st));
+    if (c->sh.verify) HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, h.count, nullptr, nullptr, 0, nullptr, c->st));
+    if (int r2 = read_counters(c)) return r2;
+    if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "recover: fingerprint set full");
+    if (c->h_ctr->overflow) return fail(c, RMC_E_IO, "recover: the checkpoint holds duplicate states");
+    c->level_start = ls;
+    c->res = h.res;
+    c->resume = 1;
+    c->resume_depth = h.depth;
     return 0;
 }
 

@@ -62,7 +62,8 @@ struct Shape {
 //        3 = sharded k_expand over store[a, b) (outbox in B);
 //        4 = k_insert_remote of `a` received records `in`;
 //        5 = k_publish over store[a, b) (verification: slot -> store index);
-//        6 = k_verify of `a` deferred hits in B.vbuf.
+//        6 = k_verify of `a` deferred hits in B.vbuf;
+//        7 = k_rehash of the stored states [a, b) (recovery).
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 

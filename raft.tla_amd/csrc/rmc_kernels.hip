@@ -802,6 +802,30 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
     commit_new<S, K>(is_new, w, m, d, P, B, ~0ull, 255);
 }
 
+// Recovery (rmc_recover): re-insert the keys of the stored states [lo, hi)
+// into an empty fingerprint set — the set is rebuilt, not checkpointed.
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_rehash(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    constexpr int NW = 2 * S + K;
+    constexpr int NP = SYM ? NPerm<S>::v : 1;
+    for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + i * (u64)NW, w, m);
+        u64 key = state_fp<S, K>(w, m);
+        if constexpr (SYM) {
+            u64 hp[NP];
+            perm_fps<S, K, NP>(w, m, PT, hp);
+            key = ~0ull;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
+        }
+        key &= P.fp_mask;
+        key = key ? key : 1ull;
+        if (!fp_insert(B.table, B.tmask, key, &B.ctr->table_full)) atomicOr(&B.ctr->overflow, 8u);  // duplicate
+    }
+}
+
 // Every enabled lane of n given states, written out without dedup.
 template <int S, int K, bool SYM>
 __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT, const u32* in, u64 n, u32* out,
@@ -958,7 +982,7 @@ constexpr int kBatch = 8;
 template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, bool verify, const Params& P, const PermTable& PT, const DevBufs& B, u64 a,
                            u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-    const u64 n = (which == 0 || which == 3 || which == 5) ? (b - a) : a;
+    const u64 n = (which == 0 || which == 3 || which == 5 || which == 7) ? (b - a) : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
@@ -984,6 +1008,8 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         hipLaunchKernelGGL((k_insert_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
     } else if (which == 5) {
         hipLaunchKernelGGL((k_publish<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
+    } else if (which == 7) {
+        hipLaunchKernelGGL((k_rehash<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 6) {
         hipLaunchKernelGGL((k_verify<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a);
     } else if (which == 1) {

@@ -116,10 +116,12 @@ int progress(const rmc_level_stats* s, void*) {
 int usage() {
     fprintf(stderr,
             "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N]\n"
-            "               [-verify] [-fpseed S] [-simulate [num=N]] [-seed S] X.tla\n"
+            "               [-verify] [-fpseed S] [-checkpoint F] [-recover F] [-simulate [num=N]] [-seed S] X.tla\n"
             "  -depth N   stop after N BFS levels (level N is left on the queue)\n"
             "  -verify    full-state verification: compare every fingerprint hit with the stored state\n"
             "  -fpseed S  fingerprint salt (TLC -fp: another member of the fingerprint family)\n"
+            "  -checkpoint F  write the search to F when it stops at -depth (TLC -checkpoint)\n"
+            "  -recover F     continue the search saved in F (TLC -recover)\n"
             "  -simulate  random simulation (TLC -simulate; num=N behaviours, default 2^20;\n"
             "             -depth = states per behaviour, default 100; -seed = RNG seed)\n");
     return 2;
@@ -182,6 +184,7 @@ int main(int argc, char** argv) {
     int depth = 0, device = 0, nodeadlock = 0, verify = 0;
     unsigned long long fpseed = 0, seed = 0, num = 0;
     int simulate = 0;
+    std::string ckpt, recover;
     unsigned long long capacity = 0;
     for (int a = 1; a < argc; ++a) {
         std::string s = argv[a];
@@ -193,6 +196,8 @@ int main(int argc, char** argv) {
         else if (s == "-capacity") { const char* v = next(); if (!v) return usage(); capacity = strtoull(v, nullptr, 10); }
         else if (s == "-workers") { if (!next()) return usage(); }  // accepted for compatibility
         else if (s == "-verify") verify = 1;
+        else if (s == "-checkpoint") { const char* v = next(); if (!v) return usage(); ckpt = v; }
+        else if (s == "-recover") { const char* v = next(); if (!v) return usage(); recover = v; }
         else if (s == "-simulate") {
             simulate = 1;
             if (a + 1 < argc && strncmp(argv[a + 1], "num=", 4) == 0) num = strtoull(argv[++a] + 4, nullptr, 10);
@@ -223,7 +228,13 @@ int main(int argc, char** argv) {
     rmc_ctx* ctx = nullptr;
     rc = rmc_create(&c, &ctx);
     if (rc) { printf("Error: rmc_create failed (%d)\n", rc); return 1; }
-    printf("Computing initial states...\n");
+    if (!recover.empty()) {
+        rc = rmc_recover(ctx, recover.c_str());
+        if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
+        printf("Recovering from checkpoint %s...\n", recover.c_str());
+    } else {
+        printf("Computing initial states...\n");
+    }
     rc = rmc_run_bfs(ctx, progress, nullptr);
     if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
     rmc_result r;
@@ -257,7 +268,15 @@ int main(int argc, char** argv) {
     printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
            (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
     printf("The depth of the complete state graph search is %d.\n", r.depth);
-    printf("Finished in %.0fms (%.0f distinct states/s)\n", r.seconds * 1e3, r.distinct / (r.seconds > 0 ? r.seconds : 1));
+    if (!ckpt.empty() && r.left_on_queue > 0 && !r.violated_inv && !r.deadlock) {
+        if (rmc_checkpoint(ctx, ckpt.c_str())) printf("Error: %s\n", rmc_last_error(ctx));
+        else printf("Checkpoint written to %s (%llu states on the queue).\n", ckpt.c_str(),
+                    (unsigned long long)r.left_on_queue);
+    }
+    if (recover.empty())
+        printf("Finished in %.0fms (%.0f distinct states/s)\n", r.seconds * 1e3, r.distinct / (r.seconds > 0 ? r.seconds : 1));
+    else
+        printf("Finished in %.0fms after recovery (counts include the checkpointed levels)\n", r.seconds * 1e3);
     rmc_destroy(ctx);
     return exitcode;
 }

@@ -25,7 +25,7 @@ FAMILIES = ("Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest"
             "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
             "DropMessage")
 ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "HIP", -28: "CAPACITY", -19: "NOGPU",
-          -74: "PARSE", -71: "STATE"}
+          -74: "PARSE", -71: "STATE", -61: "IO"}
 
 
 class Config(C.Structure):
@@ -101,7 +101,7 @@ EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_ru
            "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
            "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level", "rmc_dist_state",
            "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits",
-           "rmc_sim_config_from_files")
+           "rmc_sim_config_from_files", "rmc_checkpoint", "rmc_recover")
 
 _lib = None
 
@@ -139,6 +139,10 @@ def native():
         lib.rmc_sim_config_from_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Config),
                                                   C.POINTER(SimConfig), C.c_char_p, C.c_size_t]
         lib.rmc_sim_config_from_files.restype = C.c_int
+        lib.rmc_checkpoint.argtypes = [C.c_void_p, C.c_char_p]
+        lib.rmc_checkpoint.restype = C.c_int
+        lib.rmc_recover.argtypes = [C.c_void_p, C.c_char_p]
+        lib.rmc_recover.restype = C.c_int
         lib.rmc_probe_bench.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int,
                                         C.POINTER(C.c_double)]
         lib.rmc_probe_bench.restype = C.c_int
@@ -275,6 +279,14 @@ class Checker:
         n = C.c_size_t()
         self._check(self.lib.rmc_sim_replay(self.ctx, C.byref(sc), behaviour, st, depth, C.byref(n)))
         return [st[k] for k in range(min(n.value, depth))]
+
+    def checkpoint(self, path: str):
+        """Write the stopped search to `path` (rmc_checkpoint; TLC -checkpoint)."""
+        self._check(self.lib.rmc_checkpoint(self.ctx, path.encode()))
+
+    def recover(self, path: str):
+        """Load a checkpoint; the next run() continues it (rmc_recover; TLC -recover)."""
+        self._check(self.lib.rmc_recover(self.ctx, path.encode()))
 
     def set_fp_bits(self, bits: int):
         """Verification-mode test hook: keep only `bits` fingerprint bits (rmc_set_fp_bits)."""

@@ -195,3 +195,53 @@ def test_cli_simulation_mode():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "SmokeInit: 19683 initial states (k = 3)." in r.stdout
     assert "No error has been found in 65536 behaviours." in r.stdout
+
+
+@pytest.mark.parametrize("name,stop", [("tiny2_v2", 9), ("small_sym", 12), ("bounded_full", 30)])
+def test_checkpoint_and_recover(name, stop, tmp_path):
+    """TLC -checkpoint / -recover: a search stopped at level `stop`, written,
+    loaded into a fresh context (the fingerprint set is rebuilt from the
+    states) and continued, ends with the full search's exact counts."""
+    g = GOLDEN[name]
+    p = dict(g["params"], max_depth=stop)
+    cap = max(1 << 22, int(g["distinct"] * 1.25))
+    with rmc.Checker(cfg_from(p, capacity=cap)) as ck:
+        r1 = ck.run()
+        assert r1.depth == stop and r1.left_on_queue > 0
+        ck.checkpoint(str(tmp_path / "ck"))
+    with rmc.Checker(cfg_from(g["params"], capacity=cap)) as ck:
+        ck.recover(str(tmp_path / "ck"))
+        r2 = ck.run()
+        levels = [lv[3] for lv in ck.levels if lv[3]]
+    assert (r2.distinct, r2.generated, r2.depth, r2.left_on_queue) == (g["distinct"], g["generated"], g["depth"], 0)
+    assert levels == g["level_new"][stop:]
+
+
+def test_recover_continues_to_the_violation_and_its_trace(tmp_path):
+    g = GOLDEN["bug_one_leader"]
+    p = g["params"]
+    with rmc.Checker(cfg_from(dict(p, max_depth=6))) as ck:
+        ck.run()
+        ck.checkpoint(str(tmp_path / "ck"))
+    with rmc.Checker(cfg_from(p)) as ck:
+        ck.recover(str(tmp_path / "ck"))
+        res = ck.run()
+        trace = ck.trace()
+    assert (res.violated_inv, res.violation_depth) == (g["violated_inv"], g["violation_depth"])
+    assert (res.distinct, res.generated) == (g["distinct"], g["generated"])
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"], bug_quorum=True)
+    check_trace(model, trace, res.violated_inv, res.violation_depth)
+
+
+def test_recover_rejects_another_model(tmp_path):
+    g = GOLDEN["tiny2"]
+    with rmc.Checker(cfg_from(dict(g["params"], max_depth=5))) as ck:
+        ck.run()
+        ck.checkpoint(str(tmp_path / "ck"))
+    other = dict(g["params"], max_term=g["params"]["max_term"] + 1)
+    with rmc.Checker(cfg_from(other)) as ck:
+        with pytest.raises(rmc.RmcError, match="another model"):
+            ck.recover(str(tmp_path / "ck"))
+        with pytest.raises(rmc.RmcError, match="not an rmc checkpoint|cannot open"):
+            ck.recover(str(tmp_path / "missing"))
