@@ -59,6 +59,9 @@ extern "C" {
 #define RMC_INV_TYPEOK (1u << 0)           /* raft.tla:482-492                          */
 #define RMC_INV_ONE_LEADER (1u << 1)       /* ElectionSafety restated (raft.tla:1124)   */
 #define RMC_INV_LOG_MATCHING (1u << 2)     /* raft.tla:1132-1136                        */
+#define RMC_INV_MESSAGES (1u << 3)         /* MessagesInv raft.tla:941-946 (:910 fixed)  */
+#define RMC_INV_LEADER_VOTES (1u << 4)     /* LeaderVotesQuorum raft.tla:1033-1037       */
+#define RMC_INV_CAND_TERM (1u << 5)        /* CandidateTermNotInLog raft.tla:1041-1047   */
 
 /* A bounded model: constants of the MC module + the CONSTRAINT bounds.
  * Replaces the CONSTANTS / CONSTRAINT / INVARIANT / SYMMETRY / CHECK_DEADLOCK

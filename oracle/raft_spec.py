@@ -479,10 +479,63 @@ def log_matching(model, s):  # raft.tla:1132-1136
     return True
 
 
+def messages_inv(model, s):
+    """MessagesInv (raft.tla:941-946) with `m.dest` of :910 read as `m.mdest`.
+    `log[src][mprevLogIndex + 1]` outside DOMAIN log[src] is a TLC evaluation
+    error; it counts as a violation here."""
+    ct, lg = s.currentTerm, s.log
+    for m, _c in s.messages:
+        t, src, dst, mt = (rget(m, k) for k in ("mtype", "msource", "mdest", "mterm"))
+        if mt > ct[src]:  # MessageTermsLtCurrentTerm :934-935
+            return False
+        if t == RVP and rget(m, "mvoteGranted") and ct[src] == ct[dst] == mt:  # :903-910
+            ld, ls = last_term(lg[dst]), last_term(lg[src])
+            if not (ld > ls or (ld == ls and len(lg[dst]) >= len(lg[src]))):
+                return False
+        if t == RVQ and s.state[src] == CANDIDATE and ct[src] == mt:  # :915-920
+            if rget(m, "mlastLogIndex") != len(lg[src]) or \
+                    rget(m, "mlastLogTerm") != last_term(lg[src]):
+                return False
+        if t == AEQ and rget(m, "mentries") and mt == ct[src]:  # :924-930
+            p = rget(m, "mprevLogIndex")
+            if not 1 <= p + 1 <= len(lg[src]):
+                return False
+            if lg[src][p] != rget(m, "mentries")[0]:
+                return False
+            if 0 < p <= len(lg[src]) and rget(lg[src][p - 1], "term") != rget(m, "mprevLogTerm"):
+                return False
+    return True
+
+
+def leader_votes_quorum(model, s):  # raft.tla:1033-1037
+    for i in model.servers:
+        if s.state[i] == LEADER:
+            q = {j for j in model.servers if s.currentTerm[j] > s.currentTerm[i] or
+                 (s.currentTerm[j] == s.currentTerm[i] and s.votedFor[j] == i)}
+            if not is_quorum(model, q):
+                return False
+    return True
+
+
+def candidate_term_not_in_log(model, s):  # raft.tla:1041-1047
+    for i in model.servers:
+        if s.state[i] != CANDIDATE:
+            continue
+        q = {j for j in model.servers if s.currentTerm[j] == s.currentTerm[i] and
+             s.votedFor[j] in (i, NIL)}
+        if is_quorum(model, q) and any(rget(e, "term") == s.currentTerm[i]
+                                       for j in model.servers for e in s.log[j]):
+            return False
+    return True
+
+
 INVARIANTS = {
     "TypeOK": type_ok,
     "OneLeaderPerTerm": one_leader_per_term,
     "LogMatching": log_matching,
+    "MessagesInv": messages_inv,
+    "LeaderVotesQuorum": leader_votes_quorum,
+    "CandidateTermNotInLog": candidate_term_not_in_log,
 }
 
 

@@ -71,6 +71,9 @@ typedef struct {
 #define INV_TYPEOK 1
 #define INV_ONE_LEADER 2
 #define INV_LOG_MATCHING 4
+#define INV_MESSAGES 8
+#define INV_LEADER_VOTES 16
+#define INV_CAND_TERM 32
 
 /* ---------------- helpers (raft.tla:81-108) ---------------- */
 static int popc(unsigned x) { return __builtin_popcount(x); }
@@ -354,11 +357,66 @@ static int log_matching(const omodel_t* M, const ost_t* s) { /* raft.tla:1132-11
     return 1;
 }
 
+/* MessagesInv raft.tla:941-946 over every message of the bag (:910's `m.dest`
+ * read as `m.mdest`); log[src][mprevLogIndex + 1] outside DOMAIN log[src] (a TLC
+ * evaluation error) counts as a violation. */
+static int messages_inv(const omodel_t* M, const ost_t* s) {
+    (void)M;
+    for (int q = 0; q < s->nmsg; q++) {
+        const msg_t* m = &s->msg[q];
+        int src = m->src, dst = m->dst, cs = s->ct[src];
+        if (m->term > cs) return 0; /* MessageTermsLtCurrentTerm :934-935 */
+        if (m->type == RVP && m->a && cs == s->ct[dst] && cs == m->term) { /* :903-910 */
+            int ld = last_term(s, dst), ls = last_term(s, src);
+            if (!(ld > ls || (ld == ls && s->len[dst] >= s->len[src]))) return 0;
+        }
+        if (m->type == RVQ && s->st[src] == CANDIDATE && cs == m->term) /* :915-920 */
+            if (m->b != s->len[src] || m->a != last_term(s, src)) return 0;
+        if (m->type == AEQ && m->n > 0 && m->term == cs) { /* :924-930 */
+            int p = m->a; /* mprevLogIndex */
+            if (p + 1 < 1 || p + 1 > s->len[src]) return 0;
+            if (memcmp(&s->log[src][p], &m->e[0], sizeof(ent_t)) != 0) return 0;
+            if (p > 0 && p <= s->len[src] && s->log[src][p - 1].term != m->b) return 0;
+        }
+    }
+    return 1;
+}
+
+/* LeaderVotesQuorum raft.tla:1033-1037 */
+static int leader_votes_quorum(const omodel_t* M, const ost_t* s) {
+    for (int i = 0; i < M->S; i++) {
+        if (s->st[i] != LEADER) continue;
+        unsigned q = 0;
+        for (int j = 0; j < M->S; j++)
+            if (s->ct[j] > s->ct[i] || (s->ct[j] == s->ct[i] && s->vf[j] == i)) q |= 1u << j;
+        if (!is_quorum(M, q)) return 0;
+    }
+    return 1;
+}
+
+/* CandidateTermNotInLog raft.tla:1041-1047 */
+static int candidate_term_not_in_log(const omodel_t* M, const ost_t* s) {
+    for (int i = 0; i < M->S; i++) {
+        if (s->st[i] != CANDIDATE) continue;
+        unsigned q = 0;
+        for (int j = 0; j < M->S; j++)
+            if (s->ct[j] == s->ct[i] && (s->vf[j] == i || s->vf[j] == NIL)) q |= 1u << j;
+        if (!is_quorum(M, q)) continue;
+        for (int j = 0; j < M->S; j++)
+            for (int n = 0; n < s->len[j]; n++)
+                if (s->log[j][n].term == s->ct[i]) return 0;
+    }
+    return 1;
+}
+
 /* returns 0 if ok, else the bit of the first violated invariant */
 static int check_invariants(const omodel_t* M, const ost_t* s) {
     if ((M->inv_mask & INV_TYPEOK) && !type_ok(M, s)) return INV_TYPEOK;
     if ((M->inv_mask & INV_ONE_LEADER) && !one_leader_per_term(M, s)) return INV_ONE_LEADER;
     if ((M->inv_mask & INV_LOG_MATCHING) && !log_matching(M, s)) return INV_LOG_MATCHING;
+    if ((M->inv_mask & INV_MESSAGES) && !messages_inv(M, s)) return INV_MESSAGES;
+    if ((M->inv_mask & INV_LEADER_VOTES) && !leader_votes_quorum(M, s)) return INV_LEADER_VOTES;
+    if ((M->inv_mask & INV_CAND_TERM) && !candidate_term_not_in_log(M, s)) return INV_CAND_TERM;
     return 0;
 }
 

@@ -527,12 +527,79 @@ RMC_HD int log_matching(const u64 (&w)[S]) {  // raft.tla:1132-1136
         }
     return 1;
 }
+// MessagesInv (raft.tla:941-946): every message in the bag satisfies
+// RequestVoteResponseInv (:903-910, `m.dest` of :910 read as `m.mdest`),
+// RequestVoteRequestInv (:915-920), AppendEntriesRequestInv (:924-930) and
+// MessageTermsLtCurrentTerm (:934-935).  `log[src][mprevLogIndex + 1]` outside
+// DOMAIN log[src] (a TLC evaluation error) counts as a violation.
+template <int S, int K>
+RMC_HD int messages_inv(const u64 (&w)[S], const u32 (&m)[K]) {
+    for (int q = 0; q < K; ++q) {
+        const u32 sl = m[q];
+        if (!sl) continue;
+        const u32 ty = m_type(sl), src = m_src(sl), dst = m_dst(sl), mt = m_term(sl);
+        const u64 ws = selw<S>(w, (int)src), wd = selw<S>(w, (int)dst);
+        const u32 cs = w_ct(ws);
+        if (mt > cs) return 0;                                   // :934-935
+        if (ty == RVP && ((sl >> 12) & 1u) && cs == w_ct(wd) && cs == mt) {  // :903-910
+            const u32 ld = w_last_term(wd), ls = w_last_term(ws);
+            if (!(ld > ls || (ld == ls && w_len(wd) >= w_len(ws)))) return 0;
+        }
+        if (ty == RVQ && w_st(ws) == CANDIDATE && cs == mt) {    // :915-920
+            if (((sl >> 16) & 3u) != w_len(ws) || ((sl >> 12) & 15u) != w_last_term(ws)) return 0;
+        }
+        if (ty == AEQ && ((sl >> 19) & 1u) && mt == cs) {        // :924-930
+            const u32 p1 = (sl >> 12) & 7u, n = w_len(ws);       // p1 = mprevLogIndex + 1
+            if (p1 < 1 || p1 > n) return 0;                      // out of DOMAIN log[src]
+            if (w_ent(ws, p1 - 1) != ((sl >> 20) & 31u)) return 0;
+            if (p1 >= 2 && ent_term(w_ent(ws, p1 - 2)) != ((sl >> 15) & 15u)) return 0;
+        }
+    }
+    return 1;
+}
+// LeaderVotesQuorum (raft.tla:1033-1037): a leader's term is backed by a quorum
+// that voted for it or has moved to a higher term.
+template <int S>
+RMC_HD int leader_votes_quorum(const u64 (&w)[S]) {
+    for (int i = 0; i < S; ++i) {
+        if (w_st(w[i]) != LEADER) continue;
+        const u32 ci = w_ct(w[i]);
+        int n = 0;
+        for (int j = 0; j < S; ++j)
+            n += (w_ct(w[j]) > ci || (w_ct(w[j]) == ci && w_vf(w[j]) == (u32)i)) ? 1 : 0;
+        if (2 * n <= S) return 0;
+    }
+    return 1;
+}
+// CandidateTermNotInLog (raft.tla:1041-1047): a candidate that can still win
+// (a quorum of its term voted for it or not at all) has no entry of its term in
+// any log.
+template <int S>
+RMC_HD int candidate_term_not_in_log(const u64 (&w)[S]) {
+    for (int i = 0; i < S; ++i) {
+        if (w_st(w[i]) != CANDIDATE) continue;
+        const u32 ci = w_ct(w[i]);
+        int n = 0;
+        for (int j = 0; j < S; ++j) {
+            const u32 vf = w_vf(w[j]);
+            n += (w_ct(w[j]) == ci && (vf == (u32)i || vf == NILV)) ? 1 : 0;
+        }
+        if (2 * n <= S) continue;
+        for (int j = 0; j < S; ++j)
+            for (u32 x = 0; x < w_len(w[j]); ++x)
+                if (ent_term(w_ent(w[j], x)) == ci) return 0;
+    }
+    return 1;
+}
 // 0 = all hold, else 1 + index of the first violated invariant bit.
 template <int S, int K>
 RMC_HD int check_invariants(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
     if ((P.inv_mask & 1) && !type_ok<S, K>(w, m, P.V)) return 1;
     if ((P.inv_mask & 2) && !one_leader_per_term<S>(w)) return 2;
     if ((P.inv_mask & 4) && !log_matching<S>(w)) return 3;
+    if ((P.inv_mask & 8) && !messages_inv<S, K>(w, m)) return 4;
+    if ((P.inv_mask & 16) && !leader_votes_quorum<S>(w)) return 5;
+    if ((P.inv_mask & 32) && !candidate_term_not_in_log<S>(w)) return 6;
     return 0;
 }
 

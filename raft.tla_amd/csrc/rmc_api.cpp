@@ -78,7 +78,7 @@ int validate(const rmc_config* c, std::string* why) {
     if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
     if ((c->flags & RMC_FLAG_SYMMETRY) && c->n_servers > 4)
         return bad("SYMMETRY is supported for up to 4 servers");
-    if (c->invariants & ~7u) return bad("unknown invariant bit");
+    if (c->invariants & ~63u) return bad("unknown invariant bit");
     if ((c->flags & RMC_FLAG_VERIFY_STATES) && (c->flags & RMC_FLAG_SYMMETRY))
         return bad("full-state verification is not supported with SYMMETRY");
     return 0;
@@ -460,10 +460,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
     depth = c->h_ctr->count ? 1 : 0;
     if (c->h_ctr->viol != ~0ull) {
-        c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 3);
+        c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 7);
         c->res.violation_depth = 1;
         c->have_target = 1;
-        c->target_idx = c->h_ctr->viol >> 2;
+        c->target_idx = c->h_ctr->viol >> 3;
     }
     }  // !resume
     const u64 CHUNK = 1ull << 26;
@@ -519,10 +519,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         }
         c->res.distinct = k.count;
         if (k.viol != ~0ull) {
-            c->res.violated_inv = 1 << (int)(k.viol & 3);
+            c->res.violated_inv = 1 << (int)(k.viol & 7);
             c->res.violation_depth = depth;
             c->have_target = 1;
-            c->target_idx = k.viol >> 2;
+            c->target_idx = k.viol >> 3;
         } else if ((c->cfg.flags & RMC_FLAG_CHECK_DEADLOCK) && k.deadlock != ~0ull) {
             c->res.deadlock = 1;
             c->have_target = 1;
@@ -908,8 +908,8 @@ int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_b
     out->truncated = h.truncated;
     out->deadlocked = h.deadlocked;
     if (h.viol != ~0ull) {
-        out->violated_inv = 1 << (int)((h.viol >> 40) & 3);
-        out->violation_depth = (int32_t)(h.viol >> 42);
+        out->violated_inv = 1 << (int)((h.viol >> 40) & 7);
+        out->violation_depth = (int32_t)(h.viol >> 43);
         out->violation_behaviour = h.viol & ((1ull << 40) - 1);
     }
     out->kernel_seconds = 1e-3 * ms;
@@ -1069,8 +1069,8 @@ int rmc_dist_end_level(rmc_ctx* c, uint64_t* out) {
     out[0] = k.count - hi;
     out[1] = k.generated;
     out[2] = k.probes;
-    out[3] = k.viol != ~0ull ? (k.viol >> 2) + 1 : 0;
-    out[4] = k.viol != ~0ull ? (1ull << (k.viol & 3)) : 0;
+    out[3] = k.viol != ~0ull ? (k.viol >> 3) + 1 : 0;
+    out[4] = k.viol != ~0ull ? (1ull << (k.viol & 7)) : 0;
     c->res.generated += k.generated;
     c->res.probes += k.probes;
     c->res.distinct = k.count;  // states stored on this rank

@@ -371,6 +371,9 @@ static int parse_model(const char* cfg_path, const char* tla_path, rmc_config* o
         if (in == "TypeOK") g.invariants |= RMC_INV_TYPEOK;
         else if (in == "OneLeaderPerTerm") g.invariants |= RMC_INV_ONE_LEADER;
         else if (in == "LogMatching") g.invariants |= RMC_INV_LOG_MATCHING;
+        else if (in == "MessagesInv") g.invariants |= RMC_INV_MESSAGES;
+        else if (in == "LeaderVotesQuorum") g.invariants |= RMC_INV_LEADER_VOTES;
+        else if (in == "CandidateTermNotInLog") g.invariants |= RMC_INV_CAND_TERM;
         else return fail("INVARIANT " + in + " is not compiled into the engine");
     }
     for (const auto& sy : C.symmetry) {

@@ -180,7 +180,7 @@ __device__ __forceinline__ void commit_new(int is_new, const u64 (&w)[S], const 
     B.parent[ni] = parent_idx;
     B.act[ni] = (uint8_t)lane;
     const int v = check_invariants<S, K>(wo, mo, P);
-    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
+    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 3) | (u64)(v - 1)));
 }
 
 // Per-wave list of new states, kept in LDS until a flush materialises them.
@@ -226,7 +226,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
         const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 3) | (u64)(v - 1)));
     }
     wave_sync_lds();
 }
@@ -423,7 +423,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
             B.parent[slot] = B.ref_tag | (lo + rel);
             B.act[slot] = (uint8_t)lane;
             const int v = check_invariants<S, K>(wo, mo, P);
-            if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 2) | (u64)(v - 1)));
+            if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 3) | (u64)(v - 1)));
         } else {
             if (slot >= B.ocap) {
                 atomicOr(&B.ctr->overflow, 2u);
@@ -684,7 +684,7 @@ __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, 
         B.parent[ni] = ref & ~(0xFFull << 40);
         B.act[ni] = (uint8_t)(ref >> 40);
         const int v = check_invariants<S, K>(w, m, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 2) | (u64)(v - 1)));
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 3) | (u64)(v - 1)));
     }
     wave_sync_lds();
 }
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
         const bool record = (i64)t == rec_beh;
         if (record) store_state<S, K>(rec, w, m);
         int v = check_invariants<S, K>(w, m, P);
-        if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 42) | ((u64)(v - 1) << 40) | t));
+        if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 43) | ((u64)(v - 1) << 40) | t));
         for (int dd = 2; dd <= depth && !v; ++dd) {
             u32 cnt = 0;
             int pick = -1;
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
             v = check_invariants<S, K>(w, m, P);
             if (v)
                 atomicMin((unsigned long long*)&out->viol,
-                          (unsigned long long)(((u64)dd << 42) | ((u64)(v - 1) << 40) | t));
+                          (unsigned long long)(((u64)dd << 43) | ((u64)(v - 1) << 40) | t));
         }
     }
     atomicAdd((unsigned long long*)&out->steps, (unsigned long long)steps);

@@ -101,6 +101,9 @@ const char* inv_name(int bit) {
         case RMC_INV_TYPEOK: return "TypeOK";
         case RMC_INV_ONE_LEADER: return "OneLeaderPerTerm";
         case RMC_INV_LOG_MATCHING: return "LogMatching";
+        case RMC_INV_MESSAGES: return "MessagesInv";
+        case RMC_INV_LEADER_VOTES: return "LeaderVotesQuorum";
+        case RMC_INV_CAND_TERM: return "CandidateTermNotInLog";
     }
     return "?";
 }

@@ -18,9 +18,11 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
 
 MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8
 FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES = 1, 2, 4, 8
-INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING = 1, 2, 4
+INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING, INV_MESSAGES = 1, 2, 4, 8
+INV_LEADER_VOTES, INV_CAND_TERM = 16, 32
 INV_NAMES = {INV_TYPEOK: "TypeOK", INV_ONE_LEADER: "OneLeaderPerTerm",
-             INV_LOG_MATCHING: "LogMatching"}
+             INV_LOG_MATCHING: "LogMatching", INV_MESSAGES: "MessagesInv",
+             INV_LEADER_VOTES: "LeaderVotesQuorum", INV_CAND_TERM: "CandidateTermNotInLog"}
 FAMILIES = ("Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
             "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
             "DropMessage")

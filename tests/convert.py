@@ -152,6 +152,8 @@ def check_trace(model, trace, violated_inv, violation_depth):
         succ = {(f, t) for f, _p, t in R.successors(model, a)}
         assert (rmc.FAMILIES[fam], b) in succ
         assert R.in_constraint(model, b)
-    inv = {rmc.INV_ONE_LEADER: R.one_leader_per_term, rmc.INV_LOG_MATCHING: R.log_matching}
+    inv = {rmc.INV_ONE_LEADER: R.one_leader_per_term, rmc.INV_LOG_MATCHING: R.log_matching,
+           rmc.INV_MESSAGES: R.messages_inv, rmc.INV_LEADER_VOTES: R.leader_votes_quorum,
+           rmc.INV_CAND_TERM: R.candidate_term_not_in_log}
     assert not inv[violated_inv](model, states[-1])
     assert all(inv[violated_inv](model, s) for s in states[:-1])

@@ -55,6 +55,9 @@ def test_version_and_state_bytes():
     ("MCraft5", (5, 2, 2, 1, 2, 1, rmc.FLAG_CHECK_DEADLOCK, rmc.INV_TYPEOK)),
     ("MCraftBug", (3, 2, 3, 1, 3, 1, rmc.FLAG_CHECK_DEADLOCK | rmc.FLAG_BUG_QUORUM,
                    rmc.INV_ONE_LEADER | rmc.INV_LOG_MATCHING)),
+    ("MCraftMessages", (3, 2, 2, 1, 1, 1, rmc.FLAG_CHECK_DEADLOCK, rmc.INV_TYPEOK | rmc.INV_MESSAGES)),
+    ("MCraftElections", (3, 2, 2, 1, 1, 1, rmc.FLAG_CHECK_DEADLOCK,
+                         rmc.INV_TYPEOK | rmc.INV_LEADER_VOTES | rmc.INV_CAND_TERM)),
 ])
 def test_front_end_reads_tlc_models(name, expect):
     c = rmc.config_from_files(os.path.join(SPECS, name + ".cfg"))

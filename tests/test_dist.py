@@ -91,7 +91,8 @@ def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,nproc", [("bug_one_leader", 2), ("bug_log_matching", 3), ("bug_both", 2)])
+@pytest.mark.parametrize("case,nproc", [("bug_one_leader", 2), ("bug_log_matching", 3), ("bug_both", 2),
+                                        ("messages_small", 2), ("bug_cand_term", 3)])
 def test_sharded_violation_and_trace(case, nproc, tmp_path):
     """Bug variant (config 5) on N ranks: the violation, its minimal depth and the
     counts at the stopping level equal the oracle's, and the counterexample,
@@ -109,6 +110,6 @@ def test_sharded_violation_and_trace(case, nproc, tmp_path):
     assert res["distinct"] == g["distinct"] and res["generated"] == g["generated"]
     model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
                     max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
-                    bug_quorum=True)
+                    bug_quorum=bool(p["bug_quorum"]))
     trace = [(f, i, rmc.StateView.from_buffer_copy(bytes.fromhex(h))) for f, i, h in res["trace"]]
     check_trace(model, trace, res["violated_inv"], res["violation_depth"])

@@ -49,7 +49,7 @@ def test_kat_first_levels():
     assert res.generated == 1 + 6 + 9
 
 
-BFS_CASES = ["bounded_full", "tiny2", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
+BFS_CASES = ["bounded_full", "tiny2", "messages_tiny2", "elections_small", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
              "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9"]
 
 
@@ -110,7 +110,8 @@ def test_full_state_verification_reports_collisions(bits):
     assert res.verified == res.probes - (res.distinct - 1)
 
 
-@pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both"])
+@pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both", "bug_messages",
+                                  "messages_small", "bug_leader_votes", "bug_cand_term"])
 def test_bug_variant_violation_and_trace(name):
     g = GOLDEN[name]
     p = g["params"]
@@ -121,7 +122,7 @@ def test_bug_variant_violation_and_trace(name):
     # the trace is a behaviour of the spec from Init to a violating state
     model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
                     max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
-                    bug_quorum=True)
+                    bug_quorum=bool(p["bug_quorum"]))
     check_trace(model, trace, res.violated_inv, res.violation_depth)
 
 
