@@ -591,15 +591,38 @@ RMC_HD int candidate_term_not_in_log(const u64 (&w)[S]) {
     }
     return 1;
 }
+// The invariants other than TypeOK, out of line: inlined into every expansion
+// kernel's new-state paths they would grow the code by ~15 % for checks that
+// the bench model never names.  The state travels by value (in VGPRs).
+template <int S, int K>
+struct PackedState {
+    u64 w[S];
+    u32 m[K];
+};
+#if defined(__HIPCC__)
+#define RMC_HD_COLD __host__ __device__ __noinline__
+#else
+#define RMC_HD_COLD inline
+#endif
+template <int S, int K>
+RMC_HD_COLD int check_named_invariants(const PackedState<S, K> s, int mask) {
+    if ((mask & 2) && !one_leader_per_term<S>(s.w)) return 2;
+    if ((mask & 4) && !log_matching<S>(s.w)) return 3;
+    if ((mask & 8) && !messages_inv<S, K>(s.w, s.m)) return 4;
+    if ((mask & 16) && !leader_votes_quorum<S>(s.w)) return 5;
+    if ((mask & 32) && !candidate_term_not_in_log<S>(s.w)) return 6;
+    return 0;
+}
 // 0 = all hold, else 1 + index of the first violated invariant bit.
 template <int S, int K>
 RMC_HD int check_invariants(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
     if ((P.inv_mask & 1) && !type_ok<S, K>(w, m, P.V)) return 1;
-    if ((P.inv_mask & 2) && !one_leader_per_term<S>(w)) return 2;
-    if ((P.inv_mask & 4) && !log_matching<S>(w)) return 3;
-    if ((P.inv_mask & 8) && !messages_inv<S, K>(w, m)) return 4;
-    if ((P.inv_mask & 16) && !leader_votes_quorum<S>(w)) return 5;
-    if ((P.inv_mask & 32) && !candidate_term_not_in_log<S>(w)) return 6;
+    if (P.inv_mask & ~1) {
+        PackedState<S, K> s;
+        for (int i = 0; i < S; ++i) s.w[i] = w[i];
+        for (int q = 0; q < K; ++q) s.m[q] = m[q];
+        return check_named_invariants<S, K>(s, P.inv_mask);
+    }
     return 0;
 }
 
