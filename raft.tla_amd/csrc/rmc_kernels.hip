@@ -648,6 +648,21 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
     expand_body<S, K, SYM, BATCH, DIST, VERIFY>(P, PT, B, lo, hi);
 }
 
+// SYMMETRY expansion (canonicalisation over the S! server permutations): 205
+// VGPRs for S = 3 unconstrained, i.e. 2 waves/SIMD to hide the fingerprint-set
+// latency.  RMC_SYM_WPE caps the register budget of the S = 3, K = 4 variant
+// (config 2; 48 B of spills); the others spill heavily under the cap and stay
+// uncapped.  0 = no cap.
+#ifndef RMC_SYM_WPE
+#define RMC_SYM_WPE 3
+#endif
+template <int S, int K, int BATCH>
+__global__ __launch_bounds__(256) __attribute__((
+    amdgpu_waves_per_eu((S == 3 && K == 4 && RMC_SYM_WPE) ? RMC_SYM_WPE : 1))) void
+k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    expand_body<S, K, true, BATCH, false, false>(P, PT, B, lo, hi);
+}
+
 // The sharded expansion at 6 waves/SIMD (its owner bookkeeping takes 82 VGPRs
 // unconstrained: 5 waves): the register budget is capped for this variant only.
 template <int S, int K, int BATCH>
@@ -991,7 +1006,7 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     if (which == 0) {
         if constexpr (SYM) {
             if (verify) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+            hipLaunchKernelGGL((k_expand_sym<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         } else if (verify) {
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
