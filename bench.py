@@ -101,7 +101,8 @@ def main():
         dev = a.device if a.device >= 0 else local
         torch.cuda.set_device(dev)
         dist.init_process_group(a.dist_backend, init_method="env://")
-    cfg = rmc.config_from_files(a.config)
+    # the GPU box has no raft.tla: the bench model checks the compiled-in lemmy/raft.tla
+    cfg = rmc.config_from_files(a.config, builtin_raft=True)
     cfg.device = (a.device if a.device >= 0 else local) if sharded else max(a.device, 0)
     cfg.state_capacity = a.capacity or int(1.5e9 / world * (1.3 if sharded else 1.0))
     W = rmc.native().rmc_state_bytes(cfg)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 1
+#define RMC_ABI_VERSION 2
 
 /* Capacity of the packed encoding (DESIGN.md "Packed state"). */
 #define RMC_MAX_SERVERS 5
@@ -62,6 +62,13 @@ extern "C" {
 #define RMC_INV_MESSAGES (1u << 3)         /* MessagesInv raft.tla:941-946 (:910 fixed)  */
 #define RMC_INV_LEADER_VOTES (1u << 4)     /* LeaderVotesQuorum raft.tla:1033-1037       */
 #define RMC_INV_CAND_TERM (1u << 5)        /* CandidateTermNotInLog raft.tla:1041-1047   */
+/* The IsPrefix invariants (raft.tla:1143-1180), restated in specs/MCraftBounded.tla
+ * with IsPrefix defined and Committed(i) = the first min(commitIndex[i], Len(log[i]))
+ * entries of log[i] (raft.tla's SubSeq is out of range when commitIndex > Len). */
+#define RMC_INV_VOTES_GRANTED (1u << 6)    /* VotesGrantedInv raft.tla:1145-1153         */
+#define RMC_INV_QUORUM_LOG (1u << 7)       /* QuorumLogInv raft.tla:1157-1161            */
+#define RMC_INV_MORE_UP_TO_DATE (1u << 8)  /* MoreUpToDateCorrect raft.tla:1167-1172     */
+#define RMC_INV_LEADER_COMPLETE (1u << 9)  /* LeaderCompleteness raft.tla:1176-1180      */
 
 /* A bounded model: constants of the MC module + the CONSTRAINT bounds.
  * Replaces the CONSTANTS / CONSTRAINT / INVARIANT / SYMMETRY / CHECK_DEADLOCK
@@ -247,6 +254,10 @@ typedef struct rmc_sim_result {
     double kernel_seconds;     /* device time of the walks (HIP events)           */
 } rmc_sim_result;
 int rmc_simulate(rmc_ctx* ctx, const rmc_sim_config* sc, rmc_sim_result* out);
+/* The initial states rmc_simulate draws for sc (SmokeInit, sc->smoke_k >= 1):
+ * host-only, no device needed.  *n receives k^9 even if it exceeds cap. */
+int rmc_smoke_init(const rmc_config* cfg, const rmc_sim_config* sc, rmc_state_view* states,
+                   size_t cap, size_t* n);
 /* Re-runs behaviour `behaviour` of the same rmc_sim_config and returns its states. */
 int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, rmc_state_view* states,
                    size_t cap, size_t* len);
@@ -290,21 +301,53 @@ int rmc_dist_state(rmc_ctx* ctx, uint64_t index, rmc_state_view* state, int32_t*
 int rmc_probe_bench(int device, uint64_t table_bytes, uint64_t accesses, int mode, double* per_second);
 
 /* ---- front-end -----------------------------------------------------------
- * Reads a TLC model (.tla root module + .cfg) of raft.tla and fills *cfg.
- * Recognises: CONSTANTS (model values, `X <- def`, `Name = n` for bounds),
- * SPECIFICATION / INIT / NEXT, INVARIANT(S), CONSTRAINT(S), SYMMETRY,
- * CHECK_DEADLOCK, and `BecomeLeader <- Def` overrides whose body weakens the
- * quorum guard.  `tla_path` may be NULL (the module next to cfg_path with the
- * same stem is used).  Errors name the unsupported construct in err. */
+ * Replaces TLC's SANY + cfg reading for this spec: reads a TLC model (root
+ * .tla module, the modules it EXTENDS next to it, its .cfg, and raft.tla) and
+ * fills *cfg — or refuses it, naming the construct the engine does not
+ * compile.  The engine compiles lemmy/raft.tla:1-505 and nothing else, so:
+ *  - raft.tla is read (raft_path, else $RMC_RAFT_TLA, else next to the
+ *    model) and every top-level unit of its module body must match the
+ *    compiled-in text (comments and whitespace normalised).  The one edit
+ *    recognised is config 5's weakened quorum guard in BecomeLeader
+ *    (raft.tla:197 `votesGranted[i] /= {}`), which sets RMC_FLAG_BUG_QUORUM.
+ *    With no raft.tla on disk the call fails unless options has
+ *    RMC_FRONT_BUILTIN_RAFT (then the compiled-in text is used, and said so);
+ *  - CONSTANTS: model values, `X <- Def`, `Name = n`; Server and Value must
+ *    be set literals of distinct model values;
+ *  - CONSTRAINT(S): split into top-level conjuncts (bulleted or infix, through
+ *    definition references); every conjunct must be one of
+ *    `\A i \in Server : currentTerm[i] <= N /\ Len(log[i]) <= N`,
+ *    `Cardinality(DOMAIN messages) <= N`, `\A m \in DOMAIN messages :
+ *    messages[m] <= N` (<, =<, \leq too); anything else is refused;
+ *  - INVARIANT(S): TypeOK, or a name from RMC_INV_* whose definition (with the
+ *    model definitions it uses) is the compiled-in restatement;
+ *  - `BecomeLeader <- Def`: Def must be the compiled-in bug variant;
+ *  - SYMMETRY: exactly Permutations(Server) (or of Server's set definition);
+ *  - simulation (RMC_FRONT_SIMULATE, TLC -simulate): `Init <- SmokeInit` must
+ *    be Smokeraft's sampler (k and SmokeNat are read as its parameters); a
+ *    CONSTRAINT that only reads TLCGet/TLCSet is a run budget, replaced by
+ *    sim->behaviours; bounds the cfg does not give are the packed capacity.
+ * On success `info` receives the provenance notes (which raft.tla was
+ * verified, which overrides were recognised), on failure the error. */
+#define RMC_FRONT_BUILTIN_RAFT (1u << 0)
+#define RMC_FRONT_SIMULATE (1u << 1)
+int rmc_model_from_files(const char* cfg_path, const char* tla_path, const char* raft_path,
+                         uint32_t options, rmc_config* cfg, rmc_sim_config* sim,
+                         char* info, size_t info_cap);
+/* rmc_model_from_files for BFS / simulation models with raft_path = NULL and
+ * RMC_FRONT_BUILTIN_RAFT taken from the environment (RMC_BUILTIN_RAFT=1).
+ * `tla_path` may be NULL (the module next to cfg_path with the same stem). */
 int rmc_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* cfg,
                           char* err, size_t err_cap);
-/* The same for a simulation model (TLC -simulate on Smokeraft.tla/.cfg):
- * `Init <- SmokeInit` sets sim->smoke_k from `k ==` and sim->smoke_nat from
- * `SmokeNat == 0..N` (Smokeraft.tla:10-19); a CONSTRAINT that is not a state
- * bound (StopAfter, Smokeraft.tla:84-92) is accepted and replaced by
- * sim->behaviours; sim->depth defaults to 100 (TLC -depth). */
 int rmc_sim_config_from_files(const char* cfg_path, const char* tla_path, rmc_config* cfg,
                               rmc_sim_config* sim, char* err, size_t err_cap);
+/* TLC's location of an action of Next in raft.tla, as its counterexample
+ * headers print it (`State k: <Action line L1, col C1 to line L2, col C2 of
+ * module raft>`): the body of the action's definition.  `action` is a family
+ * name of rmc.h's lane table, "UpdateTerm", or "Receive:<mtype>" for the
+ * Receive disjunct of that message type (raft.tla:393-403).  out4 = L1, C1,
+ * L2, C2. */
+int rmc_action_location(const char* action, int32_t* out4);
 
 #ifdef __cplusplus
 }

@@ -529,6 +529,45 @@ def candidate_term_not_in_log(model, s):  # raft.tla:1041-1047
     return True
 
 
+def committed(s, i):
+    """Committed(i) as restated in specs/MCraftBounded.tla: raft.tla:896's
+    SubSeq(log[i], 1, commitIndex[i]) with the commit index clamped to
+    Len(log[i]) (this spec lets commitIndex exceed Len, raft.tla:309,323)."""
+    return s.log[i][:min(s.commitIndex[i], len(s.log[i]))]
+
+
+def is_prefix(a, b):  # SequencesExt's IsPrefix (not in raft.tla's EXTENDS)
+    return len(a) <= len(b) and b[:len(a)] == a
+
+
+def votes_granted_inv(model, s):  # raft.tla:1145-1153
+    return all(is_prefix(committed(s, j), s.log[i])
+               for i in model.servers for j in s.votesGranted[i]
+               if s.currentTerm[i] == s.currentTerm[j])
+
+
+def quorum_log_inv(model, s):  # raft.tla:1157-1161, every quorum enumerated
+    quorums = [set(q) for r in range(model.n_servers + 1)
+               for q in itertools.combinations(model.servers, r) if is_quorum(model, set(q))]
+    return all(any(is_prefix(committed(s, i), s.log[j]) for j in q)
+               for i in model.servers for q in quorums)
+
+
+def more_up_to_date_correct(model, s):  # raft.tla:1167-1172
+    for i in model.servers:
+        for j in model.servers:
+            li, lj = last_term(s.log[i]), last_term(s.log[j])
+            if (li > lj or (li == lj and len(s.log[i]) >= len(s.log[j]))) and \
+                    not is_prefix(committed(s, j), s.log[i]):
+                return False
+    return True
+
+
+def leader_completeness(model, s):  # raft.tla:1176-1180
+    return all(is_prefix(committed(s, j), s.log[i])
+               for i in model.servers if s.state[i] == LEADER for j in model.servers)
+
+
 INVARIANTS = {
     "TypeOK": type_ok,
     "OneLeaderPerTerm": one_leader_per_term,
@@ -536,7 +575,17 @@ INVARIANTS = {
     "MessagesInv": messages_inv,
     "LeaderVotesQuorum": leader_votes_quorum,
     "CandidateTermNotInLog": candidate_term_not_in_log,
+    "VotesGrantedInv": votes_granted_inv,
+    "QuorumLogInv": quorum_log_inv,
+    "MoreUpToDateCorrect": more_up_to_date_correct,
+    "LeaderCompleteness": leader_completeness,
 }
+
+
+# rmc.h's RMC_INV_* bits
+INV_BITS = {1: "TypeOK", 2: "OneLeaderPerTerm", 4: "LogMatching", 8: "MessagesInv",
+            16: "LeaderVotesQuorum", 32: "CandidateTermNotInLog", 64: "VotesGrantedInv",
+            128: "QuorumLogInv", 256: "MoreUpToDateCorrect", 512: "LeaderCompleteness"}
 
 
 # ---- symmetry (SYMMETRY Permutations(Server)) -------------------------------

@@ -74,6 +74,10 @@ typedef struct {
 #define INV_MESSAGES 8
 #define INV_LEADER_VOTES 16
 #define INV_CAND_TERM 32
+#define INV_VOTES_GRANTED 64
+#define INV_QUORUM_LOG 128
+#define INV_MORE_UP_TO_DATE 256
+#define INV_LEADER_COMPLETE 512
 
 /* ---------------- helpers (raft.tla:81-108) ---------------- */
 static int popc(unsigned x) { return __builtin_popcount(x); }
@@ -409,6 +413,47 @@ static int candidate_term_not_in_log(const omodel_t* M, const ost_t* s) {
     return 1;
 }
 
+/* The IsPrefix invariants (raft.tla:1143-1180) as restated in
+ * specs/MCraftBounded.tla: Committed(j) = the first min(commitIndex[j],
+ * Len(log[j])) entries of log[j]; IsPrefix(s, t) = Len(s) <= Len(t) and t
+ * starts with s. */
+static int committed_prefix_of(const ost_t* s, int j, int i) { /* IsPrefix(Committed(j), log[i]) */
+    int c = s->ci[j] < s->len[j] ? s->ci[j] : s->len[j];
+    if (s->len[i] < c) return 0;
+    return memcmp(s->log[i], s->log[j], (size_t)c * sizeof(ent_t)) == 0;
+}
+static int votes_granted_inv(const omodel_t* M, const ost_t* s) { /* raft.tla:1145-1153 */
+    for (int i = 0; i < M->S; i++)
+        for (int j = 0; j < M->S; j++)
+            if (((s->vG[i] >> j) & 1u) && s->ct[i] == s->ct[j] && !committed_prefix_of(s, j, i)) return 0;
+    return 1;
+}
+static int quorum_log_inv(const omodel_t* M, const ost_t* s) { /* raft.tla:1157-1161 */
+    for (int i = 0; i < M->S; i++) {
+        unsigned miss = 0; /* servers whose log lacks Committed(i): no quorum may lie inside */
+        for (int j = 0; j < M->S; j++)
+            if (!committed_prefix_of(s, i, j)) miss |= 1u << j;
+        if (is_quorum(M, miss)) return 0;
+    }
+    return 1;
+}
+static int more_up_to_date_correct(const omodel_t* M, const ost_t* s) { /* raft.tla:1167-1172 */
+    for (int i = 0; i < M->S; i++)
+        for (int j = 0; j < M->S; j++) {
+            int li = last_term(s, i), lj = last_term(s, j);
+            if ((li > lj || (li == lj && s->len[i] >= s->len[j])) && !committed_prefix_of(s, j, i)) return 0;
+        }
+    return 1;
+}
+static int leader_completeness(const omodel_t* M, const ost_t* s) { /* raft.tla:1176-1180 */
+    for (int i = 0; i < M->S; i++) {
+        if (s->st[i] != LEADER) continue;
+        for (int j = 0; j < M->S; j++)
+            if (!committed_prefix_of(s, j, i)) return 0;
+    }
+    return 1;
+}
+
 /* returns 0 if ok, else the bit of the first violated invariant */
 static int check_invariants(const omodel_t* M, const ost_t* s) {
     if ((M->inv_mask & INV_TYPEOK) && !type_ok(M, s)) return INV_TYPEOK;
@@ -417,6 +462,10 @@ static int check_invariants(const omodel_t* M, const ost_t* s) {
     if ((M->inv_mask & INV_MESSAGES) && !messages_inv(M, s)) return INV_MESSAGES;
     if ((M->inv_mask & INV_LEADER_VOTES) && !leader_votes_quorum(M, s)) return INV_LEADER_VOTES;
     if ((M->inv_mask & INV_CAND_TERM) && !candidate_term_not_in_log(M, s)) return INV_CAND_TERM;
+    if ((M->inv_mask & INV_VOTES_GRANTED) && !votes_granted_inv(M, s)) return INV_VOTES_GRANTED;
+    if ((M->inv_mask & INV_QUORUM_LOG) && !quorum_log_inv(M, s)) return INV_QUORUM_LOG;
+    if ((M->inv_mask & INV_MORE_UP_TO_DATE) && !more_up_to_date_correct(M, s)) return INV_MORE_UP_TO_DATE;
+    if ((M->inv_mask & INV_LEADER_COMPLETE) && !leader_completeness(M, s)) return INV_LEADER_COMPLETE;
     return 0;
 }
 

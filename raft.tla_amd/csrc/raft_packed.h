@@ -440,6 +440,71 @@ RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d
     return 1;
 }
 
+// The parent's per-component mixes, computed once per expanded state: a lane
+// then mixes only the components it creates (the new server word, the
+// decremented / incremented / added bag slot), about half of delta_fp's
+// mixes, and the hash is the expansion kernel's main VALU cost (a mix64 is
+// 17 VALU instructions, six of them quarter-rate 32-bit multiplies).
+template <int S, int K>
+struct ParentMix {
+    u64 hw[S];
+    u64 hm[K];
+    u64 h0;
+    int nmsg;
+};
+template <int S, int K>
+RMC_HD void parent_mix(const u64 (&w)[S], const u32 (&m)[K], ParentMix<S, K>& pm) {
+    pm.h0 = 0;
+    pm.nmsg = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) { pm.hw[i] = hS(w[i], (u32)i); pm.h0 += pm.hw[i]; }
+#pragma unroll
+    for (int q = 0; q < K; ++q) { pm.hm[q] = hM(m[q]); pm.h0 += pm.hm[q]; pm.nmsg += m[q] ? 1 : 0; }
+}
+template <int N>
+RMC_HD u64 sel64(const u64 (&a)[N], int i) {
+    u64 r = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) r |= a[k] & (0ull - (u64)(i == k));
+    return r;
+}
+// delta_fp with the parent's mixes precomputed: same result, fewer mixes.
+template <int S, int K>
+RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
+                        const Params& P, u64* h) {
+    u64 hh = pm.h0;
+    int nmsg = pm.nmsg;
+    if (d.srv >= 0) {
+        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
+        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
+        const u64 wo = selw<S>(w, d.srv);
+        if (d.w_new != wo) hh += hS(d.w_new, (u32)d.srv) - sel64<S>(pm.hw, d.srv);
+    }
+    if (d.rm >= 0) {
+        const u32 sl = selm<K>(m, d.rm);
+        hh -= sel64<K>(pm.hm, d.rm);
+        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
+        else nmsg -= 1;
+    }
+    if (d.has_add) {
+        int found = -1;
+#pragma unroll
+        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+        if (found >= 0) {
+            const u32 sl = selm<K>(m, found);
+            if ((int)m_cnt(sl) + 1 > P.max_dup) return 0;
+            hh += hM(sl + CNT_ONE) - sel64<K>(pm.hm, found);
+        } else {
+            if (1 > P.max_dup) return 0;
+            nmsg += 1;
+            hh += hM(d.add | CNT_ONE);
+        }
+    }
+    if (nmsg > P.max_msgs) return 0;
+    *h = hh;
+    return 1;
+}
+
 template <int S, int K>
 RMC_HD u64 state_fp(const u64 (&w)[S], const u32 (&m)[K]) {
     u64 h = 0;
@@ -591,6 +656,51 @@ RMC_HD int candidate_term_not_in_log(const u64 (&w)[S]) {
     }
     return 1;
 }
+// The IsPrefix invariants (raft.tla:1143-1180) as restated in
+// specs/MCraftBounded.tla: Committed(j) = the first min(commitIndex[j],
+// Len(log[j])) entries of log[j].  IsPrefix(Committed(j), log[i]) compares
+// packed entry bits.
+RMC_HD int committed_prefix_of(u64 wj, u64 wi) {
+    const u32 c = w_ci(wj) < w_len(wj) ? w_ci(wj) : w_len(wj);
+    if (w_len(wi) < c) return 0;
+    const u64 pm = (1ull << (ENT_W * c)) - 1;
+    return ((wi >> LOG_SH) & pm) == ((wj >> LOG_SH) & pm);
+}
+template <int S>
+RMC_HD int votes_granted_inv(const u64 (&w)[S]) {  // raft.tla:1145-1153
+    for (int i = 0; i < S; ++i)
+        for (int j = 0; j < S; ++j)
+            if (((w_vg<S>(w[i]) >> j) & 1u) && w_ct(w[i]) == w_ct(w[j]) && !committed_prefix_of(w[j], w[i]))
+                return 0;
+    return 1;
+}
+template <int S>
+RMC_HD int quorum_log_inv(const u64 (&w)[S]) {  // raft.tla:1157-1161
+    for (int i = 0; i < S; ++i) {
+        int miss = 0;  // servers lacking Committed(i): they must not contain a quorum
+        for (int j = 0; j < S; ++j) miss += committed_prefix_of(w[i], w[j]) ? 0 : 1;
+        if (2 * miss > S) return 0;
+    }
+    return 1;
+}
+template <int S>
+RMC_HD int more_up_to_date_correct(const u64 (&w)[S]) {  // raft.tla:1167-1172
+    for (int i = 0; i < S; ++i)
+        for (int j = 0; j < S; ++j) {
+            const u32 li = w_last_term(w[i]), lj = w_last_term(w[j]);
+            if ((li > lj || (li == lj && w_len(w[i]) >= w_len(w[j]))) && !committed_prefix_of(w[j], w[i])) return 0;
+        }
+    return 1;
+}
+template <int S>
+RMC_HD int leader_completeness(const u64 (&w)[S]) {  // raft.tla:1176-1180
+    for (int i = 0; i < S; ++i) {
+        if (w_st(w[i]) != LEADER) continue;
+        for (int j = 0; j < S; ++j)
+            if (!committed_prefix_of(w[j], w[i])) return 0;
+    }
+    return 1;
+}
 // The invariants other than TypeOK, out of line: inlined into every expansion
 // kernel's new-state paths they would grow the code by ~15 % for checks that
 // the bench model never names.  The state travels by value (in VGPRs).
@@ -611,6 +721,10 @@ RMC_HD_COLD int check_named_invariants(const PackedState<S, K> s, int mask) {
     if ((mask & 8) && !messages_inv<S, K>(s.w, s.m)) return 4;
     if ((mask & 16) && !leader_votes_quorum<S>(s.w)) return 5;
     if ((mask & 32) && !candidate_term_not_in_log<S>(s.w)) return 6;
+    if ((mask & 64) && !votes_granted_inv<S>(s.w)) return 7;
+    if ((mask & 128) && !quorum_log_inv<S>(s.w)) return 8;
+    if ((mask & 256) && !more_up_to_date_correct<S>(s.w)) return 9;
+    if ((mask & 512) && !leader_completeness<S>(s.w)) return 10;
     return 0;
 }
 // 0 = all hold, else 1 + index of the first violated invariant bit.

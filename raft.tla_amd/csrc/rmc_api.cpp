@@ -78,7 +78,7 @@ int validate(const rmc_config* c, std::string* why) {
     if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
     if ((c->flags & RMC_FLAG_SYMMETRY) && c->n_servers > 4)
         return bad("SYMMETRY is supported for up to 4 servers");
-    if (c->invariants & ~63u) return bad("unknown invariant bit");
+    if (c->invariants & ~1023u) return bad("unknown invariant bit");
     if ((c->flags & RMC_FLAG_VERIFY_STATES) && (c->flags & RMC_FLAG_SYMMETRY))
         return bad("full-state verification is not supported with SYMMETRY");
     return 0;
@@ -460,10 +460,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
     depth = c->h_ctr->count ? 1 : 0;
     if (c->h_ctr->viol != ~0ull) {
-        c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 7);
+        c->res.violated_inv = 1 << (int)(c->h_ctr->viol & 15);
         c->res.violation_depth = 1;
         c->have_target = 1;
-        c->target_idx = c->h_ctr->viol >> 3;
+        c->target_idx = c->h_ctr->viol >> 4;
     }
     }  // !resume
     const u64 CHUNK = 1ull << 26;
@@ -519,10 +519,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         }
         c->res.distinct = k.count;
         if (k.viol != ~0ull) {
-            c->res.violated_inv = 1 << (int)(k.viol & 7);
+            c->res.violated_inv = 1 << (int)(k.viol & 15);
             c->res.violation_depth = depth;
             c->have_target = 1;
-            c->target_idx = k.viol >> 3;
+            c->target_idx = k.viol >> 4;
         } else if ((c->cfg.flags & RMC_FLAG_CHECK_DEADLOCK) && k.deadlock != ~0ull) {
             c->res.deadlock = 1;
             c->have_target = 1;
@@ -908,8 +908,8 @@ int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_b
     out->truncated = h.truncated;
     out->deadlocked = h.deadlocked;
     if (h.viol != ~0ull) {
-        out->violated_inv = 1 << (int)((h.viol >> 40) & 7);
-        out->violation_depth = (int32_t)(h.viol >> 43);
+        out->violated_inv = 1 << (int)((h.viol >> 40) & 15);
+        out->violation_depth = (int32_t)(h.viol >> 44);
         out->violation_behaviour = h.viol & ((1ull << 40) - 1);
     }
     out->kernel_seconds = 1e-3 * ms;
@@ -922,6 +922,20 @@ int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_b
 extern "C" {
 
 int rmc_simulate(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out) { return run_sim(c, sc, out, -1, nullptr); }
+
+int rmc_smoke_init(const rmc_config* cfg, const rmc_sim_config* sc, rmc_state_view* states, size_t cap, size_t* n) {
+    if (!cfg || !sc || !n || sc->smoke_k < 1) return RMC_E_INVAL;
+    std::string why;
+    if (validate(cfg, &why)) return RMC_E_INVAL;
+    rmc_ctx host;  // codec only: no device, no allocation
+    host.cfg = *cfg;
+    fill_params(&host);
+    std::vector<u32> packed;
+    if (smoke_init(&host, *sc, &packed, &why)) return RMC_E_INVAL;
+    *n = packed.size() / (size_t)host.NW;
+    for (size_t q = 0; q < *n && q < cap && states; ++q) decode_state(&host, packed.data() + q * host.NW, &states[q]);
+    return 0;
+}
 
 int rmc_sim_replay(rmc_ctx* c, const rmc_sim_config* sc, uint64_t behaviour, rmc_state_view* states, size_t cap,
                    size_t* len) {
@@ -1069,8 +1083,8 @@ int rmc_dist_end_level(rmc_ctx* c, uint64_t* out) {
     out[0] = k.count - hi;
     out[1] = k.generated;
     out[2] = k.probes;
-    out[3] = k.viol != ~0ull ? (k.viol >> 3) + 1 : 0;
-    out[4] = k.viol != ~0ull ? (1ull << (k.viol & 7)) : 0;
+    out[3] = k.viol != ~0ull ? (k.viol >> 4) + 1 : 0;
+    out[4] = k.viol != ~0ull ? (1ull << (k.viol & 15)) : 0;
     c->res.generated += k.generated;
     c->res.probes += k.probes;
     c->res.distinct = k.count;  // states stored on this rank

@@ -11,7 +11,7 @@ namespace rmc {
 struct Counters {
     u64 count;      // next free index of the state store (= distinct so far)
     u64 generated;  // successors generated in this launch
-    u64 viol;       // min over violating new states of (index << 2 | invariant), ~0 = none
+    u64 viol;       // min over violating new states of (index << 4 | invariant), ~0 = none
     u64 deadlock;   // min index of a state with no enabled lane, ~0 = none
     u32 overflow;   // state store full
     u32 table_full; // fingerprint set full
@@ -71,7 +71,7 @@ hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& 
 typedef int64_t i64;
 struct SimCounters {
     u64 steps, truncated, deadlocked;
-    u64 viol;  // min over violations of (depth << 42 | invariant << 40 | behaviour), ~0 = none
+    u64 viol;  // min over violations of (depth << 44 | invariant << 40 | behaviour), ~0 = none
 };
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
                       int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);

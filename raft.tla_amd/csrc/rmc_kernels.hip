@@ -12,6 +12,7 @@
 //  k_list   : the same lane code with every enabled successor written out
 //             (no dedup) — the differential-test entry point (rmc_expand).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "raft_packed.h"
 #include "rmc_internal.h"
@@ -80,12 +81,14 @@ __device__ __forceinline__ void load_state(const u32* __restrict__ base, u64 (&w
     const u64* ws = reinterpret_cast<const u64*>(base);
 #pragma unroll
     for (int i = 0; i < S; ++i) w[i] = ws[i];
-    if constexpr (K % 4 == 0) {
-        const uint4* ms = reinterpret_cast<const uint4*>(base + 2 * S);
+    // Records are 8-byte aligned (2S + K words, K even), so the bag is read
+    // as 8-byte pairs: a 16-byte load would be misaligned for odd S.
+    if constexpr (K % 2 == 0) {
+        const uint2* ms = reinterpret_cast<const uint2*>(base + 2 * S);
 #pragma unroll
-        for (int q = 0; q < K / 4; ++q) {
-            const uint4 v = ms[q];
-            m[4 * q] = v.x; m[4 * q + 1] = v.y; m[4 * q + 2] = v.z; m[4 * q + 3] = v.w;
+        for (int q = 0; q < K / 2; ++q) {
+            const uint2 v = ms[q];
+            m[2 * q] = v.x; m[2 * q + 1] = v.y;
         }
     } else {
 #pragma unroll
@@ -180,7 +183,7 @@ __device__ __forceinline__ void commit_new(int is_new, const u64 (&w)[S], const 
     B.parent[ni] = parent_idx;
     B.act[ni] = (uint8_t)lane;
     const int v = check_invariants<S, K>(wo, mo, P);
-    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 3) | (u64)(v - 1)));
+    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
 }
 
 // Per-wave list of new states, kept in LDS until a flush materialises them.
@@ -226,7 +229,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
         const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 3) | (u64)(v - 1)));
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
     wave_sync_lds();
 }
@@ -423,7 +426,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
             B.parent[slot] = B.ref_tag | (lo + rel);
             B.act[slot] = (uint8_t)lane;
             const int v = check_invariants<S, K>(wo, mo, P);
-            if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 3) | (u64)(v - 1)));
+            if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
         } else {
             if (slot >= B.ocap) {
                 atomicOr(&B.ctr->overflow, 2u);
@@ -446,7 +449,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // DIST: sharded mode — successors owned by another rank are looked up in the
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
-template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false>
+template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr int NP = SYM ? NPerm<S>::v : 1;
@@ -484,7 +487,14 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
 #pragma unroll
             for (int q = 0; q < K; ++q) m[q] = 0;
         }
-        const u64 h0 = state_fp<S, K>(w, m);
+        ParentMix<S, K> pmx;
+        u64 h0;
+        if constexpr (PRE) {
+            parent_mix<S, K>(w, m, pmx);
+            h0 = pmx.h0;
+        } else {
+            h0 = state_fp<S, K>(w, m);
+        }
         u64 hp[NP];
         if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
         u32 g = 0;
@@ -499,7 +509,12 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     const int en = d.en && live;
                     g += (u32)en;
                     u64 h = 0;
-                    if (en && delta_fp<S, K>(w, m, h0, d, P, &h) && h != h0) {
+                    int in_model = 0;
+                    if (en) {
+                        if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h);
+                        else in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
+                    }
+                    if (in_model && h != h0) {
                         key = h;
                         if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
                         if constexpr (VERIFY) key &= P.fp_mask;
@@ -643,9 +658,16 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
 }
 
-template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false>
+template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false>
 __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    expand_body<S, K, SYM, BATCH, DIST, VERIFY>(P, PT, B, lo, hi);
+    expand_body<S, K, SYM, BATCH, DIST, VERIFY, PRE>(P, PT, B, lo, hi);
+}
+
+// Precomputed parent mixes at 6 waves/SIMD (91 VGPRs unconstrained = 5 waves).
+template <int S, int K, int BATCH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_expand_pre6(
+    const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    expand_body<S, K, false, BATCH, false, false, true>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion (canonicalisation over the S! server permutations): 205
@@ -699,7 +721,7 @@ __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, 
         B.parent[ni] = ref & ~(0xFFull << 40);
         B.act[ni] = (uint8_t)(ref >> 40);
         const int v = check_invariants<S, K>(w, m, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 3) | (u64)(v - 1)));
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
     wave_sync_lds();
 }
@@ -918,7 +940,7 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
         const bool record = (i64)t == rec_beh;
         if (record) store_state<S, K>(rec, w, m);
         int v = check_invariants<S, K>(w, m, P);
-        if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 43) | ((u64)(v - 1) << 40) | t));
+        if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 44) | ((u64)(v - 1) << 40) | t));
         for (int dd = 2; dd <= depth && !v; ++dd) {
             u32 cnt = 0;
             int pick = -1;
@@ -954,7 +976,7 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
             v = check_invariants<S, K>(w, m, P);
             if (v)
                 atomicMin((unsigned long long*)&out->viol,
-                          (unsigned long long)(((u64)dd << 43) | ((u64)(v - 1) << 40) | t));
+                          (unsigned long long)(((u64)dd << 44) | ((u64)(v - 1) << 40) | t));
         }
     }
     atomicAdd((unsigned long long*)&out->steps, (unsigned long long)steps);
@@ -991,6 +1013,16 @@ hipError_t set_fp_salt(u64 seed, hipStream_t st) {
 
 static const u64 kExpandGrid = 2048;
 
+// Expansion kernel variant for same-box A/B runs (RMC_EXPAND_VARIANT):
+// 0 = mixes recomputed per lane, 1 = the parent's mixes precomputed.
+static int expand_variant() {
+    static int v = [] {
+        const char* e = getenv("RMC_EXPAND_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 // Probes in flight per thread: 8 (measured best of 4/8 on MI355X).
 constexpr int kBatch = 8;
 
@@ -1010,6 +1042,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (verify) {
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
+        } else if (expand_variant() == 2) {
+            hipLaunchKernelGGL((k_expand_pre6<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        } else if (expand_variant() == 1) {
+            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3((unsigned)g), dim3(256), 0, st,
+                               P, PT, B, a, b);
         } else {
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
                                b);

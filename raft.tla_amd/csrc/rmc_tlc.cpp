@@ -104,8 +104,38 @@ const char* inv_name(int bit) {
         case RMC_INV_MESSAGES: return "MessagesInv";
         case RMC_INV_LEADER_VOTES: return "LeaderVotesQuorum";
         case RMC_INV_CAND_TERM: return "CandidateTermNotInLog";
+        case RMC_INV_VOTES_GRANTED: return "VotesGrantedInv";
+        case RMC_INV_QUORUM_LOG: return "QuorumLogInv";
+        case RMC_INV_MORE_UP_TO_DATE: return "MoreUpToDateCorrect";
+        case RMC_INV_LEADER_COMPLETE: return "LeaderCompleteness";
     }
     return "?";
+}
+
+// TLC's header of a behaviour step: the action of Next that produced the
+// state and its location in raft.tla (the body of the action's definition;
+// for Receive, the disjunct of raft.tla:393-403 that fired: UpdateTerm when
+// the message's term is newer, else the one for its mtype).
+std::string g_override_header;  // an override's action location (front-end notes), e.g. BugBecomeLeader
+
+std::string step_header(int family, int instance, const rmc_state_view& parent) {
+    if (family == 3 && !g_override_header.empty()) return g_override_header;
+    std::string action = kFamilies[family], shown = action;
+    if (family == 7) {
+        const int S = parent.n_servers;
+        const int q = instance - (6 * S + 2 * S * S);  // Receive lanes start after the server families
+        if (q >= 0 && q < parent.n_msgs) {
+            const rmc_msg_view& m = parent.msgs[q];
+            if (m.mterm > parent.currentTerm[m.mdest]) action = shown = "UpdateTerm";
+            else action = std::string("Receive:") + kMtypes[m.mtype];
+        }
+    }
+    int32_t loc[4];
+    if (rmc_action_location(action.c_str(), loc) != 0) return "<" + shown + ">";
+    char buf[256];
+    snprintf(buf, sizeof buf, "<%s line %d, col %d to line %d, col %d of module raft>", shown.c_str(), loc[0], loc[1],
+             loc[2], loc[3]);
+    return buf;
 }
 
 int progress(const rmc_level_stats* s, void*) {
@@ -119,7 +149,10 @@ int progress(const rmc_level_stats* s, void*) {
 int usage() {
     fprintf(stderr,
             "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N]\n"
-            "               [-verify] [-fpseed S] [-checkpoint F] [-recover F] [-simulate [num=N]] [-seed S] X.tla\n"
+            "               [-verify] [-fpseed S] [-checkpoint F] [-recover F] [-simulate [num=N]] [-seed S]\n"
+            "               [-raft raft.tla] [-builtin-raft] X.tla\n"
+            "  -raft F        the raft.tla to verify against the compiled-in spec (default: next to X.tla)\n"
+            "  -builtin-raft  no raft.tla on disk: check the compiled-in lemmy/raft.tla (said in the output)\n"
             "  -depth N   stop after N BFS levels (level N is left on the queue)\n"
             "  -verify    full-state verification: compare every fingerprint hit with the stored state\n"
             "  -fpseed S  fingerprint salt (TLC -fp: another member of the fingerprint family)\n"
@@ -132,13 +165,15 @@ int usage() {
 
 // TLC -simulate: random behaviours with the invariants checked on every state
 // (Smokeraft.cfg:43-48 through rmc_sim_config_from_files).
-int run_simulation(const std::string& cfg, const std::string& tla, int device, int depth, unsigned long long num,
-                   unsigned long long seed) {
+int run_simulation(const std::string& cfg, const std::string& tla, const std::string& raft, uint32_t fopts, int device,
+                   int depth, unsigned long long num, unsigned long long seed) {
     rmc_config c;
     rmc_sim_config sc;
-    char err[512];
-    int rc = rmc_sim_config_from_files(cfg.c_str(), tla.c_str(), &c, &sc, err, sizeof err);
-    if (rc) { printf("Error: %s\n", err); return 1; }
+    char info[2048];
+    int rc = rmc_model_from_files(cfg.c_str(), tla.c_str(), raft.empty() ? nullptr : raft.c_str(),
+                                  fopts | RMC_FRONT_SIMULATE, &c, &sc, info, sizeof info);
+    if (rc) { printf("Error: %s\n", info); return 1; }
+    if (info[0]) printf("%s\n", info);
     c.device = device;
     c.state_capacity = 1 << 12;  // no state store needed for walks
     if (depth > 0) sc.depth = depth;
@@ -187,7 +222,8 @@ int main(int argc, char** argv) {
     int depth = 0, device = 0, nodeadlock = 0, verify = 0;
     unsigned long long fpseed = 0, seed = 0, num = 0;
     int simulate = 0;
-    std::string ckpt, recover;
+    std::string ckpt, recover, raft;
+    uint32_t fopts = 0;
     unsigned long long capacity = 0;
     for (int a = 1; a < argc; ++a) {
         std::string s = argv[a];
@@ -199,6 +235,8 @@ int main(int argc, char** argv) {
         else if (s == "-capacity") { const char* v = next(); if (!v) return usage(); capacity = strtoull(v, nullptr, 10); }
         else if (s == "-workers") { if (!next()) return usage(); }  // accepted for compatibility
         else if (s == "-verify") verify = 1;
+        else if (s == "-raft") { const char* v = next(); if (!v) return usage(); raft = v; }
+        else if (s == "-builtin-raft") fopts |= RMC_FRONT_BUILTIN_RAFT;
         else if (s == "-checkpoint") { const char* v = next(); if (!v) return usage(); ckpt = v; }
         else if (s == "-recover") { const char* v = next(); if (!v) return usage(); recover = v; }
         else if (s == "-simulate") {
@@ -213,11 +251,17 @@ int main(int argc, char** argv) {
     if (tla.empty()) return usage();
     if (cfg.empty()) cfg = (tla.size() > 4 && tla.substr(tla.size() - 4) == ".tla" ? tla.substr(0, tla.size() - 4) : tla) + ".cfg";
     printf("rmc-tlc: %s\n", rmc_version());
-    if (simulate) return run_simulation(cfg, tla, device, depth, num, seed);
+    if (const char* b = getenv("RMC_BUILTIN_RAFT")) if (b[0] == '1') fopts |= RMC_FRONT_BUILTIN_RAFT;
+    if (simulate) return run_simulation(cfg, tla, raft, fopts, device, depth, num, seed);
     rmc_config c;
-    char err[512];
-    int rc = rmc_config_from_files(cfg.c_str(), tla.c_str(), &c, err, sizeof err);
-    if (rc) { printf("Error: %s\n", err); return 1; }
+    char info[2048];
+    int rc = rmc_model_from_files(cfg.c_str(), tla.c_str(), raft.empty() ? nullptr : raft.c_str(), fopts, &c, nullptr,
+                                  info, sizeof info);
+    if (rc) { printf("Error: %s\n", info); return 1; }
+    if (info[0]) printf("%s\n", info);
+    if (const char* a = strstr(info, "BecomeLeader <- "))
+        if (const char* b = strstr(a, "; action <"))
+            if (const char* e = strchr(b, '>')) g_override_header.assign(b + 9, e + 1);
     c.device = device;
     c.max_depth = depth;
     c.state_capacity = capacity;
@@ -253,8 +297,8 @@ int main(int argc, char** argv) {
         std::vector<int32_t> fam(len), inst(len);
         rmc_trace(ctx, st.data(), fam.data(), inst.data(), len, &len);
         for (size_t k = 0; k < len; ++k) {
-            if (fam[k] < 0) printf("State %zu: <Initial predicate>\n", k + 1);
-            else printf("State %zu: <%s lane %d of module raft>\n", k + 1, kFamilies[fam[k]], inst[k]);
+            if (fam[k] < 0 || k == 0) printf("State %zu: <Initial predicate>\n", k + 1);
+            else printf("State %zu: %s\n", k + 1, step_header(fam[k], inst[k], st[k - 1]).c_str());
             print_state(st[k]);
             printf("\n");
         }

@@ -20,9 +20,13 @@ MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8
 FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES = 1, 2, 4, 8
 INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING, INV_MESSAGES = 1, 2, 4, 8
 INV_LEADER_VOTES, INV_CAND_TERM = 16, 32
+INV_VOTES_GRANTED, INV_QUORUM_LOG, INV_MORE_UP_TO_DATE, INV_LEADER_COMPLETE = 64, 128, 256, 512
 INV_NAMES = {INV_TYPEOK: "TypeOK", INV_ONE_LEADER: "OneLeaderPerTerm",
              INV_LOG_MATCHING: "LogMatching", INV_MESSAGES: "MessagesInv",
-             INV_LEADER_VOTES: "LeaderVotesQuorum", INV_CAND_TERM: "CandidateTermNotInLog"}
+             INV_LEADER_VOTES: "LeaderVotesQuorum", INV_CAND_TERM: "CandidateTermNotInLog",
+             INV_VOTES_GRANTED: "VotesGrantedInv", INV_QUORUM_LOG: "QuorumLogInv",
+             INV_MORE_UP_TO_DATE: "MoreUpToDateCorrect", INV_LEADER_COMPLETE: "LeaderCompleteness"}
+FRONT_BUILTIN_RAFT, FRONT_SIMULATE = 1, 2
 FAMILIES = ("Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
             "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
             "DropMessage")
@@ -103,7 +107,8 @@ EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_ru
            "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
            "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level", "rmc_dist_state",
            "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits",
-           "rmc_sim_config_from_files", "rmc_checkpoint", "rmc_recover")
+           "rmc_sim_config_from_files", "rmc_checkpoint", "rmc_recover", "rmc_model_from_files",
+           "rmc_action_location", "rmc_smoke_init")
 
 _lib = None
 
@@ -141,6 +146,15 @@ def native():
         lib.rmc_sim_config_from_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Config),
                                                   C.POINTER(SimConfig), C.c_char_p, C.c_size_t]
         lib.rmc_sim_config_from_files.restype = C.c_int
+        lib.rmc_model_from_files.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32,
+                                             C.POINTER(Config), C.POINTER(SimConfig), C.c_char_p,
+                                             C.c_size_t]
+        lib.rmc_model_from_files.restype = C.c_int
+        lib.rmc_action_location.argtypes = [C.c_char_p, C.POINTER(C.c_int32)]
+        lib.rmc_action_location.restype = C.c_int
+        lib.rmc_smoke_init.argtypes = [C.POINTER(Config), C.POINTER(SimConfig), C.POINTER(StateView),
+                                       C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.rmc_smoke_init.restype = C.c_int
         lib.rmc_checkpoint.argtypes = [C.c_void_p, C.c_char_p]
         lib.rmc_checkpoint.restype = C.c_int
         lib.rmc_recover.argtypes = [C.c_void_p, C.c_char_p]
@@ -192,27 +206,53 @@ def make_config(n_servers=3, n_values=2, max_term=2, max_log_len=1, max_msgs=2, 
                   invariants, device, max_depth, state_capacity, 0)
 
 
-def config_from_files(cfg_path, tla_path=None):
-    lib = native()
-    cfg = Config()
-    err = C.create_string_buffer(512)
-    rc = lib.rmc_config_from_files(cfg_path.encode(), tla_path.encode() if tla_path else None,
-                                   C.byref(cfg), err, 512)
-    if rc:
-        raise RmcError(rc, err.value.decode())
-    return cfg
-
-
-def sim_config_from_files(cfg_path, tla_path=None):
-    """(Config, SimConfig) of a simulation model (Smokeraft.cfg: Init <- SmokeInit)."""
+def model_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False, simulate=False):
+    """rmc_model_from_files: (Config, SimConfig or None, provenance notes).
+    Raises RmcError naming the construct when the model is not the compiled-in
+    raft.tla (with its recognised bug variant, bounds and invariants)."""
     lib = native()
     cfg, sc = Config(), SimConfig()
-    err = C.create_string_buffer(512)
-    rc = lib.rmc_sim_config_from_files(cfg_path.encode(), tla_path.encode() if tla_path else None,
-                                       C.byref(cfg), C.byref(sc), err, 512)
+    info = C.create_string_buffer(4096)
+    opts = (FRONT_BUILTIN_RAFT if builtin_raft else 0) | (FRONT_SIMULATE if simulate else 0)
+    rc = lib.rmc_model_from_files(cfg_path.encode(), tla_path.encode() if tla_path else None,
+                                  raft_path.encode() if raft_path else None, opts, C.byref(cfg),
+                                  C.byref(sc) if simulate else None, info, 4096)
     if rc:
-        raise RmcError(rc, err.value.decode())
+        raise RmcError(rc, info.value.decode())
+    return cfg, (sc if simulate else None), info.value.decode()
+
+
+def config_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False):
+    return model_from_files(cfg_path, tla_path, raft_path, builtin_raft)[0]
+
+
+def sim_config_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False):
+    """(Config, SimConfig) of a simulation model (Smokeraft.cfg: Init <- SmokeInit)."""
+    cfg, sc, _ = model_from_files(cfg_path, tla_path, raft_path, builtin_raft, simulate=True)
     return cfg, sc
+
+
+def smoke_init(cfg, smoke_k, smoke_nat=2, seed=0):
+    """The SmokeInit initial states rmc_simulate would draw (host only)."""
+    sc = SimConfig(1, 100, smoke_k, smoke_nat, 0, seed)
+    n = C.c_size_t()
+    rc = native().rmc_smoke_init(C.byref(cfg), C.byref(sc), None, 0, C.byref(n))
+    if rc:
+        raise RmcError(rc, "rmc_smoke_init failed")
+    st = (StateView * n.value)()
+    rc = native().rmc_smoke_init(C.byref(cfg), C.byref(sc), st, n.value, C.byref(n))
+    if rc:
+        raise RmcError(rc, "rmc_smoke_init failed")
+    return list(st)
+
+
+def action_location(action):
+    """(line, col, line, col) of an action of Next in raft.tla (TLC's trace headers)."""
+    out = (C.c_int32 * 4)()
+    rc = native().rmc_action_location(action.encode(), out)
+    if rc:
+        raise RmcError(rc, f"no action {action!r}")
+    return tuple(out)
 
 
 def probe_bench(device=0, table_bytes=64 << 30, accesses=1 << 31, mode=0):

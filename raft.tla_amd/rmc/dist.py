@@ -203,7 +203,7 @@ def run(ck: Checker, chunk_states=1 << 22, cap_per_dest=1 << 22, sent_cache_slot
 
     def expand(ob):
         """Expand this rank's next chunk into outbox `ob`; returns the send counts."""
-        nonlocal consumed, cur_chunk
+        nonlocal consumed, cur_chunk, cap_bound
         t1 = time.perf_counter()
         n_exp = min(cur_chunk, local_frontier - consumed)
         chk(lib.rmc_dist_expand(ctx, cur_chunk, C.c_void_p(outboxes[ob].data_ptr()), cap_per_dest,

@@ -140,6 +140,51 @@ def random_state(model, rng: random.Random):
     )
 
 
+def random_state_edge(model, rng: random.Random):
+    """random_state pushed to the packed capacity's edges:
+    terms at MaxTerm and just below (a Timeout or UpdateTerm there leaves the
+    CONSTRAINT, term 15 = MaxTerm + 1 at MaxTerm 14 is the last packable one),
+    full 3-entry logs (ClientRequest / NoConflict beyond them), counts at MaxDup
+    (Duplicate beyond it), a full bag of MaxMsgs messages, mprevLogIndex = -1."""
+    S, V = model.n_servers, model.n_values
+    T, L = model.max_term, model.max_log
+    term = lambda: rng.choice([0, max(0, T - 1), T, T])
+    ent = lambda: R.entry(term(), rng.randrange(V))
+    lg = lambda: tuple(ent() for _ in range(rng.choice([0, L, L, L])))
+
+    def rnd_msg():
+        t = rng.choice([R.RVQ, R.RVP, R.AEQ, R.AEP])
+        c = dict(mtype=t, mterm=term(), msource=rng.randrange(S), mdest=rng.randrange(S))
+        if t == R.RVQ:
+            return R.rec(mlastLogTerm=term(), mlastLogIndex=rng.choice([0, L]), **c)
+        if t == R.RVP:
+            return R.rec(mvoteGranted=rng.random() < 0.5, mlog=lg(), **c)
+        if t == R.AEQ:
+            return R.rec(mprevLogIndex=rng.choice([-1, -1, 0, L - 1, L]), mprevLogTerm=term(),
+                         mentries=tuple(ent() for _ in range(rng.randint(0, 1))),
+                         mcommitIndex=rng.choice([0, L]), **c)
+        return R.rec(msuccess=rng.random() < 0.5, mmatchIndex=rng.choice([0, L]), **c)
+
+    msgs = {}
+    target = rng.choice([model.max_msgs, model.max_msgs, rng.randint(0, model.max_msgs)])
+    for _ in range(64):
+        if len(msgs) >= target:
+            break
+        msgs[rnd_msg()] = rng.choice([1, model.max_dup, model.max_dup])
+    return R.State(
+        messages=frozenset(msgs.items()),
+        currentTerm=tuple(term() for _ in range(S)),
+        state=tuple(rng.choice([R.FOLLOWER, R.CANDIDATE, R.LEADER]) for _ in range(S)),
+        votedFor=tuple(rng.choice([R.NIL] + list(range(S))) for _ in range(S)),
+        log=tuple(lg() for _ in range(S)),
+        commitIndex=tuple(rng.choice([0, L]) for _ in range(S)),
+        votesResponded=tuple(frozenset(k for k in range(S) if rng.random() < 0.5) for _ in range(S)),
+        votesGranted=tuple(frozenset(k for k in range(S) if rng.random() < 0.5) for _ in range(S)),
+        nextIndex=tuple(tuple(rng.choice([1, L, L + 1]) for _ in range(S)) for _ in range(S)),
+        matchIndex=tuple(tuple(rng.choice([0, L]) for _ in range(S)) for _ in range(S)),
+    )
+
+
 def check_trace(model, trace, violated_inv, violation_depth):
     """A counterexample [(family, lane, StateView)] must be a behaviour of the
     spec (Python restatement) from Init to a state violating `violated_inv`,
@@ -152,8 +197,6 @@ def check_trace(model, trace, violated_inv, violation_depth):
         succ = {(f, t) for f, _p, t in R.successors(model, a)}
         assert (rmc.FAMILIES[fam], b) in succ
         assert R.in_constraint(model, b)
-    inv = {rmc.INV_ONE_LEADER: R.one_leader_per_term, rmc.INV_LOG_MATCHING: R.log_matching,
-           rmc.INV_MESSAGES: R.messages_inv, rmc.INV_LEADER_VOTES: R.leader_votes_quorum,
-           rmc.INV_CAND_TERM: R.candidate_term_not_in_log}
-    assert not inv[violated_inv](model, states[-1])
-    assert all(inv[violated_inv](model, s) for s in states[:-1])
+    check = R.INVARIANTS[R.INV_BITS[violated_inv]]
+    assert not check(model, states[-1])
+    assert all(check(model, s) for s in states[:-1])

@@ -49,7 +49,7 @@ def main():
                               max_depth=p["max_depth"],
                               state_capacity=args.capacity or max(1 << 20, g["distinct"]))
     else:
-        cfg = rmc.config_from_files(args.cfg)
+        cfg = rmc.config_from_files(args.cfg, builtin_raft=True)
         cfg.device = dev
         cfg.state_capacity = args.capacity or (1 << 26)
     with rmc.Checker(cfg) as ck:

@@ -43,19 +43,32 @@ CONFIGS = {
     "elections_small": (3, 2, 2, 1, 1, 1, 0, 49, 0, 0),
     "bug_leader_votes": (3, 2, 2, 1, 1, 1, 1, 16, 0, 0),
     "bug_cand_term": (3, 2, 2, 1, 1, 1, 1, 32, 0, 0),
+    # The IsPrefix invariants (raft.tla:1143-1180, restated in specs/MCraftBounded.tla
+    # with Committed(i) clamped to Len(log[i])): VotesGrantedInv (64) fails on the
+    # unmodified spec; QuorumLogInv (128), MoreUpToDateCorrect (256) and
+    # LeaderCompleteness (512) hold, also with 2-entry logs; the bug variant breaks all.
+    "votes_granted_small": (3, 2, 2, 1, 1, 1, 0, 64, 0, 0),
+    "isprefix_small": (3, 2, 2, 1, 1, 1, 0, 897, 0, 0),
+    "isprefix_s3v1_log2": (3, 1, 2, 2, 1, 1, 0, 897, 0, 0),
+    "bug_votes_granted": (3, 2, 2, 1, 1, 1, 1, 64, 0, 0),
+    "bug_quorum_log": (3, 2, 2, 1, 1, 1, 1, 128, 0, 0),
+    "bug_more_up_to_date": (3, 2, 2, 1, 1, 1, 1, 256, 0, 0),
+    "bug_leader_complete": (3, 2, 2, 1, 1, 1, 1, 512, 0, 0),
+    # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
+    "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }
 
 
 def main(only=None):
-    """`only`: names to (re)generate, merged into the existing file (entries
-    such as bounded_full, 78 M states, are kept as they are)."""
+    """`only`: names to (re)generate, merged into the existing file; without
+    names every entry is regenerated (bounded_full included)."""
     path = os.path.join(ROOT, "tests", "golden", "oracle_levels.json")
     out = json.load(open(path)) if only else {}
     for name, (S, V, mt, ml, mm, md, bug, inv, sym, lv) in CONFIGS.items():
         if only and name not in only:
             continue
         r, ln, lg = oracle_c.bfs(S, V, mt, ml, mm, md, bug=bug, inv=inv, sym=sym, threads=8,
-                                 max_levels=lv, capacity=1 << 25)
+                                 max_levels=lv, capacity=1 << 27)
         out[name] = dict(params=dict(n_servers=S, n_values=V, max_term=mt, max_log_len=ml,
                                      max_msgs=mm, max_dup=md, bug_quorum=bug, invariants=inv,
                                      symmetry=sym, max_depth=lv),

@@ -12,7 +12,7 @@ import pytest
 
 import rmc
 from oracle import raft_spec as R
-from tests.convert import check_trace, from_view, random_state, to_view
+from tests.convert import check_trace, from_view, random_state, random_state_edge, to_view
 
 pytestmark = pytest.mark.gpu
 
@@ -50,7 +50,8 @@ def test_kat_first_levels():
 
 
 BFS_CASES = ["bounded_full", "tiny2", "messages_tiny2", "elections_small", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
-             "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9"]
+             "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9", "isprefix_small",
+             "isprefix_s3v1_log2"]
 
 
 @pytest.mark.parametrize("name", BFS_CASES)
@@ -111,7 +112,9 @@ def test_full_state_verification_reports_collisions(bits):
 
 
 @pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both", "bug_messages",
-                                  "messages_small", "bug_leader_votes", "bug_cand_term"])
+                                  "messages_small", "bug_leader_votes", "bug_cand_term", "votes_granted_small",
+                                  "bug_votes_granted", "bug_quorum_log", "bug_more_up_to_date",
+                                  "bug_leader_complete"])
 def test_bug_variant_violation_and_trace(name):
     g = GOLDEN[name]
     p = g["params"]
@@ -142,7 +145,28 @@ def test_expand_matches_oracle_on_fuzzed_states(k):
     every lane of random type-correct states, GPU vs the Python restatement."""
     m = R.Model(**FUZZ[k])
     rng = random.Random(1000 + k)
-    states = [random_state(m, rng) for _ in range(600)]
+    compare_expand(m, [random_state(m, rng) for _ in range(600)])
+
+
+FUZZ_EDGE = [
+    dict(n_servers=3, n_values=2, max_term=14, max_log=3, max_msgs=8, max_dup=3),
+    dict(n_servers=5, n_values=2, max_term=14, max_log=3, max_msgs=8, max_dup=3),
+    dict(n_servers=2, n_values=1, max_term=14, max_log=3, max_msgs=4, max_dup=3, bug_quorum=True),
+    dict(n_servers=4, n_values=2, max_term=13, max_log=2, max_msgs=8, max_dup=2),
+]
+
+
+@pytest.mark.parametrize("k", range(len(FUZZ_EDGE)))
+def test_expand_matches_oracle_at_capacity_edges(k):
+    """The same differential test at the packed capacity's edges (terms 13-15,
+    3-entry logs, counts at MaxDup, a full 8-slot bag, mprevLogIndex = -1):
+    successors beyond a field's width must leave the CONSTRAINT, never wrap."""
+    m = R.Model(**FUZZ_EDGE[k])
+    rng = random.Random(2000 + k)
+    compare_expand(m, [random_state_edge(m, rng) for _ in range(800)])
+
+
+def compare_expand(m, states):
     cfg = rmc.make_config(n_servers=m.n_servers, n_values=m.n_values, max_term=m.max_term,
                           max_log_len=m.max_log, max_msgs=m.max_msgs, max_dup=m.max_dup,
                           bug_quorum=m.bug_quorum, state_capacity=1 << 12)
@@ -178,7 +202,7 @@ def test_cli_bfs_summary_with_verification():
     """rmc-tlc prints TLC's summary lines; -verify adds the collision count."""
     import subprocess
     g = GOLDEN["tiny2"]
-    r = subprocess.run([CLI, "-verify", "-config", os.path.join(SPECS, "MCraftTiny2.cfg"),
+    r = subprocess.run([CLI, "-builtin-raft", "-verify", "-config", os.path.join(SPECS, "MCraftTiny2.cfg"),
                         os.path.join(SPECS, "MCraftTiny2.tla")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert f"{g['generated']} states generated, {g['distinct']} distinct states found, 0 states left on queue." \
@@ -191,7 +215,7 @@ def test_cli_simulation_mode():
     """rmc-tlc -simulate on a SmokeInit model (k = 3: 3^9 initial states, as
     Smokeraft.tla:17-19 lists); TypeOK holds on every state."""
     import subprocess
-    r = subprocess.run([CLI, "-simulate", "num=65536", "-seed", "3", os.path.join(MODELS, "SmokeFixture.tla")],
+    r = subprocess.run([CLI, "-builtin-raft", "-simulate", "num=65536", "-seed", "3", os.path.join(MODELS, "SmokeFixture.tla")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "SmokeInit: 19683 initial states (k = 3)." in r.stdout
@@ -246,3 +270,53 @@ def test_recover_rejects_another_model(tmp_path):
             ck.recover(str(tmp_path / "ck"))
         with pytest.raises(rmc.RmcError, match="not an rmc checkpoint|cannot open"):
             ck.recover(str(tmp_path / "missing"))
+
+
+FRONT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "front_models.json")))
+
+
+@pytest.mark.parametrize("model,golden", [("MCraftBug_raft_tla_edited", "bug_both"), ("MCraftTiny2", "tiny2")])
+def test_front_end_configs_from_raft_tla_run_to_the_oracle_result(model, golden):
+    """Config 5 through the raft.tla file path: the rmc_config the front-end made
+    from a raft.tla with line 197 weakened (tests/golden/make_front_fixtures.py,
+    CPU side, where raft.tla exists) runs to the oracle's violation, depth and
+    counts; likewise an unmodified model verified against raft.tla."""
+    f = FRONT[model]
+    g = GOLDEN[golden]
+    cfg = rmc.make_config(n_servers=f["n_servers"], n_values=f["n_values"], max_term=f["max_term"],
+                          max_log_len=f["max_log_len"], max_msgs=f["max_msgs"], max_dup=f["max_dup"],
+                          state_capacity=1 << 25)
+    cfg.flags, cfg.invariants = f["flags"], f["invariants"]
+    p = g["params"]
+    assert (cfg.n_servers, cfg.max_term, cfg.max_msgs, bool(cfg.flags & rmc.FLAG_BUG_QUORUM), cfg.invariants) == \
+        (p["n_servers"], p["max_term"], p["max_msgs"], bool(p["bug_quorum"]), p["invariants"])
+    res, levels, _trace = run(cfg)
+    assert (res.distinct, res.generated, res.violated_inv, res.violation_depth) == \
+        (g["distinct"], g["generated"], g["violated_inv"], g["violation_depth"])
+
+
+@pytest.mark.parametrize("cfgname,golden", [("MCraftBug", "bug_both"), ("MCraftMessages", "messages_small")])
+def test_cli_counterexample_is_tlc_format_and_replays(cfgname, golden, tmp_path):
+    """rmc-tlc's counterexample (config 5 and the MessagesInv model): TLC's
+    summary and `State k: <Action line L1, col C1 to line L2, col C2 of module
+    M>` headers; tests/tla_transcript.py reads the TLA+ values back and the
+    Python restatement re-validates every step, its header (the action and
+    its raft.tla or override location) and the violation.  The transcript is
+    kept in tmp for the committed-golden check (tests/golden/cli_*.txt)."""
+    import subprocess
+    from tests import tla_transcript
+    g = GOLDEN[golden]
+    p = g["params"]
+    r = subprocess.run([CLI, "-builtin-raft", "-config", os.path.join(SPECS, cfgname + ".cfg"),
+                        os.path.join(SPECS, cfgname + ".tla")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 12, r.stdout[-2000:] + r.stderr
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
+                    bug_quorum=bool(p["bug_quorum"]))
+    inv, n = tla_transcript.validate(r.stdout, model)
+    assert rmc.INV_NAMES[g["violated_inv"]] == inv and n == g["violation_depth"]
+    assert f"{g['generated']} states generated, {g['distinct']} distinct states found, 0 states left on queue." \
+        in r.stdout
+    out = os.path.join(os.path.dirname(os.path.dirname(__file__)), "gpurun_out")
+    if os.path.isdir(out):
+        open(os.path.join(out, f"cli_{cfgname}.txt"), "w").write(r.stdout)

@@ -2,5 +2,5 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-bash tools_prof.sh || exit 1
+bash tools/gpu/prof.sh || exit 1
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || exit 1

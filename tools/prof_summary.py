@@ -1,4 +1,4 @@
-"""Summarise the rocprofv3 databases of tools_prof.sh into profiles/<round>/:
+"""Summarise the rocprofv3 databases of tools/gpu/prof.sh into profiles/<round>/:
 
   kernel_stats_<cfg>.csv     per-kernel calls / total / average (kernel-trace pass)
   pmc_traffic_<cfg>.json     HBM bytes per k_expand launch (FETCH_SIZE and
@@ -44,7 +44,7 @@ def main():
     write = counter(one_db(os.path.join(src, "write")), "WRITE_SIZE")
     n = len(fetch)
     rec = {
-        "command": "tools_prof.sh: rocprofv3 --kernel-trace --stats | --pmc FETCH_SIZE | --pmc WRITE_SIZE "
+        "command": "tools/gpu/prof.sh: rocprofv3 --kernel-trace --stats | --pmc FETCH_SIZE | --pmc WRITE_SIZE "
                    "(separate passes) -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-probe-ceiling",
         "workload": f"specs/{stem}.cfg, BFS to fixpoint (bench step + the untimed fingerprint-salt re-run)",
         "kernel": name,
