@@ -4,9 +4,10 @@
 A "step" is one complete breadth-first search of the bounded MCraft model to
 its fixpoint (time-to-fixpoint); `value` = distinct states / seconds per step,
 whole job.  The workload is deterministic: an exhaustive BFS has no input data.
-With N > 1 ranks the fingerprint space is sharded over the GPUs (rmc.dist:
-owner-routed successors, RCCL all-to-all per frontier chunk) and the SAME
-model is searched, so scaling is strong.
+With N > 1 ranks the state space is sharded over the GPUs inside librmc
+(rmc_shard: owner-routed successors, fingerprint-first two-phase exchange
+over librmc's own RCCL communicator) and the SAME model is searched, so
+scaling is strong.
 """
 import argparse
 import json
@@ -34,10 +35,11 @@ def parse():
                     help="state capacity per GPU (0 = 1.5e9 / world * 1.3 for the bench model)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK (one GPU per rank)")
-    ap.add_argument("--chunk", type=int, default=1 << 24, help="frontier states per exchange")
-    ap.add_argument("--cap-per-dest", type=int, default=1 << 25, help="outbox records per destination rank")
+    ap.add_argument("--keys-per-dest", type=int, default=1 << 25,
+                    help="sharded mode: phase-1 keys one chunk may send one owner")
     ap.add_argument("--sent-cache", type=int, default=1 << 30,
                     help="sharded mode: slots of the per-rank cache of fingerprints already sent")
+    ap.add_argument("--transport", default="auto", help="sharded mode: rccl | host | auto")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the sharded path even at one rank (measures its overhead)")
     ap.add_argument("--no-probe-ceiling", action="store_true",
@@ -115,20 +117,19 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    last_dist = [None]
+    last = [None]
 
     def one_run(ck, first):
-        if not sharded:
-            r = ck.run()
-            return r.distinct, r.generated, r.depth, r.probes, r.expand_kernel_seconds, r.expand_launches
-        from rmc import dist as rdist
-        r = rdist.run(ck, chunk_states=a.chunk, cap_per_dest=a.cap_per_dest, sent_cache_slots=a.sent_cache,
-                      init=first)
-        cr = ck.result()  # rmc_dist_start resets the per-run counters
-        last_dist[0] = r
-        return (r.distinct, r.generated, r.depth, r.probes, cr.expand_kernel_seconds, cr.expand_launches)
+        # sharded: rmc_run_bfs is a collective inside librmc (two-phase
+        # exchange over its own RCCL communicator); the result is global
+        r = ck.run()
+        last[0] = r
+        return r.distinct, r.generated, r.depth, r.probes, r.expand_kernel_seconds, r.expand_launches
 
     with rmc.Checker(cfg) as ck:
+        if sharded:
+            from rmc import dist as rdist
+            rdist.shard(ck, transport=a.transport, keys_per_dest=a.keys_per_dest, sent_cache_slots=a.sent_cache)
         first = True
         for _ in range(a.warmup):
             one_run(ck, first)
@@ -188,7 +189,7 @@ def main():
                         f"{cfg.max_log_len} MaxMsgs={cfg.max_msgs} MaxDup={cfg.max_dup}, BFS to fixpoint",
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
-            "parallelism": f"fingerprint-sharded x{world} (RCCL all-to-all)" if sharded else "single GPU",
+            "parallelism": f"state-space sharded x{world} (librmc two-phase exchange, RCCL)" if sharded else "single GPU",
             "fp_salt_crosscheck": salt_check,
         },
         "roofline": {
@@ -203,11 +204,11 @@ def main():
         },
     }
     if sharded:
-        ld = last_dist[0]
-        out["sharded"] = {"chunks_per_step": ld.chunks, "records_sent_rank0": ld.records_sent,
-                          "max_records_per_dest_per_state": round(ld.max_dest_per_state, 4),
-                          "phase_s_rank0": {k: round(v, 6) for k, v in ld.phase.items()},
-                          "chunk_states": a.chunk, "cap_per_dest": a.cap_per_dest}
+        ld = last[0]
+        out["sharded"] = {"in_library": "rmc_shard + rmc_run_bfs (two-phase fingerprint-first exchange)",
+                          "transport": a.transport, "chunks_rank0": ld.chunks, "keys_sent_rank0": ld.keys_sent,
+                          "states_sent_rank0": ld.states_sent, "stored_rank0": ld.stored_here,
+                          "exchange_s_rank0": round(ld.exchange_seconds, 6), "keys_per_dest": a.keys_per_dest}
         out["roofline"]["note"] = "per-rank kernel time of rank 0; achieved is rank 0's share"
         out["roofline"]["achieved"] = (b_alg / world) / ks / 1e9 if ks > 0 else 0.0
         out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS

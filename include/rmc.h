@@ -110,6 +110,12 @@ typedef struct rmc_result {
     uint64_t collisions;       /* RMC_FLAG_VERIFY_STATES: fingerprint hits whose stored state */
                                /* differs (0 = the counts are exact, not probabilistic)   */
     uint64_t verified;         /* RMC_FLAG_VERIFY_STATES: hits compared state by state    */
+    /* sharded mode (rmc_shard): this rank's exchange */
+    uint64_t keys_sent;        /* phase-1 keys sent to other owners                        */
+    uint64_t states_sent;      /* phase-2 accepted states shipped                          */
+    uint64_t chunks;           /* frontier chunks (exchange rounds)                        */
+    double exchange_seconds;   /* wall time in collectives and count read-backs            */
+    uint64_t stored_here;      /* distinct states this rank stores                         */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */
@@ -229,12 +235,13 @@ int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_vi
  * (Smokeraft.tla:64-76: one RandomSubset(k, .) per variable, k^9 states, over
  * SmokeNat = 0..smoke_nat, SmokeInt = -1..1, BoundedSeq(.,3)/(.,1) logs);
  * smoke_k = 0 starts from Init.  TLC's StopAfter (a 1-s budget,
- * Smokeraft.tla:88-92) is replaced by an explicit behaviour count.  The packed
- * state holds terms <= 15, logs <= 3 entries, <= K distinct messages, counts <= 3:
- * RMC_SIM_WITHIN_CAPACITY draws each step uniformly among the enabled
- * successors that fit (the capacity acts as a state constraint, so behaviours
- * run to `depth`); RMC_SIM_TRUNCATE draws among all enabled successors and a
- * draw beyond the capacity ends that behaviour (counted in `truncated`). */
+ * Smokeraft.tla:88-92) is replaced by an explicit behaviour count.  Walks stay
+ * within the config's bounds (max_term, max_log_len, max_msgs, max_dup: the
+ * model's CONSTRAINT, or the packed capacity when it has none — the front-end
+ * fills them in): RMC_SIM_WITHIN_CAPACITY draws each step uniformly among the
+ * enabled successors within them (so behaviours run to `depth`);
+ * RMC_SIM_TRUNCATE draws among all enabled successors and a draw beyond them
+ * ends that behaviour (counted in `truncated`). */
 #define RMC_SIM_WITHIN_CAPACITY 0
 #define RMC_SIM_TRUNCATE 1
 typedef struct rmc_sim_config {
@@ -262,36 +269,41 @@ int rmc_smoke_init(const rmc_config* cfg, const rmc_sim_config* sc, rmc_state_vi
 int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, rmc_state_view* states,
                    size_t cap, size_t* len);
 
-/* ---- sharded BFS over several GPUs (one process per GPU) --------------------
+/* ---- sharded BFS over several GPUs (one process or thread per GPU) ---------
  * Replaces TLC's distributed mode (TLCServer/TLCWorker with a partitioned
- * FPSet).  A state is owned by the rank given by a hash
- * of its servers 0 and 1 words (RMC_OWNER=2, default; 1: server 0's word only;
- * 0: by fingerprint, ((fp >> 32) * world) >> 32); each rank stores and expands
- * the states it owns.
- * Per level, every rank runs:
- *   loop { rmc_dist_expand(chunk) -> per-destination record counts;
- *          host all-to-all of counts and records (torch.distributed / RCCL);
- *          rmc_dist_insert(received records) } until every rank's frontier is done;
- *   rmc_dist_end_level -> local stats; host all-reduce; stop when no rank has new states.
- * A record is rmc_dist_record_words() u32: the packed successor and its
- * global parent ref (rank << 48 | lane << 40 | index); the owner recomputes
- * the fingerprint from the state.
- * The outbox is caller-owned device memory: [world][cap_per_dest][record]. */
-int rmc_dist_init(rmc_ctx* ctx, int32_t rank, int32_t world, uint64_t sent_cache_slots);
-size_t rmc_dist_record_words(const rmc_ctx* ctx);
-int rmc_dist_start(rmc_ctx* ctx);
-int rmc_dist_expand(rmc_ctx* ctx, uint64_t max_states, uint32_t* outbox, uint64_t cap_per_dest,
-                    uint64_t* send_counts, int32_t* frontier_done);
-int rmc_dist_insert(rmc_ctx* ctx, const uint32_t* inbox, uint64_t n_records);
-int rmc_dist_end_level(rmc_ctx* ctx, uint64_t* out5);
-/* Trace reconstruction across ranks (TLC's distributed mode rebuilds the
- * counterexample from the workers' parent fingerprints): the state this rank
- * stores at `index`, the action family and lane of the step into it (-1 for an
- * initial state) and its parent's global reference (rank << 48 | index on that
- * rank; ~0 for an initial state).  out5[3] of rmc_dist_end_level is 1 + the
- * index of a violating state.  The host walks the chain rank by rank. */
-int rmc_dist_state(rmc_ctx* ctx, uint64_t index, rmc_state_view* state, int32_t* family,
-                   int32_t* instance, uint64_t* parent_ref);
+ * FPSet).  rmc_shard turns a ctx into rank `rank`
+ * of `world`; rmc_run_bfs, rmc_get_result and rmc_trace then become
+ * collectives that every rank calls, and return the GLOBAL result on every
+ * rank.  A state is owned by the rank given by a hash of its servers 0 and 1
+ * words (RMC_OWNER=2, default; 1: server 0 only; 0: by fingerprint, always
+ * under SYMMETRY); each rank stores and expands the states it owns.
+ * Per frontier chunk the exchange is fingerprint-first (two phases):
+ *   1. a successor owned elsewhere (and not in this rank's lossy sent-cache)
+ *      sends only its 8-byte key; the owner inserts the keys it receives
+ *      into its fingerprint set and answers new / seen (1 byte per key);
+ *   2. for the keys answered "new" the sender re-derives the successor and
+ *      ships the state and its global parent ref ((rank << 48) | index, lane
+ *      in bits 40-47); the owner stores it for the next level.
+ * Counts stay on the device until one read-back per phase; one all-gather
+ * per level combines the level statistics.
+ * Transport: RCCL over xGMI (rccl_id = an id from rmc_rccl_unique_id on rank
+ * 0, given to every rank; host = NULL), or a caller-supplied host transport
+ * (rccl_id = NULL) whose callbacks move host buffers: alltoallv sends
+ * send_bytes[d] bytes to rank d (blocks back to back in `send`) and receives
+ * recv_bytes[s] from rank s (back to back in `recv`); allgather gathers
+ * `bytes` from every rank into recv (rank order).  They return 0 on success.
+ * keys_per_dest bounds the keys one chunk sends to one owner (0 = auto);
+ * sent_cache_slots sizes the sent-cache (0 = auto).  Checkpoints and
+ * full-state verification are single-GPU only. */
+typedef struct rmc_transport {
+    void* user;
+    int (*alltoallv)(void* user, const void* send, const uint64_t* send_bytes, void* recv,
+                     const uint64_t* recv_bytes);
+    int (*allgather)(void* user, const void* send, uint64_t bytes, void* recv);
+} rmc_transport;
+int rmc_rccl_unique_id(uint8_t id[128]);
+int rmc_shard(rmc_ctx* ctx, int32_t rank, int32_t world, const uint8_t* rccl_id,
+              const rmc_transport* host, uint64_t keys_per_dest, uint64_t sent_cache_slots);
 
 /* ---- roofline microbenchmark -----------------------------------------------
  * Random 8-byte accesses into a table of table_bytes on `device`, 8 in flight

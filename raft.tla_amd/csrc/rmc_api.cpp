@@ -15,56 +15,20 @@
 #include <string>
 #include <vector>
 
-#include "../../include/rmc.h"
-#include "raft_packed.h"
-#include "rmc_internal.h"
+#include "rmc_ctx.h"
 
 using namespace rmc;
 
-struct rmc_ctx {
-    rmc_config cfg{};
-    Shape sh{};
-    Params P{};
-    PermTable PT{};
-    int NW = 0;  // 32-bit words per packed state
-    hipStream_t st = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // bracket each level's expansion launches
-    DevBufs B{};
-    Counters* h_ctr = nullptr;  // pinned
-    u32* d_staged = nullptr;
-    u64 table_slots = 0;
-    rmc_result res{};
-    std::string err;
-    std::vector<u64> level_start;  // level d (1-based) = [level_start[d-1], level_start[d])
-    int have_target = 0;           // a violation / deadlock state to trace
-    u64 target_idx = 0;
-    // sharded mode (rmc_dist_*): one ctx per GPU process, exchange by the host driver
-    int dist = 0;
-    u64 sent_slots = 0;
-    u64* h_ocount = nullptr;  // pinned [world]
-    u64 cursor = 0;           // next unexpanded state of the current local frontier
-    int depth = 0;
-    // recovery (rmc_recover): the next rmc_run_bfs continues from this level
-    int resume = 0;
-    int resume_depth = 0;
-};
-
 namespace {
+const char* kVersion = "rmc 2 (raft.tla BFS, gfx950 HIP, packed-delta lanes, HBM fp set, RCCL sharding)";
+}  // namespace
 
-const char* kVersion = "rmc 1 (raft.tla BFS, gfx950 HIP, packed-delta lanes, HBM fp set)";
+namespace rmc_host {
 
 int fail(rmc_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
     return code;
 }
-
-#define HIPCHK(c, expr)                                                                              \
-    do {                                                                                             \
-        hipError_t e_ = (expr);                                                                      \
-        if (e_ != hipSuccess)                                                                        \
-            return fail((c), e_ == hipErrorOutOfMemory ? RMC_E_NOMEM : RMC_E_HIP,                    \
-                        std::string(#expr) + ": " + hipGetErrorString(e_));                          \
-    } while (0)
 
 int kcap_for(int max_msgs) { return max_msgs <= 4 ? 4 : 8; }
 
@@ -309,7 +273,9 @@ int read_counters(rmc_ctx* c) {
     return 0;
 }
 
-}  // namespace
+}  // namespace rmc_host
+
+using namespace rmc_host;
 
 extern "C" {
 
@@ -408,11 +374,9 @@ void rmc_destroy(rmc_ctx* c) {
     (void)hipFree(c->B.table);
     (void)hipFree(c->B.ctr);
     (void)hipFree(c->d_staged);
-    (void)hipFree(c->B.sent);
-    (void)hipFree(c->B.ocount);
+    free_dist(c);
     (void)hipFree(c->B.sidx);
     (void)hipFree(c->B.vbuf);
-    if (c->h_ocount) (void)hipHostFree(c->h_ocount);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -423,6 +387,7 @@ void rmc_destroy(rmc_ctx* c) {
 int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (!c) return RMC_E_INVAL;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->dist.on) return run_bfs_sharded(c, cb, user);
     const auto t0 = std::chrono::steady_clock::now();
     auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
     const bool resume = c->resume != 0;  // rmc_recover restored store, set and counters
@@ -616,7 +581,7 @@ int move_file(rmc_ctx* c, FILE* f, void* dev, u64 n, bool to_file) {
 
 int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
-    if (c->dist) return fail(c, RMC_E_INVAL, "checkpoint: single-GPU runs only");
+    if (c->dist.on) return fail(c, RMC_E_INVAL, "checkpoint: single-GPU runs only");
     if (c->level_start.size() < 2 || c->have_target)
         return fail(c, RMC_E_STATE, "checkpoint: needs a BFS stopped at a level boundary without a violation");
     if (c->res.left_on_queue == 0) return fail(c, RMC_E_STATE, "checkpoint: the search is complete");
@@ -644,7 +609,7 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
 
 int rmc_recover(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
-    if (c->dist) return fail(c, RMC_E_INVAL, "recover: single-GPU runs only");
+    if (c->dist.on) return fail(c, RMC_E_INVAL, "recover: single-GPU runs only");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     FILE* f = fopen(path, "rb");
     if (!f) return fail(c, RMC_E_IO, std::string("recover: cannot open ") + path);
@@ -688,6 +653,7 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
     if (!c || !len) return RMC_E_INVAL;
     if (!c->have_target) return fail(c, RMC_E_STATE, "no violation or deadlock to trace");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->dist.on) return trace_sharded(c, states, families, instances, cap, len);
     std::vector<u64> chain;
     u64 idx = c->target_idx;
     for (;;) {
@@ -873,11 +839,12 @@ int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_b
         if (int rc = encode_view(c, iv, inits.data(), &why)) return fail(c, rc, why);
     }
     const u64 n_init = inits.size() / (u64)c->NW;
-    Params P = c->P;  // no CONSTRAINT in simulation: only the packed capacity bounds
-    P.max_term = 15;
-    P.max_log = LOG_CAP;
-    P.max_msgs = c->sh.K;
-    P.max_dup = 3;
+    // The model's bounds, as TLC's simulator respects a state CONSTRAINT; a
+    // simulation model without one gets the packed capacity from the front-end
+    // (rmc_model_from_files with RMC_FRONT_SIMULATE), so walks never exceed
+    // what a state can hold.
+    Params P = c->P;
+    P.max_msgs = std::min(P.max_msgs, c->sh.K);
     u32 *d_init = nullptr, *d_rec = nullptr;
     SimCounters* d_out = nullptr;
     HIPCHK(c, hipMalloc(&d_init, inits.size() * 4));
@@ -945,153 +912,6 @@ int rmc_sim_replay(rmc_ctx* c, const rmc_sim_config* sc, uint64_t behaviour, rmc
     if (int rc = run_sim(c, sc, &r, (i64)behaviour, &rec)) return rc;
     *len = rec.size() / (size_t)c->NW;
     for (size_t q = 0; q < *len && q < cap; ++q) decode_state(c, rec.data() + q * c->NW, &states[q]);
-    return 0;
-}
-
-// ---- sharded BFS (one process per GPU; the host driver does the all-to-all) ----
-int rmc_dist_init(rmc_ctx* c, int32_t rank, int32_t world, uint64_t sent_cache_slots) {
-    if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return RMC_E_INVAL;
-    if (c->sh.verify) return fail(c, RMC_E_INVAL, "sharded mode does not support full-state verification yet");
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    u64 slots = 1;
-    while (slots < std::max<u64>(sent_cache_slots, 1024)) slots <<= 1;
-    (void)hipFree(c->B.sent);
-    (void)hipFree(c->B.ocount);
-    (void)hipFree(c->B.sidx);
-    (void)hipFree(c->B.vbuf);
-    if (c->h_ocount) (void)hipHostFree(c->h_ocount);
-    c->B.sent = nullptr;
-    c->B.ocount = nullptr;
-    c->h_ocount = nullptr;
-    HIPCHK(c, hipMalloc(&c->B.sent, slots * 8));
-    HIPCHK(c, hipMalloc(&c->B.ocount, 64 * 8));
-    HIPCHK(c, hipHostMalloc(&c->h_ocount, 64 * 8, hipHostMallocDefault));
-    c->sent_slots = slots;
-    c->B.smask = slots - 1;
-    c->B.rank = (u32)rank;
-    c->B.world = (u32)world;
-    c->B.ref_tag = (u64)rank << 48;
-    const char* om = getenv("RMC_OWNER");  // partition: 0 fingerprint, 1 server-0 word, 2 servers 0+1
-    c->B.owner_mode = om ? (u32)std::min(2, std::max(0, atoi(om))) : 2u;
-    // SYMMETRY: the states of one orbit must meet at one owner, so the owner is
-    // a function of the canonical fingerprint (server words differ across the orbit)
-    if (c->sh.sym) c->B.owner_mode = 0;
-    c->dist = 1;
-    return 0;
-}
-
-size_t rmc_dist_record_words(const rmc_ctx* c) { return c ? (size_t)c->NW + 2 : 0; }
-
-int rmc_dist_start(rmc_ctx* c) {
-    if (!c || !c->dist) return RMC_E_STATE;
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    c->res = rmc_result{};
-    c->level_start.clear();
-    c->have_target = 0;
-    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
-    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
-    HIPCHK(c, hipMemsetAsync(c->B.sent, 0, c->sent_slots * 8, c->st));
-    if (int rc = reset_counters(c, false)) return rc;
-    rmc_state_view iv;
-    init_view(c->cfg, &iv);
-    std::vector<u32> packed((size_t)c->NW);
-    std::string why;
-    if (encode_view(c, iv, packed.data(), &why)) return fail(c, RMC_E_INVAL, why);
-    HIPCHK(c, hipMemcpyAsync(c->d_staged, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
-    if (int rc = read_counters(c)) return rc;
-    c->res.generated = c->B.rank == 0 ? 1 : 0;  // the initial state is counted once, globally
-    c->res.distinct = c->h_ctr->count;         // initial states stored on this rank (its first frontier)
-    c->level_start.push_back(0);
-    c->level_start.push_back(c->h_ctr->count);
-    c->cursor = 0;
-    c->depth = 1;
-    if (int rc = reset_counters(c, true)) return rc;
-    return 0;
-}
-
-int rmc_dist_expand(rmc_ctx* c, uint64_t max_states, uint32_t* outbox, uint64_t cap_per_dest, uint64_t* send_counts,
-                    int32_t* frontier_done) {
-    if (!c || !c->dist || !send_counts || !frontier_done || (!outbox && c->B.world > 1)) return RMC_E_INVAL;
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    const u64 hi = c->level_start.back();
-    const u64 a = c->cursor, b = std::min<u64>(hi, a + std::max<u64>(max_states, 1));
-    for (u32 d = 0; d < c->B.world; ++d) send_counts[d] = 0;
-    if (a < b) {
-        c->B.outbox = outbox;
-        c->B.ocap = cap_per_dest;
-        HIPCHK(c, hipMemsetAsync(c->B.ocount, 0, 8 * c->B.world, c->st));
-        HIPCHK(c, hipEventRecord(c->ev0, c->st));
-        HIPCHK(c, launch(c->sh, 3, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
-        HIPCHK(c, hipEventRecord(c->ev1, c->st));
-        HIPCHK(c, hipMemcpyAsync(c->h_ocount, c->B.ocount, 8 * c->B.world, hipMemcpyDeviceToHost, c->st));
-        if (int rc = read_counters(c)) return rc;
-        float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        c->res.expand_kernel_seconds += 1e-3 * ms;
-        c->res.expand_launches += 1;
-        if (c->h_ctr->overflow & 2u)
-            return fail(c, RMC_E_CAPACITY, "outbox full: lower max_states or raise cap_per_dest");
-        if (c->h_ctr->overflow) return fail(c, RMC_E_CAPACITY, "state store full");
-        if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
-        for (u32 d = 0; d < c->B.world; ++d) send_counts[d] = c->h_ocount[d];
-    }
-    c->cursor = b;
-    *frontier_done = b >= hi ? 1 : 0;
-    return 0;
-}
-
-int rmc_dist_insert(rmc_ctx* c, const uint32_t* inbox, uint64_t n_records) {
-    if (!c || !c->dist || (!inbox && n_records)) return RMC_E_INVAL;
-    if (n_records == 0) return 0;
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    HIPCHK(c, launch(c->sh, 4, c->P, c->PT, c->B, n_records, 0, inbox, nullptr, 0, nullptr, c->st));
-    if (int rc = read_counters(c)) return rc;
-    if (c->h_ctr->overflow) return fail(c, RMC_E_CAPACITY, "state store full");
-    if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
-    return 0;
-}
-
-int rmc_dist_state(rmc_ctx* c, uint64_t index, rmc_state_view* state, int32_t* family, int32_t* instance,
-                   uint64_t* parent_ref) {
-    if (!c || !c->dist) return RMC_E_INVAL;
-    if (c->level_start.empty() || index >= c->level_start.back())
-        return fail(c, RMC_E_INVAL, "rmc_dist_state: index beyond the stored states");
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    std::vector<u32> buf((size_t)c->NW);
-    u64 p = 0;
-    uint8_t a = 0;
-    HIPCHK(c, hipMemcpy(buf.data(), c->B.store + index * (u64)c->NW, buf.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemcpy(&p, c->B.parent + index, 8, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemcpy(&a, c->B.act + index, 1, hipMemcpyDeviceToHost));
-    if (state) decode_state(c, buf.data(), state);
-    if (family) *family = family_of(c->P, a);
-    if (instance) *instance = a == 255 ? -1 : a;
-    if (parent_ref) *parent_ref = p;
-    return 0;
-}
-
-// Closes the current level on this rank.  out[0..4] = new states stored here
-// (the next local frontier), successors generated here, probes, 1 + index of
-// a violating state (0 = none), violated invariant bit.
-int rmc_dist_end_level(rmc_ctx* c, uint64_t* out) {
-    if (!c || !c->dist || !out) return RMC_E_INVAL;
-    HIPCHK(c, hipSetDevice(c->cfg.device));
-    if (int rc = read_counters(c)) return rc;
-    const Counters k = *c->h_ctr;
-    const u64 hi = c->level_start.back();
-    out[0] = k.count - hi;
-    out[1] = k.generated;
-    out[2] = k.probes;
-    out[3] = k.viol != ~0ull ? (k.viol >> 4) + 1 : 0;
-    out[4] = k.viol != ~0ull ? (1ull << (k.viol & 15)) : 0;
-    c->res.generated += k.generated;
-    c->res.probes += k.probes;
-    c->res.distinct = k.count;  // states stored on this rank
-    c->level_start.push_back(k.count);
-    c->cursor = hi;
-    c->depth += 1;
-    if (int rc = reset_counters(c, true)) return rc;
     return 0;
 }
 

@@ -1,0 +1,84 @@
+// rmc_ctx.h — the host-side context behind the C ABI (rmc_api.cpp, rmc_dist.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rmc.h"
+#include "raft_packed.h"
+#include "rmc_internal.h"
+
+// Sharded mode (rmc_shard): this ctx is one rank of a BFS whose fingerprint
+// space is partitioned over `world` GPUs.  The exchange runs
+// over RCCL (one communicator per ctx, on the ctx stream) or over a
+// caller-supplied host transport (rmc_transport, e.g. gloo in tests).
+struct DistState {
+    int on = 0;
+    int rank = 0, world = 1;
+    int rccl = 0;                   // 1: RCCL communicator, 0: host transport
+    ncclComm_t comm = nullptr;
+    rmc_transport host{};
+    // device buffers (B.key_out / tick_out / st_out / ocount / scount live in DevBufs)
+    rmc::u64* key_in = nullptr;     // keys received, blocks by source
+    uint8_t* rep_out = nullptr;     // replies to the keys received (same layout)
+    uint8_t* rep_in = nullptr;      // replies to the keys sent, [world][kcap]
+    rmc::u32* st_in = nullptr;      // accepted states received, blocks by source
+    rmc::u64 in_cap = 0;            // keys / states receivable per chunk (all sources)
+    rmc::u64* h_cnt = nullptr;      // pinned scratch: per-destination counts (2 x world)
+    std::vector<uint8_t> stage_send, stage_recv;  // host transport staging
+    rmc::u64 sent_slots = 0;
+    // statistics of the last run
+    rmc::u64 keys_sent = 0, states_sent = 0, chunks = 0;
+    double xfer_seconds = 0;        // wall time in collectives and count read-backs
+};
+
+struct rmc_ctx {
+    rmc_config cfg{};
+    rmc::Shape sh{};
+    rmc::Params P{};
+    rmc::PermTable PT{};
+    int NW = 0;  // 32-bit words per packed state
+    hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // bracket each level's expansion launches
+    rmc::DevBufs B{};
+    rmc::Counters* h_ctr = nullptr;  // pinned
+    rmc::u32* d_staged = nullptr;
+    rmc::u64 table_slots = 0;
+    rmc_result res{};
+    std::string err;
+    std::vector<rmc::u64> level_start;  // level d (1-based) = [level_start[d-1], level_start[d])
+    int have_target = 0;                // a violation / deadlock state to trace
+    rmc::u64 target_idx = 0;            // sharded: global ref (rank << 48 | index)
+    DistState dist;
+    // recovery (rmc_recover): the next rmc_run_bfs continues from this level
+    int resume = 0;
+    int resume_depth = 0;
+};
+
+#define HIPCHK(c, expr)                                                                              \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            return rmc_host::fail((c), e_ == hipErrorOutOfMemory ? RMC_E_NOMEM : RMC_E_HIP,           \
+                                  std::string(#expr) + ": " + hipGetErrorString(e_));                \
+    } while (0)
+
+namespace rmc_host {
+int fail(rmc_ctx* c, int code, const std::string& msg);
+int kcap_for(int max_msgs);
+int validate(const rmc_config* c, std::string* why);
+void fill_params(rmc_ctx* c);
+int family_of(const rmc::Params& P, int lane);
+int encode_view(const rmc_ctx* c, const rmc_state_view& v, rmc::u32* out, std::string* why);
+void decode_state(const rmc_ctx* c, const rmc::u32* in, rmc_state_view* v);
+void init_view(const rmc_config& g, rmc_state_view* v);
+int reset_counters(rmc_ctx* c, bool keep_count);
+int read_counters(rmc_ctx* c);
+// sharded mode (rmc_dist.cpp)
+int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user);
+int trace_sharded(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* instances, size_t cap,
+                  size_t* len);
+void free_dist(rmc_ctx* c);
+}  // namespace rmc_host

@@ -36,9 +36,14 @@ struct DevBufs {
     u64 ref_tag;               // (rank << 48): parent refs are global (rank, index)
     u64* sent;                 // lossy cache of fingerprints already shipped to their owner
     u64 smask;                 // sent-cache slots - 1
-    u32* outbox;               // [world][ocap][NW + 6] records, caller-owned
-    u64 ocap;                  // records per destination
-    unsigned long long* ocount;  // [world] records written per destination
+    // two-phase exchange: phase 1 keys, phase 2 accepted states
+    u64* key_out;              // [world][kcap] keys for each owner
+    u64* tick_out;             // [world][kcap] local tickets: parent index | lane << 56
+    u64 kcap;                  // keys per destination and chunk
+    unsigned long long* ocount;  // [world] keys written per destination
+    u32* st_out;               // [world][scap][NW + 2] accepted states for each owner
+    u64 scap;                  // state records per destination and round
+    unsigned long long* scount;  // [world] state records written per destination
     // full-state verification mode: store index of the state owning each
     // fingerprint-set slot (~0 = not yet published; published between launches
     // by k_publish) and the deferred hits {parent index, slot | lane << 56}
@@ -60,7 +65,8 @@ struct Shape {
 // which: 0 = k_expand over store[a, b); 1 = k_seed of `a` staged states `in`;
 //        2 = k_list of `a` states `in` into `out` (cap records, *count);
 //        3 = sharded k_expand over store[a, b) (outbox in B);
-//        4 = k_insert_remote of `a` received records `in`;
+//        8 = k_materialize_remote of window [b, b + a) of each destination's keys, in = replies;
+//        9 = k_store_remote of `a` received state records `in`;
 //        5 = k_publish over store[a, b) (verification: slot -> store index);
 //        6 = k_verify of `a` deferred hits in B.vbuf;
 //        7 = k_rehash of the stored states [a, b) (recovery).
@@ -75,6 +81,9 @@ struct SimCounters {
 };
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
                       int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
+
+// Sharded mode, phase 1 owner side: insert n received keys, reply[t] = new.
+hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, hipStream_t st);
 
 // Fingerprint salt for the kernels of this device (0 = default hash).
 hipError_t set_fp_salt(u64 seed, hipStream_t st);

@@ -366,15 +366,17 @@ __device__ __forceinline__ u64 fp_of_materialised(const u64 (&w)[S], const u32 (
     return h ? h : 1ull;
 }
 
-// Sharded mode: the listed successors carry their owner rank.  Owned ones are
-// stored as above; the others are materialised into the outbox of their owner
-// as records {state, fingerprint, global parent ref, lane} (RecW words), for
-// the host driver's all-to-all.  Slots are reserved with one atomic per
-// destination per 64-entry round.
+// Sharded mode, phase 1 (fingerprint first): the listed
+// successors carry their owner rank.  Owned ones were inserted into the local
+// set at probe time and are stored as in flush_new; for the others only the
+// key travels: it goes to the owner's key outbox, with a local ticket (parent
+// index | lane << 56) kept here so that, if the owner answers "new", phase 2
+// re-derives the successor and ships the state.  Slots are reserved with one
+// atomic per destination per flush.
 template <int S, int K>
 __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
-                                           const uint8_t* l_lane, const uint8_t* l_dest, u32 n) {
-    constexpr int NW = 2 * S + K, RW = NW + 2;
+                                           const uint8_t* l_lane, const uint8_t* l_dest, const u64* l_key, u32 n) {
+    constexpr int NW = 2 * S + K;
     wave_sync_lds();
     const int me = (int)__lane_id();
     const u64 lt = (1ull << me) - 1ull;
@@ -409,6 +411,19 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         if (!valid) continue;
         const u64 rel = l_rel[e];
         const int lane = l_lane[e];
+        if (dest != B.rank) {  // the key to its owner, the ticket stays here
+            if (slot >= B.kcap) {
+                atomicOr(&B.ctr->overflow, 2u);
+                continue;
+            }
+            B.key_out[(u64)dest * B.kcap + slot] = l_key[e];
+            B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
+            continue;
+        }
+        if (slot >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
         u64 w[S];
         u32 m[K];
         load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
@@ -417,28 +432,11 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         u64 wo[S];
         u32 mo[K];
         materialise<S, K>(w, m, d, wo, mo);
-        if (dest == B.rank) {
-            if (slot >= B.cap) {
-                atomicOr(&B.ctr->overflow, 1u);
-                continue;
-            }
-            store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
-            B.parent[slot] = B.ref_tag | (lo + rel);
-            B.act[slot] = (uint8_t)lane;
-            const int v = check_invariants<S, K>(wo, mo, P);
-            if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
-        } else {
-            if (slot >= B.ocap) {
-                atomicOr(&B.ctr->overflow, 2u);
-                continue;
-            }
-            u32* r = B.outbox + ((u64)dest * B.ocap + slot) * (u64)RW;
-            store_state<S, K>(r, wo, mo);
-            // global parent ref with the lane in bits 40-47 (the owner
-            // recomputes the fingerprint from the state: 8 B less per record)
-            const u64 ref = B.ref_tag | ((u64)lane << 40) | (lo + rel);
-            r[NW] = (u32)ref; r[NW + 1] = (u32)(ref >> 32);
-        }
+        store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
+        B.parent[slot] = B.ref_tag | (lo + rel);
+        B.act[slot] = (uint8_t)lane;
+        const int v = check_invariants<S, K>(wo, mo, P);
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
     }
     wave_sync_lds();
 }
@@ -456,10 +454,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
-    constexpr int LCAP = DIST ? 320 : WCAP;
+    constexpr int LCAP = DIST ? 256 : WCAP;
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
     __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? LCAP : 1];
+    __shared__ u64 s_lkey[DIST ? 4 : 1][DIST ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
     __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
     const int wv = (int)(threadIdx.x >> 6);
@@ -468,6 +467,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u32* l_rel = s_rel[wv];
     uint8_t* l_lane = s_lane[wv];
     uint8_t* l_dest = s_dest[DIST ? wv : 0];
+    u64* l_key = s_lkey[DIST ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u64 gen = 0;
     u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
@@ -625,11 +625,14 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
                         l_rel[pos] = (u32)rel;
                         l_lane[pos] = (uint8_t)(lane0 + b);
-                        if constexpr (DIST) l_dest[pos] = s_own[b][threadIdx.x];
+                        if constexpr (DIST) {
+                            l_dest[pos] = s_own[b][threadIdx.x];
+                            l_key[pos] = key[b];
+                        }
                     }
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
-                        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
+                        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
                     }
@@ -640,7 +643,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         gen += g;
     }
     if (n) {
-        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
+        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
     // wave reductions of the generated and probe counts, one atomic each per wave
@@ -685,34 +688,86 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
     expand_body<S, K, true, BATCH, false, false>(P, PT, B, lo, hi);
 }
 
-// The sharded expansion at 6 waves/SIMD (its owner bookkeeping takes 82 VGPRs
-// unconstrained: 5 waves): the register budget is capped for this variant only.
+// The sharded expansion (owner routing, sent-cache, per-wave key lists).
 template <int S, int K, int BATCH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_expand_dist(
+__global__ __launch_bounds__(256) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
 
-// Sharded mode, owner side: insert the n records received from other ranks
-// (k_expand<DIST> outboxes after the all-to-all).  A winning record's state is
-// copied into the store with its global parent ref; same per-wave list and
-// single allocation atomic per flush as k_expand.
+// Sharded mode, phase 1, owner side: insert the keys other ranks sent;
+// reply[t] = 1 if key t was new here (its sender then ships the state).
+__global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64* keys, uint8_t* reply, u64 n) {
+    u64 pr = 0;
+    for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
+        const u64 t = t0 + threadIdx.x;
+        if (t < n) reply[t] = (uint8_t)fp_insert(B.table, B.tmask, keys[t], &B.ctr->table_full);
+        pr += (u64)__popcll(__ballot(t < n));
+    }
+    if (__lane_id() == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+}
+
+// Sharded mode, phase 2, sender side: for every key an owner accepted
+// (reply[d * kcap + i] = 1), re-derive the successor from its ticket and put
+// the record {state, global parent ref | lane << 40} into owner d's state
+// outbox.  Grid over (destination, key index).
 template <int S, int K>
-__device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, const u32* inbox, const u32* l_idx,
-                                             u32 n) {
+__global__ __launch_bounds__(256) void k_materialize_remote(const Params P, const DevBufs B, const uint8_t* reply,
+                                                            u64 per_dest, u64 i0) {
     constexpr int NW = 2 * S + K, RW = NW + 2;
-    wave_sync_lds();
+    const u64 total = per_dest * B.world;  // window [i0, i0 + per_dest) of every destination's keys
+    for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < total; t += (u64)gridDim.x * 256ull) {
+        const u32 d = (u32)(t / per_dest);
+        const u64 i = i0 + (t - (u64)d * per_dest);
+        if (d == B.rank || i >= B.ocount[d] || !reply[(u64)d * B.kcap + i]) continue;
+        const u64 tick = B.tick_out[(u64)d * B.kcap + i];
+        const u64 pidx = tick & ((1ull << 56) - 1);
+        const int lane = (int)(tick >> 56);
+        const u64 slot = atomicAdd((unsigned long long*)&B.scount[d], 1ull);
+        if (slot >= B.scap) {
+            atomicOr(&B.ctr->overflow, 2u);
+            continue;
+        }
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + pidx * (u64)NW, w, m);
+        Delta dl;
+        lane_delta<S, K>(w, m, lane, P, dl);
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, dl, wo, mo);
+        u32* r = B.st_out + ((u64)d * B.scap + slot) * (u64)RW;
+        store_state<S, K>(r, wo, mo);
+        const u64 ref = B.ref_tag | ((u64)lane << 40) | pidx;
+        r[NW] = (u32)ref;
+        r[NW + 1] = (u32)(ref >> 32);
+    }
+}
+
+// Sharded mode, phase 2, owner side: store the n accepted states received (their
+// keys are already in this rank's set since phase 1): one allocation atomic per
+// wave, parent ref and lane from the record, fused invariants.
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevBufs B, const u32* inbox, u64 n) {
+    constexpr int NW = 2 * S + K, RW = NW + 2;
     const int me = (int)__lane_id();
-    u64 base = 0;
-    if (me == 0) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)n);
-    base = bcast64(base, 0);
-    for (u32 e = (u32)me; e < n; e += 64) {
-        const u64 ni = base + e;
+    const u64 lt = (1ull << me) - 1ull;
+    for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
+        const u64 t = t0 + threadIdx.x;
+        const bool live = t < n;
+        const u64 bal = __ballot(live);
+        if (!bal) continue;
+        const int leader = __ffsll((long long)bal) - 1;
+        u64 base = 0;
+        if (me == leader) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)__popcll(bal));
+        base = bcast64(base, leader);
+        if (!live) continue;
+        const u64 ni = base + (u64)__popcll(bal & lt);
         if (ni >= B.cap) {
             atomicOr(&B.ctr->overflow, 1u);
             continue;
         }
-        const u32* r = inbox + (u64)l_idx[e] * RW;
+        const u32* r = inbox + t * (u64)RW;
         u64 w[S];
         u32 m[K];
         load_state<S, K>(r, w, m);
@@ -723,54 +778,6 @@ __device__ __forceinline__ void flush_remote(const Params& P, const DevBufs& B, 
         const int v = check_invariants<S, K>(w, m, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
-    wave_sync_lds();
-}
-
-// SYM: the key is the canonical (least permuted) fingerprint, as k_expand's.
-template <int S, int K, bool SYM>
-__global__ __launch_bounds__(256) void k_insert_remote(const Params P, const PermTable PT, const DevBufs B,
-                                                       const u32* inbox, u64 n) {
-    constexpr int NW = 2 * S + K, RW = NW + 2;
-    constexpr int NP = SYM ? NPerm<S>::v : 1;
-    __shared__ u32 s_idx[4][WCAP];
-    const int wv = (int)(threadIdx.x >> 6);
-    const int me = (int)__lane_id();
-    const u64 lt = (1ull << me) - 1ull;
-    u32* l_idx = s_idx[wv];
-    u32 cnt = 0;
-    u64 pr = 0;
-    for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
-        const u64 t = t0 + threadIdx.x;
-        const bool live = t < n;
-        int is_new = 0;
-        if (live) {
-            u64 w[S];
-            u32 m[K];
-            load_state<S, K>(inbox + t * (u64)RW, w, m);
-            u64 key = fp_of_materialised<S, K>(w, m, P);
-            if constexpr (SYM) {
-                u64 hp[NP];
-                perm_fps<S, K, NP>(w, m, PT, hp);
-                key = ~0ull;
-#pragma unroll
-                for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
-                key = key ? key : 1ull;
-            }
-            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
-        }
-        pr += (u64)__popcll(__ballot(live));
-        const u64 bal = __ballot(is_new);
-        if (bal) {
-            if (is_new) l_idx[cnt + (u32)__popcll(bal & lt)] = (u32)t;
-            cnt += (u32)__popcll(bal);
-            if (cnt > (u32)(WCAP - 64)) {
-                flush_remote<S, K>(P, B, inbox, l_idx, cnt);
-                cnt = 0;
-            }
-        }
-    }
-    if (cnt) flush_remote<S, K>(P, B, inbox, l_idx, cnt);
-    if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
 }
 
 // Probe-rate microbenchmark (the roofline ceiling for k_expand): every thread
@@ -793,6 +800,14 @@ __global__ __launch_bounds__(256) void k_probe_bench(u64* table, u64 mask, u32 i
         for (int b = 0; b < BATCH; ++b) acc ^= v[b];
     }
     if (acc == 0x5A5A5A5A5A5A5A5Aull) sink[0] = acc;  // keeps the loads live
+}
+
+hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const u64 blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_owner_insert, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, st, B, keys,
+                       reply, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st) {
@@ -1013,12 +1028,14 @@ hipError_t set_fp_salt(u64 seed, hipStream_t st) {
 
 static const u64 kExpandGrid = 2048;
 
-// Expansion kernel variant for same-box A/B runs (RMC_EXPAND_VARIANT):
-// 0 = mixes recomputed per lane, 1 = the parent's mixes precomputed.
+// Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs):
+// 1 (default) = the parent's per-component mixes precomputed once per state
+// (91 VGPRs, 5 waves/SIMD; 2.5 % faster on MCraftBench than 0, profiles/r02),
+// 0 = every lane recomputes them (77 VGPRs, 6 waves), 2 = 1 capped at 6 waves.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     return v;
 }
@@ -1029,7 +1046,8 @@ constexpr int kBatch = 8;
 template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, bool verify, const Params& P, const PermTable& PT, const DevBufs& B, u64 a,
                            u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-    const u64 n = (which == 0 || which == 3 || which == 5 || which == 7) ? (b - a) : a;
+    const u64 n = (which == 0 || which == 3 || which == 5 || which == 7) ? (b - a)
+                : which == 8 ? a * (u64)B.world : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
@@ -1056,8 +1074,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         else
             hipLaunchKernelGGL((k_expand_dist<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-    } else if (which == 4) {
-        hipLaunchKernelGGL((k_insert_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
+    } else if (which == 8) {  // a = keys per destination block (max); out = replies
+        hipLaunchKernelGGL((k_materialize_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B,
+                           reinterpret_cast<const uint8_t*>(in), a, b);
+    } else if (which == 9) {
+        hipLaunchKernelGGL((k_store_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, in, a);
     } else if (which == 5) {
         hipLaunchKernelGGL((k_publish<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
     } else if (which == 7) {

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <ctime>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rmc.h"
@@ -150,7 +151,8 @@ int usage() {
     fprintf(stderr,
             "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N]\n"
             "               [-verify] [-fpseed S] [-checkpoint F] [-recover F] [-simulate [num=N]] [-seed S]\n"
-            "               [-raft raft.tla] [-builtin-raft] X.tla\n"
+            "               [-raft raft.tla] [-builtin-raft] [-gpus N] X.tla\n"
+            "  -gpus N        shard the search over N GPUs (one ctx and RCCL rank per GPU)\n"
             "  -raft F        the raft.tla to verify against the compiled-in spec (default: next to X.tla)\n"
             "  -builtin-raft  no raft.tla on disk: check the compiled-in lemmy/raft.tla (said in the output)\n"
             "  -depth N   stop after N BFS levels (level N is left on the queue)\n"
@@ -221,7 +223,7 @@ int main(int argc, char** argv) {
     std::string cfg, tla;
     int depth = 0, device = 0, nodeadlock = 0, verify = 0;
     unsigned long long fpseed = 0, seed = 0, num = 0;
-    int simulate = 0;
+    int simulate = 0, gpus = 1;
     std::string ckpt, recover, raft;
     uint32_t fopts = 0;
     unsigned long long capacity = 0;
@@ -234,6 +236,7 @@ int main(int argc, char** argv) {
         else if (s == "-device") { const char* v = next(); if (!v) return usage(); device = atoi(v); }
         else if (s == "-capacity") { const char* v = next(); if (!v) return usage(); capacity = strtoull(v, nullptr, 10); }
         else if (s == "-workers") { if (!next()) return usage(); }  // accepted for compatibility
+        else if (s == "-gpus") { const char* v = next(); if (!v) return usage(); gpus = atoi(v); }
         else if (s == "-verify") verify = 1;
         else if (s == "-raft") { const char* v = next(); if (!v) return usage(); raft = v; }
         else if (s == "-builtin-raft") fopts |= RMC_FRONT_BUILTIN_RAFT;
@@ -275,6 +278,41 @@ int main(int argc, char** argv) {
     rmc_ctx* ctx = nullptr;
     rc = rmc_create(&c, &ctx);
     if (rc) { printf("Error: rmc_create failed (%d)\n", rc); return 1; }
+    // -gpus N: one ctx per GPU (devices device..device+N-1), each a rank of the
+    // sharded search on librmc's RCCL communicator; ranks 1..N-1 run on helper
+    // threads and take part in every collective (the BFS and the trace walk)
+    std::vector<std::thread> helpers;
+    if (gpus > 1) {
+        if (verify || !ckpt.empty() || !recover.empty()) {
+            printf("Error: -verify, -checkpoint and -recover are single-GPU options\n");
+            return 1;
+        }
+        uint8_t id[128];
+        if (rmc_rccl_unique_id(id)) { printf("Error: rmc_rccl_unique_id failed\n"); return 1; }
+        for (int r = 1; r < gpus; ++r) {
+            helpers.emplace_back([=]() {
+                rmc_config cr = c;
+                cr.device = device + r;
+                rmc_ctx* h = nullptr;
+                if (rmc_create(&cr, &h)) { fprintf(stderr, "rank %d: rmc_create failed\n", r); return; }
+                if (rmc_shard(h, r, gpus, id, nullptr, 0, 0)) { fprintf(stderr, "rank %d: %s\n", r, rmc_last_error(h)); return; }
+                if (rmc_run_bfs(h, nullptr, nullptr)) { fprintf(stderr, "rank %d: %s\n", r, rmc_last_error(h)); return; }
+                rmc_result rr;
+                rmc_get_result(h, &rr);
+                if (rr.violated_inv || rr.deadlock) {  // the trace walk is collective: same calls as rank 0
+                    size_t n = 0;
+                    rmc_trace(h, nullptr, nullptr, nullptr, 0, &n);
+                    std::vector<rmc_state_view> st(n);
+                    std::vector<int32_t> f(n), in(n);
+                    rmc_trace(h, st.data(), f.data(), in.data(), n, &n);
+                }
+                rmc_destroy(h);
+            });
+        }
+        rc = rmc_shard(ctx, 0, gpus, id, nullptr, 0, 0);
+        if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); return 1; }
+        printf("Sharded over %d GPUs (librmc two-phase exchange over RCCL).\n", gpus);
+    }
     if (!recover.empty()) {
         rc = rmc_recover(ctx, recover.c_str());
         if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
@@ -324,6 +362,7 @@ int main(int argc, char** argv) {
         printf("Finished in %.0fms (%.0f distinct states/s)\n", r.seconds * 1e3, r.distinct / (r.seconds > 0 ? r.seconds : 1));
     else
         printf("Finished in %.0fms after recovery (counts include the checkpointed levels)\n", r.seconds * 1e3);
+    for (auto& t : helpers) t.join();
     rmc_destroy(ctx);
     return exitcode;
 }

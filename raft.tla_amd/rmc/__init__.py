@@ -47,7 +47,9 @@ class Result(C.Structure):
                 ("deadlock", C.c_int32), ("collision_probability", C.c_double),
                 ("seconds", C.c_double), ("expand_kernel_seconds", C.c_double),
                 ("expand_launches", C.c_uint64), ("probes", C.c_uint64),
-                ("collisions", C.c_uint64), ("verified", C.c_uint64)]
+                ("collisions", C.c_uint64), ("verified", C.c_uint64),
+                ("keys_sent", C.c_uint64), ("states_sent", C.c_uint64), ("chunks", C.c_uint64),
+                ("exchange_seconds", C.c_double), ("stored_here", C.c_uint64)]
 
 
 class LevelStats(C.Structure):
@@ -100,12 +102,18 @@ class SimResult(C.Structure):
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.POINTER(LevelStats), C.c_void_p)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p,
+                           C.POINTER(C.c_uint64))
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
+
+
+class Transport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("alltoallv", ALLTOALLV_FN), ("allgather", ALLGATHER_FN)]
 
 # Every symbol include/rmc.h declares (checked by tests/test_abi.py).
 EXPORTS = ("rmc_create", "rmc_destroy", "rmc_last_error", "rmc_version", "rmc_run_bfs",
            "rmc_get_result", "rmc_trace", "rmc_state_bytes", "rmc_expand",
-           "rmc_config_from_files", "rmc_probe_bench", "rmc_dist_init", "rmc_dist_record_words",
-           "rmc_dist_start", "rmc_dist_expand", "rmc_dist_insert", "rmc_dist_end_level", "rmc_dist_state",
+           "rmc_config_from_files", "rmc_probe_bench", "rmc_rccl_unique_id", "rmc_shard",
            "rmc_set_seed", "rmc_simulate", "rmc_sim_replay", "rmc_set_fp_bits",
            "rmc_sim_config_from_files", "rmc_checkpoint", "rmc_recover", "rmc_model_from_files",
            "rmc_action_location", "rmc_smoke_init")
@@ -162,22 +170,11 @@ def native():
         lib.rmc_probe_bench.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int,
                                         C.POINTER(C.c_double)]
         lib.rmc_probe_bench.restype = C.c_int
-        lib.rmc_dist_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_uint64]
-        lib.rmc_dist_init.restype = C.c_int
-        lib.rmc_dist_record_words.argtypes = [C.c_void_p]
-        lib.rmc_dist_record_words.restype = C.c_size_t
-        lib.rmc_dist_start.argtypes = [C.c_void_p]
-        lib.rmc_dist_start.restype = C.c_int
-        lib.rmc_dist_expand.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
-                                        C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
-        lib.rmc_dist_expand.restype = C.c_int
-        lib.rmc_dist_insert.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-        lib.rmc_dist_insert.restype = C.c_int
-        lib.rmc_dist_end_level.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
-        lib.rmc_dist_end_level.restype = C.c_int
-        lib.rmc_dist_state.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(StateView), C.POINTER(C.c_int32),
-                                       C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
-        lib.rmc_dist_state.restype = C.c_int
+        lib.rmc_rccl_unique_id.argtypes = [C.c_char_p]
+        lib.rmc_rccl_unique_id.restype = C.c_int
+        lib.rmc_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p, C.POINTER(Transport),
+                                  C.c_uint64, C.c_uint64]
+        lib.rmc_shard.restype = C.c_int
         lib.rmc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
         lib.rmc_set_seed.restype = C.c_int
         lib.rmc_set_fp_bits.argtypes = [C.c_void_p, C.c_int32]
@@ -244,6 +241,15 @@ def smoke_init(cfg, smoke_k, smoke_nat=2, seed=0):
     if rc:
         raise RmcError(rc, "rmc_smoke_init failed")
     return list(st)
+
+
+def rccl_unique_id() -> bytes:
+    """rmc_rccl_unique_id: the 128-byte id rank 0 hands to every rank's rmc_shard."""
+    buf = C.create_string_buffer(128)
+    rc = native().rmc_rccl_unique_id(buf)
+    if rc:
+        raise RmcError(rc, "rmc_rccl_unique_id failed")
+    return buf.raw
 
 
 def action_location(action):
@@ -321,6 +327,17 @@ class Checker:
         n = C.c_size_t()
         self._check(self.lib.rmc_sim_replay(self.ctx, C.byref(sc), behaviour, st, depth, C.byref(n)))
         return [st[k] for k in range(min(n.value, depth))]
+
+    def shard(self, rank: int, world: int, rccl_id: bytes | None = None, transport=None,
+              keys_per_dest: int = 0, sent_cache_slots: int = 0):
+        """rmc_shard: make this ctx rank `rank` of `world`.  RCCL when rccl_id
+        (from rccl_unique_id() on rank 0) is given, else `transport` (a
+        Transport, e.g. rmc.dist.GlooTransport().struct)."""
+        self._shard_keep = transport  # the callbacks must outlive the ctx
+        st = getattr(transport, "struct", transport)
+        self._check(self.lib.rmc_shard(self.ctx, rank, world, rccl_id,
+                                       C.byref(st) if st is not None else None,
+                                       keys_per_dest, sent_cache_slots))
 
     def checkpoint(self, path: str):
         """Write the stopped search to `path` (rmc_checkpoint; TLC -checkpoint)."""

@@ -2,9 +2,9 @@
 torchrun).
 
 Every rank uses GPU `--device` (several ranks may share one GPU with the gloo
-backend), runs rmc.dist.run on a golden config (`--case`) or a TLC model
-(`--cfg`), and rank 0 writes the global result plus per-rank balance stats as
-JSON."""
+host transport), makes its Checker a shard (rmc_shard through rmc.dist.shard)
+of a golden config (`--case`) or a TLC model (`--cfg`), runs the BFS inside
+librmc, and rank 0 writes the global result plus per-rank stats as JSON."""
 import argparse
 import json
 import os
@@ -27,9 +27,9 @@ def main():
     ap.add_argument("--cfg")
     ap.add_argument("--out", required=True)
     ap.add_argument("--backend", default="gloo")
+    ap.add_argument("--transport", default="auto", help="rccl | host | auto (rccl on nccl)")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK")
-    ap.add_argument("--chunk", type=int, default=1 << 16)
-    ap.add_argument("--cap-per-dest", type=int, default=1 << 20)
+    ap.add_argument("--keys-per-dest", type=int, default=1 << 18)
     ap.add_argument("--capacity", type=int, default=0)
     ap.add_argument("--rerun", type=int, default=1)
     args = ap.parse_args()
@@ -53,30 +53,30 @@ def main():
         cfg.device = dev
         cfg.state_capacity = args.capacity or (1 << 26)
     with rmc.Checker(cfg) as ck:
+        info = rdist.shard(ck, transport=args.transport, keys_per_dest=args.keys_per_dest,
+                           sent_cache_slots=1 << 22)
         t0 = time.time()
-        r = rdist.run(ck, chunk_states=args.chunk, cap_per_dest=args.cap_per_dest,
-                      sent_cache_slots=1 << 24)
+        r = ck.run()  # collective: the global result on every rank
         wall = time.time() - t0
-        local = ck.result()
-        reruns = [rdist.run(ck, chunk_states=args.chunk, cap_per_dest=args.cap_per_dest, init=False)
-                  for _ in range(args.rerun)]
-        # the trace is identical on every rank (it is broadcast step by step)
-        if r.trace:
-            mine = [[f, i, bytes(v).hex()] for f, i, v in r.trace]
+        levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+        trace = ck.trace() if (r.violated_inv or r.deadlock) else []
+        if trace:  # identical on every rank (gathered step by step)
+            mine = [[f, i, bytes(v).hex()] for f, i, v in trace]
             allt = [None] * world
             dist.all_gather_object(allt, mine)
             assert all(t == mine for t in allt), "ranks disagree on the trace"
-
-    per_rank = [None] * world
-    dist.all_gather_object(per_rank, dict(rank=rank, distinct=local.distinct,
-                                          records_sent=r.records_sent))
+        reruns = [ck.run() for _ in range(args.rerun)]
+        fields = ("distinct", "generated", "depth", "left_on_queue", "violated_inv", "violation_depth")
+        summary = {k: getattr(r, k) for k in fields}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, dict(rank=rank, stored=r.stored_here, keys_sent=r.keys_sent,
+                                              states_sent=r.states_sent, chunks=r.chunks,
+                                              summary=summary, exchange_s=r.exchange_seconds))
     if rank == 0:
-        json.dump(dict(distinct=r.distinct, generated=r.generated, depth=r.depth,
-                       left_on_queue=r.left_on_queue,
-                       levels=r.levels, violated_inv=r.violated_inv,
-                       violation_depth=r.violation_depth, records_sent=r.records_sent,
-                       per_rank=per_rank, wall_s=wall,
-                       trace=[[f, i, bytes(v).hex()] for f, i, v in r.trace],
+        json.dump(dict(summary, levels=levels, keys_sent=sum(p["keys_sent"] for p in per_rank),
+                       states_sent=sum(p["states_sent"] for p in per_rank), per_rank=per_rank,
+                       wall_s=wall, transport=info.transport,
+                       trace=[[f, i, bytes(v).hex()] for f, i, v in trace],
                        owner_mode=os.environ.get("RMC_OWNER", "2"),
                        rerun=[[x.distinct, x.generated, x.depth] for x in reruns]),
                   open(args.out, "w"))

@@ -27,39 +27,39 @@ def _torchrun(nproc, args, port):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
 
 
-EXCHANGE_WORKER = r"""
-import os, sys, torch, torch.distributed as dist
+TRANSPORT_WORKER = r"""
+import ctypes as C, os, sys, torch, torch.distributed as dist
 sys.path.insert(0, os.path.join(sys.argv[1], 'raft.tla_amd'))
-from rmc.dist import exchange, _allgather
+from rmc.dist import GlooTransport
 dist.init_process_group('gloo', init_method='env://')
 r, w = dist.get_rank(), dist.get_world_size()
-cap, rw = 8, 3
-ob = torch.zeros((w, cap, rw), dtype=torch.int32)
-send = [(r + d) % 3 for d in range(w)]
-for d in range(w):
-    for k in range(send[d]):
-        ob[d, k] = torch.tensor([r, d, k])
-out, rc, fl = exchange(ob, send, more=(r == 0))
-assert fl == [1] + [0] * (w - 1), fl
-row = 0
-for s in range(w):
-    assert rc[s] == (s + r) % 3, (rc, s, r)
-    for k in range(rc[s]):
-        assert out[row].tolist() == [s, r, k]
-        row += 1
-assert row == out.shape[0]
-e, rc0, _ = exchange(ob, [0] * w if r == 0 else [1] + [0] * (w - 1))
-assert e.shape[0] == (w - 1 if r == 0 else 0)
-assert rc0 == ([0] + [1] * (w - 1) if r == 0 else [0] * w)
-assert _allgather([r, 7], None, True, None) == [[q, 7] for q in range(w)]
+t = GlooTransport()
+# alltoallv: rank r sends (r + d) % 3 bytes of value 10 * r + d to rank d
+sb = [(r + d) % 3 for d in range(w)]
+rb = [(s + r) % 3 for s in range(w)]
+send = bytes(b for d in range(w) for b in [10 * r + d] * sb[d])
+sbuf = C.create_string_buffer(send, max(1, len(send)))
+rbuf = C.create_string_buffer(max(1, sum(rb)))
+SB, RB = (C.c_uint64 * w)(*sb), (C.c_uint64 * w)(*rb)
+assert t.struct.alltoallv(None, C.addressof(sbuf), SB, C.addressof(rbuf), RB) == 0, t.errors
+want = bytes(b for s in range(w) for b in [10 * s + r] * rb[s])
+assert rbuf.raw[:sum(rb)] == want, (rbuf.raw, want)
+# allgather of 8 bytes per rank
+mine = C.create_string_buffer(bytes([r] * 8), 8)
+out = C.create_string_buffer(8 * w)
+assert t.struct.allgather(None, C.addressof(mine), 8, C.addressof(out)) == 0, t.errors
+assert out.raw == bytes(b for q in range(w) for b in [q] * 8)
 dist.destroy_process_group()
 """
 
 
-def test_exchange_protocol_gloo_world2(tmp_path):
-    script = tmp_path / "xw.py"
-    script.write_text(EXCHANGE_WORKER)
-    r = _torchrun(2, [str(script), ROOT], 29611)
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_host_transport_gloo(nproc, tmp_path):
+    """The host transport librmc's sharded BFS calls back into (rmc_transport):
+    all-to-all of byte blocks and all-gather, world 2 and 3 on gloo (CPU)."""
+    script = tmp_path / "tw.py"
+    script.write_text(TRANSPORT_WORKER)
+    r = _torchrun(nproc, [str(script), ROOT], 29611 + nproc)
     assert r.returncode == 0, r.stderr[-3000:]
 
 
@@ -70,10 +70,13 @@ def test_exchange_protocol_gloo_world2(tmp_path):
                                                 ("msgs5_dup2_prefix9", 2, "gloo"), ("s4_prefix10", 3, "gloo"),
                                                 ("small", 1, "nccl")])
 def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
-    """gloo: N ranks share the box's one GPU.  nccl: one rank through RCCL, the
-    code path of the driver's multi-GPU bench (device tensors, stream sync).
-    SYMMETRY cases route by the canonical fingerprint; depth-bounded cases stop
-    with the last level unexpanded, as rmc_run_bfs."""
+    """The sharded BFS inside librmc (rmc_shard + rmc_run_bfs), through the C
+    ABI.  gloo: N ranks share the box's one GPU over the host transport.
+    nccl: one rank on librmc's own RCCL communicator, the code path of the
+    driver's multi-GPU bench.  SYMMETRY cases route by the canonical
+    fingerprint; depth-bounded cases stop with the last level unexpanded, as
+    the single-GPU search.  A small key outbox forces several chunks per
+    level and several phase-2 rounds."""
     g = GOLDEN[case]
     out = tmp_path / "r.json"
     r = _torchrun(nproc, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out",
@@ -84,10 +87,12 @@ def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
     assert res["generated"] == g["generated"]
     assert res["depth"] == g["depth"]
     assert res["left_on_queue"] == g["left_on_queue"]
-    assert [1] + [x for x in res["levels"] if x] == g["level_new"]
+    assert res["levels"] == g["level_new"]
     assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
-    assert res["records_sent"] > 0 or nproc == 1
-    assert sum(p["distinct"] for p in res["per_rank"]) == g["distinct"]
+    assert res["keys_sent"] > 0 or nproc == 1
+    assert res["states_sent"] > 0 or nproc == 1
+    assert sum(p["stored"] for p in res["per_rank"]) == g["distinct"]
+    assert all(p["summary"]["distinct"] == g["distinct"] for p in res["per_rank"])  # global on every rank
 
 
 @pytest.mark.gpu
