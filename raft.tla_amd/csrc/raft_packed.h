@@ -505,6 +505,32 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
     return 1;
 }
 
+// CONSTRAINT of a delta without its fingerprint (the SYMMETRY kernels hash the
+// canonical form instead).
+template <int S, int K>
+RMC_HD int delta_in_model(const u32 (&m)[K], const Delta& d, const Params& P) {
+    int nmsg = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
+    if (d.srv >= 0) {
+        if ((d.w_new >> 63) != 0) return 0;
+        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
+    }
+    if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
+    if (d.has_add) {
+        int found = -1;
+#pragma unroll
+        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+        if (found >= 0) {
+            if ((int)m_cnt(selm<K>(m, found)) + 1 > P.max_dup) return 0;
+        } else {
+            if (1 > P.max_dup) return 0;
+            nmsg += 1;
+        }
+    }
+    return nmsg <= P.max_msgs;
+}
+
 template <int S, int K>
 RMC_HD u64 state_fp(const u64 (&w)[S], const u32 (&m)[K]) {
     u64 h = 0;
@@ -741,10 +767,10 @@ RMC_HD int check_invariants(const u64 (&w)[S], const u32 (&m)[K], const Params& 
 }
 
 // ---- symmetry: server permutations -----------------------------------------------
-// A permutation p (old server id -> new id, S <= 4) is packed 2 bits per
+// A permutation p (old server id -> new id, S <= 5) is packed 3 bits per
 // entry into a u32 `code`, so applying it is shifts and masks: a small array
 // indexed by runtime ids would be forced out of registers.
-RMC_HD u32 pe(u32 code, u32 x) { return (code >> (2 * x)) & 3u; }
+RMC_HD u32 pe(u32 code, u32 x) { return (code >> (3 * x)) & 7u; }
 template <int S>
 RMC_HD u64 perm_word(u64 w, u32 code) {  // the word moves to position pe(code, i)
     u64 r = w & (0x3Full | (0x3ull << CI_SH) | (0x1FFFFull << LEN_SH));  // ct, st, ci, log
@@ -763,6 +789,167 @@ RMC_HD u64 perm_word(u64 w, u32 code) {  // the word moves to position pe(code, 
 RMC_HD u32 perm_slot(u32 sl, u32 code) {
     if (!sl) return 0;
     return (sl & ~(0xFCu)) | (pe(code, m_src(sl)) << 2) | (pe(code, m_dst(sl)) << 5);
+}
+
+// Canonical key under SYMMETRY Permutations(Server): the least fingerprint of
+// the permuted states pi(s) over the permutations pi that SORT the servers by
+// a permutation-invariant signature, every order of tied servers included.
+// Relabelling s by sigma relabels the signatures the same way, so the set
+// {pi(s)} -- and its least fingerprint -- is the same for every member of the
+// orbit: an exact canonical key (up to fingerprint collisions), whatever the
+// signature.  A weak signature only costs ties (more permutations to try);
+// with messages folded in, 99 % of the MCraftBench states have none (measured
+// on BFS levels 10-14), so a lane usually fingerprints ONE permuted state
+// instead of all S! (DESIGN.md "SYMMETRY").
+// Signature, part 1: the server word without server ids (term, role, commit
+// index, log), votedFor as Nil / self / other, vote-set sizes and self bits,
+// its own (nextIndex, matchIndex) and an order-free sum over its peers'.
+template <int S>
+RMC_HD u64 sig_base(u64 w, u32 i) {
+    u64 s = w & (0x3Full | (0x7FFFFull << CI_SH));  // ct, st, ci, len, log
+    const u32 vf = w_vf(w);
+    s |= (u64)(vf == NILV ? 0u : vf == i ? 1u : 2u) << 6;
+    const u32 vr = w_vr<S>(w), vg = w_vg<S>(w);
+    s |= ((u64)__builtin_popcount(vr) << 28) | ((u64)__builtin_popcount(vg) << 31) |
+         ((u64)((vr >> i) & 1u) << 34) | ((u64)((vg >> i) & 1u) << 35);
+    u32 selfp = 0, others = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+        const u32 pr = (bits(w, SL<S>::NI + 2 * j, 2) << 2) | bits(w, SL<S>::MI + 2 * j, 2);
+        if ((u32)j == i) selfp = pr;
+        else others += (pr + 1u) * (pr + 7u);
+    }
+    return s | ((u64)selfp << 36) | ((u64)(others & 0xFFFFu) << 40);
+}
+// Signature, part 2: the messages a server sends and receives, ids masked,
+// summed order-free.
+RMC_HD u32 sig_src(u32 sl) { return (sl & ~0xFCu) * 0x9E3779B1u + 0x7F4A7C15u; }
+RMC_HD u32 sig_dst(u32 sl) { return (sl & ~0xFCu) * 0x85EBCA77u + 0xC2B2AE3Du; }
+template <int S, int K1>
+RMC_HD void signatures(const u64 (&base)[S], const u32 (&m)[K1], u64 (&sig)[S]) {
+    u32 ms[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) ms[i] = 0;
+#pragma unroll
+    for (int q = 0; q < K1; ++q) {
+        const u32 sl = m[q];
+        const u32 a = sl ? sig_src(sl) : 0u, b = sl ? sig_dst(sl) : 0u;
+        const u32 src = m_src(sl), dst = m_dst(sl);
+#pragma unroll
+        for (int i = 0; i < S; ++i) ms[i] += (src == (u32)i ? a : 0u) + (dst == (u32)i ? b : 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) sig[i] = base[i] + ((u64)ms[i] << 29);
+}
+// Fingerprint of pi(s) (any slot order; empty slots are 0).
+template <int S, int K1>
+RMC_HD u64 fp_perm(const u64 (&w)[S], const u32 (&m)[K1], u32 code) {
+    u64 h = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) h += hS(perm_word<S>(w[i], code), pe(code, (u32)i));
+#pragma unroll
+    for (int q = 0; q < K1; ++q) h += hM(perm_slot(m[q], code));
+    return h;
+}
+// A state passed by value (out-of-line calls keep their registers apart).
+template <int S, int K1>
+struct SymState {
+    u64 w[S];
+    u32 m[K1];
+};
+// Ties (rare): the least fingerprint over every order of the tied servers,
+// i.e. over the permutations whose position for server i lies in
+// [lo_i, lo_i + tc_i) (3 bits per server in lo / tc).  Out of line: the
+// common untied path stays small.
+template <int S, int K1>
+RMC_HD u64 canon_ties(const SymState<S, K1> t, u32 lo, u32 tc, const u32* codes, int np) {
+    u64 best = ~0ull;
+    for (int p = 0; p < np; ++p) {
+        const u32 c = codes[p];
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const u32 pos = pe(c, (u32)i), l = pe(lo, (u32)i);
+            ok &= pos >= l && pos < l + pe(tc, (u32)i);
+        }
+        if (ok) {
+            const u64 h = fp_perm<S, K1>(t.w, t.m, c);
+            best = h < best ? h : best;
+        }
+    }
+    return best;
+}
+// codes: every permutation of 0..S-1 (np = S!), for the tied case.  With
+// NOTIE the tied case is not resolved here: *tied is set and 0 returned (the
+// single-GPU SYMMETRY kernel defers those lanes to k_ties, so its hot loop
+// carries no permutation enumeration).
+template <int S, int K1, bool NOTIE = false>
+RMC_HD u64 canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const u64 (&sig)[S], const u32* codes, int np,
+                        int* tied = nullptr) {
+    u32 lo = 0, tc = 0;
+    bool tie = false;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        u32 l = 0, n = 0;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            l += sig[j] < sig[i] ? 1u : 0u;
+            n += sig[j] == sig[i] ? 1u : 0u;
+        }
+        lo |= l << (3 * i);
+        tc |= n << (3 * i);
+        tie |= n > 1;
+    }
+    if (!tie) return fp_perm<S, K1>(w, m, lo);  // the sorting permutation: server i -> its rank
+    if constexpr (NOTIE) {
+        *tied = 1;
+        return 0;
+    }
+    SymState<S, K1> t;
+#pragma unroll
+    for (int i = 0; i < S; ++i) t.w[i] = w[i];
+#pragma unroll
+    for (int q = 0; q < K1; ++q) t.m[q] = m[q];
+    return canon_ties<S, K1>(t, lo, tc, codes, np);
+}
+// The canonical key of a stored (materialised) state.
+template <int S, int K>
+RMC_HD u64 canon_state(const u64 (&w)[S], const u32 (&m)[K], const u32* codes, int np) {
+    u64 base[S], sig[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) base[i] = sig_base<S>(w[i], (u32)i);
+    signatures<S, K>(base, m, sig);
+    return canon_sorted<S, K>(w, m, sig, codes, np);
+}
+// The canonical key of the successor a delta makes of (w, m): the successor's
+// words and slots (unsorted: fingerprints are order-free), the parent's
+// signature bases reused for the servers the delta leaves alone.
+template <int S, int K, bool NOTIE = false>
+RMC_HD u64 canon_delta(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], const Delta& d, const u32* codes,
+                       int np, int* tied = nullptr) {
+    u64 ws[S], bs[S], sig[S];
+    u32 ms[K + 1];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        ws[i] = d.srv == i ? d.w_new : w[i];
+        bs[i] = d.srv == i ? sig_base<S>(d.w_new, (u32)i) : base[i];
+    }
+    int found = -1;
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        u32 sl = m[q];
+        if (q == d.rm) sl = m_cnt(sl) > 1 ? sl - CNT_ONE : 0u;
+        ms[q] = sl;
+        found = (d.has_add && sl && (sl & MSG_MASK) == d.add) ? q : found;
+    }
+    ms[K] = 0;
+    if (d.has_add) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) ms[q] += q == found ? CNT_ONE : 0u;
+        ms[K] = found < 0 ? (d.add | CNT_ONE) : 0u;
+    }
+    signatures<S, K + 1>(bs, ms, sig);
+    return canon_sorted<S, K + 1, NOTIE>(ws, ms, sig, codes, np, tied);
 }
 
 }  // namespace rmc

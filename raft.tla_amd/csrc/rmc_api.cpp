@@ -40,11 +40,7 @@ int validate(const rmc_config* c, std::string* why) {
     if (c->max_log_len < 0 || c->max_log_len > RMC_MAX_LOG) return bad("max_log_len must be 0..3");
     if (c->max_msgs < 0 || c->max_msgs > RMC_MAX_MSGS) return bad("max_msgs must be 0..8");
     if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
-    if ((c->flags & RMC_FLAG_SYMMETRY) && c->n_servers > 4)
-        return bad("SYMMETRY is supported for up to 4 servers");
     if (c->invariants & ~1023u) return bad("unknown invariant bit");
-    if ((c->flags & RMC_FLAG_VERIFY_STATES) && (c->flags & RMC_FLAG_SYMMETRY))
-        return bad("full-state verification is not supported with SYMMETRY");
     return 0;
 }
 
@@ -69,17 +65,18 @@ void fill_params(rmc_ctx* c) {
     const int sizes[10] = {S, S, S * S, S, S * VMAX, S, S * S, K, K, K};  // = Lanes<S,K>
     P.off[0] = 0;
     for (int f = 0; f < 10; ++f) P.off[f + 1] = P.off[f] + sizes[f];
-    // permutations of 0..S-1 in lexicographic order (identity first)
+    // permutations of 0..S-1 in lexicographic order (identity first), 3 bits per id
     memset(&c->PT, 0, sizeof c->PT);
-    if (S <= 4) {
-        int a[4] = {0, 1, 2, 3};
+    {
+        int a[5] = {0, 1, 2, 3, 4};
         int n = 0;
         do {
             u32 code = 0;
-            for (int i = 0; i < 4; ++i) code |= (u32)a[i] << (2 * i);
+            for (int i = 0; i < S; ++i) code |= (u32)a[i] << (3 * i);
             c->PT.code[n] = code;
             ++n;
         } while (std::next_permutation(a, a + S));
+        c->PT.np = n;
     }
 }
 
@@ -351,6 +348,13 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         return bail(RMC_E_NOMEM);
     }
     memset(c->h_ctr, 0, sizeof(Counters));
+    if (c->sh.sym) {  // successors with tied signatures, canonicalised by k_ties after each launch
+        c->B.tie_cap = 1ull << 25;
+        if (hipMalloc(&c->B.ties, c->B.tie_cap * 8) != hipSuccess) {
+            c->err = "device allocation failed (symmetry tie buffer)";
+            return bail(RMC_E_NOMEM);
+        }
+    }
     if (c->sh.verify) {  // slot -> store index (8 B per slot) + deferred-hit buffer (16 B per record)
         c->B.vcap = 1ull << 26;
         if (hipMalloc(&c->B.sidx, slots * 8) != hipSuccess || hipMalloc(&c->B.vbuf, c->B.vcap * 16) != hipSuccess) {
@@ -377,6 +381,7 @@ void rmc_destroy(rmc_ctx* c) {
     free_dist(c);
     (void)hipFree(c->B.sidx);
     (void)hipFree(c->B.vbuf);
+    (void)hipFree(c->B.ties);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -443,11 +448,17 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, hipEventRecord(c->ev0, c->st));
         // verification mode: smaller launches, each followed by publishing its
         // new states (k_publish) and checking its deferred hits (k_verify)
-        const u64 chunk = c->sh.verify ? (1ull << 20) : CHUNK;
+        // SYMMETRY: at most 2^24 states per launch, so the tied successors it
+        // defers (~1 % of lanes) fit the tie buffer
+        const u64 chunk = c->sh.verify ? (1ull << 20) : c->sh.sym ? (1ull << 24) : CHUNK;
         for (u64 a = lo; a < hi; a += chunk) {
             const u64 b = std::min(hi, a + chunk);
             HIPCHK(c, launch(c->sh, 0, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
             c->res.expand_launches += 1;
+            if (c->sh.sym && !c->sh.verify) {
+                HIPCHK(c, launch(c->sh, 10, c->P, c->PT, c->B, 0, 0, nullptr, nullptr, 0, nullptr, c->st));
+                HIPCHK(c, hipMemsetAsync(&c->B.ctr->nties, 0, 8, c->st));
+            }
             if (c->sh.verify) {
                 const u64 before = c->h_ctr->count;
                 if (int rc = read_counters(c)) return rc;
@@ -468,6 +479,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         const Counters& k = *c->h_ctr;
         if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
         if (k.overflow & 4u) return fail(c, RMC_E_CAPACITY, "verification buffer full");
+        if (k.overflow & 16u) return fail(c, RMC_E_CAPACITY, "symmetry tie buffer full");
         if (k.overflow & 8u) return fail(c, RMC_E_HIP, "verification: a stored state has no fingerprint slot");
         c->res.collisions += k.collisions;
         c->res.verified += k.vchecked;

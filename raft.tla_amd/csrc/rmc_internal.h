@@ -20,6 +20,7 @@ struct Counters {
     u64 collisions; // fingerprint hits whose stored state differs from the successor
     u64 vchecked;   // fingerprint hits compared state against state
     u64 vcount;     // deferred hits in vbuf (stored twin not yet published)
+    u64 nties;      // SYMMETRY: successors with tied signatures deferred to k_ties
 };
 
 struct DevBufs {
@@ -50,16 +51,21 @@ struct DevBufs {
     u64* sidx;
     u64* vbuf;
     u64 vcap;                  // records in vbuf
+    // SYMMETRY: successors whose server signatures tie, {parent index | lane << 56},
+    // canonicalised by k_ties after each expansion launch
+    u64* ties;
+    u64 tie_cap;
 };
 
 struct PermTable {
-    u32 code[24];  // server permutations (old id -> new id), 2 bits per id, S <= 4
+    u32 code[120];  // every server permutation (old id -> new id), 3 bits per id, S <= 5
+    int np;         // S!
 };
 
 struct Shape {
     int S, K;
     bool sym;
-    bool verify;  // full-state verification (no symmetry, single GPU)
+    bool verify;  // full-state verification (single GPU)
 };
 
 // which: 0 = k_expand over store[a, b); 1 = k_seed of `a` staged states `in`;
@@ -67,6 +73,7 @@ struct Shape {
 //        3 = sharded k_expand over store[a, b) (outbox in B);
 //        8 = k_materialize_remote of window [b, b + a) of each destination's keys, in = replies;
 //        9 = k_store_remote of `a` received state records `in`;
+//       10 = k_ties over the deferred tied successors (count on the device);
 //        5 = k_publish over store[a, b) (verification: slot -> store index);
 //        6 = k_verify of `a` deferred hits in B.vbuf;
 //        7 = k_rehash of the stored states [a, b) (recovery).

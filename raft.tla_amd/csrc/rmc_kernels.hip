@@ -105,58 +105,6 @@ __device__ __forceinline__ void store_state(u32* __restrict__ base, const u64 (&
     for (int q = 0; q < K; ++q) base[2 * S + q] = m[q];
 }
 
-// Fingerprints of every server permutation of a full state.
-template <int S, int K, int NP>
-__device__ __forceinline__ void perm_fps(const u64 (&w)[S], const u32 (&m)[K], const PermTable& PT, u64 (&hp)[NP]) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const u32 pm = PT.code[p];
-        u64 h = 0;
-#pragma unroll
-        for (int i = 0; i < S; ++i) h += hS(perm_word<S>(w[i], pm), pe(pm, (u32)i));
-#pragma unroll
-        for (int q = 0; q < K; ++q) h += hM(perm_slot(m[q], pm));
-        hp[p] = h;
-    }
-}
-
-// Canonical key of a successor under SYMMETRY Permutations(Server): the least
-// permuted fingerprint, computed incrementally from the parent's per-permutation
-// fingerprints (the delta touches one server word and <= 2 bag slots).
-template <int S, int K, int NP>
-__device__ __forceinline__ u64 canon_key(const u64 (&w)[S], const u32 (&m)[K], const u64 (&hp)[NP],
-                                         const Delta& d, const PermTable& PT) {
-    u64 best = ~0ull;
-    const u64 wo = d.srv >= 0 ? selw<S>(w, d.srv) : 0ull;
-    u32 rm_old = 0, rm_new = 0, add_old = 0, add_new = 0;
-    if (d.rm >= 0) {
-        rm_old = selm<K>(m, d.rm);
-        rm_new = m_cnt(rm_old) > 1 ? rm_old - CNT_ONE : 0u;
-    }
-    if (d.has_add) {
-        int found = -1;
-#pragma unroll
-        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
-        add_old = found >= 0 ? selm<K>(m, found) : 0u;
-        add_new = found >= 0 ? add_old + CNT_ONE : (d.add | CNT_ONE);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const u32 pm = PT.code[p];
-        u64 h = hp[p];
-        if (d.srv >= 0 && d.w_new != wo) {
-            const u32 ps = pe(pm, (u32)d.srv);
-            h += hS(perm_word<S>(d.w_new, pm), ps) - hS(perm_word<S>(wo, pm), ps);
-        }
-        if (d.rm >= 0) h += hM(perm_slot(rm_new, pm)) - hM(perm_slot(rm_old, pm));
-        if (d.has_add) h += hM(perm_slot(add_new, pm)) - hM(perm_slot(add_old, pm));
-        best = h < best ? h : best;
-    }
-    return best;
-}
-
-template <int S> struct NPerm { static constexpr int v = S == 1 ? 1 : S == 2 ? 2 : S == 3 ? 6 : 24; };
-
 // Wave-aggregated allocation of store slots for the lanes with is_new set,
 // then materialise + store + parent + invariants.  Must be reached by every
 // lane of the wave (it contains a ballot).
@@ -255,23 +203,62 @@ __device__ __forceinline__ bool same_state(const u64 (&w)[S], const u32 (&m)[K],
     return eq;
 }
 
+// SYMMETRY: the successor and the stored state are the same orbit iff some
+// server permutation maps one onto the other (bag re-sorted after permuting).
+template <int S, int K>
+__device__ __noinline__ bool same_orbit(const PackedState<S, K> a, const u32* __restrict__ st, const PermTable& PT) {
+    u64 w2[S];
+    u32 m2[K];
+    load_state<S, K>(st, w2, m2);
+    for (int p = 0; p < PT.np; ++p) {
+        const u32 c = PT.code[p];
+        u64 wp[S];
+        u32 mp[K];
+#pragma unroll
+        for (int t = 0; t < S; ++t) {
+            u64 v = 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) v |= pe(c, (u32)i) == (u32)t ? perm_word<S>(a.w[i], c) : 0ull;
+            wp[t] = v;
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q) mp[q] = perm_slot(a.m[q], c);
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+#pragma unroll
+            for (int q = (r & 1); q + 1 < K; q += 2) {
+                const u32 x = mp[q], y = mp[q + 1];
+                mp[q] = x > y ? x : y;
+                mp[q + 1] = x > y ? y : x;
+            }
+        }
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < S; ++i) eq &= wp[i] == w2[i];
+#pragma unroll
+        for (int q = 0; q < K; ++q) eq &= mp[q] == m2[q];
+        if (eq) return true;
+    }
+    return false;
+}
+
 // Check one fingerprint hit: 0 = the stored state equals the successor,
 // 1 = it differs (a collision), 2 = the owner is not published yet (defer),
 // 3 = no slot (table full, flagged by the insert).  Counting and deferral are
 // aggregated by the caller (one atomic per wave, not per hit).
-template <int S, int K>
+template <int S, int K, bool SYM>
 __device__ __forceinline__ int verify_hit(const u64 (&w)[S], const u32 (&m)[K], int lane, u64 slot, const Params& P,
-                                       const DevBufs& B) {
+                                       const PermTable& PT, const DevBufs& B) {
     constexpr int NW = 2 * S + K;
     if (slot == ~0ull) return 3;
     const u64 ix = B.sidx[slot];
     if (ix == ~0ull) return 2;  // owner found in this launch: check after it
     Delta d;
     lane_delta<S, K>(w, m, lane, P, d);
-    u64 wo[S];
-    u32 mo[K];
-    materialise<S, K>(w, m, d, wo, mo);
-    return same_state<S, K>(wo, mo, B.store + ix * (u64)NW) ? 0 : 1;
+    PackedState<S, K> o;
+    materialise<S, K>(w, m, d, o.w, o.m);
+    if constexpr (SYM) return same_orbit<S, K>(o, B.store + ix * (u64)NW, PT) ? 0 : 1;
+    return same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW) ? 0 : 1;
 }
 
 __device__ __forceinline__ u64 wave_sum64(u64 v) {
@@ -281,21 +268,21 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
     return v;
 }
 
-template <int S, int K>
-__device__ __forceinline__ u64 verify_key(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
-    const u64 k = state_fp<S, K>(w, m) & P.fp_mask;
+template <int S, int K, bool SYM>
+__device__ __forceinline__ u64 verify_key(const u64 (&w)[S], const u32 (&m)[K], const Params& P, const PermTable& PT) {
+    const u64 k = (SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m)) & P.fp_mask;
     return k ? k : 1ull;
 }
 
 // sidx[slot of state i's fingerprint] = i for the stored states [lo, hi).
-template <int S, int K>
-__global__ __launch_bounds__(256) void k_publish(const Params P, const DevBufs B, u64 lo, u64 hi) {
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_publish(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u64 w[S];
         u32 m[K];
         load_state<S, K>(B.store + i * (u64)NW, w, m);
-        const u64 key = verify_key<S, K>(w, m, P);
+        const u64 key = verify_key<S, K, SYM>(w, m, P, PT);
         u64 s = key & B.tmask;
         u64 n = 0;
         while (B.table[s] != key && n <= B.tmask) { s = (s + 1) & B.tmask; ++n; }
@@ -305,8 +292,8 @@ __global__ __launch_bounds__(256) void k_publish(const Params P, const DevBufs B
 }
 
 // The deferred hits of the last launch, now that their owners are published.
-template <int S, int K>
-__global__ __launch_bounds__(256) void k_verify(const Params P, const DevBufs B, u64 n) {
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable PT, const DevBufs B, u64 n) {
     constexpr int NW = 2 * S + K;
     u64 vchk = 0, vcol = 0;
     for (u64 q = (u64)blockIdx.x * 256ull + threadIdx.x; q < n; q += (u64)gridDim.x * 256ull) {
@@ -318,16 +305,18 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const DevBufs B,
         load_state<S, K>(B.store + parent * (u64)NW, w, m);
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);
-        u64 wo[S];
-        u32 mo[K];
-        materialise<S, K>(w, m, d, wo, mo);
+        PackedState<S, K> o;
+        materialise<S, K>(w, m, d, o.w, o.m);
         const u64 ix = B.sidx[slot];
         if (ix == ~0ull) {
             atomicOr(&B.ctr->overflow, 8u);
             continue;
         }
         ++vchk;
-        vcol += same_state<S, K>(wo, mo, B.store + ix * (u64)NW) ? 0u : 1u;
+        bool same;
+        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)NW, PT);
+        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW);
+        vcol += same ? 0u : 1u;
     }
     vchk = wave_sum64(vchk);
     vcol = wave_sum64(vcol);
@@ -450,7 +439,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
-    constexpr int NP = SYM ? NPerm<S>::v : 1;
+    constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
@@ -495,11 +484,17 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         } else {
             h0 = state_fp<S, K>(w, m);
         }
-        u64 hp[NP];
-        if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
+        // SYMMETRY: the parent's signature bases (reused by every lane)
+        u64 sbase[SYM ? S : 1];
+        if constexpr (SYM) {
+#pragma unroll
+            for (int i = 0; i < S; ++i) sbase[i] = sig_base<S>(w[i], (u32)i);
+        }
         u32 g = 0;
         for (int lane0 = 0; lane0 < nl; lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
+            // Rolled under SYMMETRY: one copy of the canonicalisation in flight.
+#pragma unroll(SYM ? 1 : BATCH)
             for (int b = 0; b < BATCH; ++b) {
                 const int lane = lane0 + b;
                 u64 key = 0;
@@ -510,13 +505,30 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     g += (u32)en;
                     u64 h = 0;
                     int in_model = 0;
-                    if (en) {
+                    if constexpr (SYM) {
+                        // a stutter (successor = parent: no bag change, no word change) is never probed
+                        const bool stutter = d.rm < 0 && !d.has_add && (d.srv < 0 || d.w_new == selw<S>(w, d.srv));
+                        if (en && !stutter && delta_in_model<S, K>(m, d, P)) {
+                            in_model = 1;
+                            if constexpr (TIEDEFER) {  // tied signatures: k_ties canonicalises it after this launch
+                                int tied = 0;
+                                h = canon_delta<S, K, true>(w, m, sbase, d, PT.code, PT.np, &tied);
+                                if (tied) {
+                                    in_model = 0;
+                                    const u64 q = atomicAdd((unsigned long long*)&B.ctr->nties, 1ull);
+                                    if (q < B.tie_cap) B.ties[q] = (lo + rel) | ((u64)lane << 56);
+                                    else atomicOr(&B.ctr->overflow, 16u);
+                                }
+                            } else {
+                                h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
+                            }
+                        }
+                    } else if (en) {
                         if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h);
                         else in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
                     }
-                    if (in_model && h != h0) {
+                    if (in_model && (SYM || h != h0)) {
                         key = h;
-                        if constexpr (SYM) key = canon_key<S, K, NP>(w, m, hp, d, PT);
                         if constexpr (VERIFY) key &= P.fp_mask;
                         key = key ? key : 1ull;
                         if constexpr (DIST) s_own[b][threadIdx.x] = (uint8_t)owner_succ<S>(key, d, w, B);
@@ -591,7 +603,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 u32 defbits = 0;
                 for (int b = 0; b < BATCH; ++b) {  // rolled: one inlined copy of the check
                     if (!((hitbits >> b) & 1u)) continue;
-                    const int r = verify_hit<S, K>(w, m, lane0 + b, s_key[b][threadIdx.x], P, B);
+                    const int r = verify_hit<S, K, SYM>(w, m, lane0 + b, s_key[b][threadIdx.x], P, PT, B);
                     vchk += (u64)(r <= 1);
                     vcol += (u64)(r == 1);
                     defbits |= (u32)(r == 2) << b;
@@ -673,18 +685,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     expand_body<S, K, false, BATCH, false, false, true>(P, PT, B, lo, hi);
 }
 
-// SYMMETRY expansion (canonicalisation over the S! server permutations): 205
-// VGPRs for S = 3 unconstrained, i.e. 2 waves/SIMD to hide the fingerprint-set
-// latency.  RMC_SYM_WPE caps the register budget of the S = 3, K = 4 variant
-// (config 2; 48 B of spills); the others spill heavily under the cap and stay
-// uncapped.  0 = no cap.
-#ifndef RMC_SYM_WPE
-#define RMC_SYM_WPE 3
-#endif
+// SYMMETRY expansion: each lane fingerprints its successor under the
+// permutation that sorts the servers by signature (canon_delta), all S! only
+// on ties.
 template <int S, int K, int BATCH>
-__global__ __launch_bounds__(256) __attribute__((
-    amdgpu_waves_per_eu((S == 3 && K == 4 && RMC_SYM_WPE) ? RMC_SYM_WPE : 1))) void
-k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? 5 : 1))) void k_expand_sym(
+    const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     expand_body<S, K, true, BATCH, false, false>(P, PT, B, lo, hi);
 }
 
@@ -780,6 +786,48 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
     }
 }
 
+// SYMMETRY, single GPU: the successors k_expand_sym deferred because their
+// server signatures tie.  Each is re-derived from its parent, canonicalised
+// over every order of the tied servers, inserted, and committed if new.
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_ties(const Params P, const PermTable PT, const DevBufs B) {
+    constexpr int NW = 2 * S + K;
+    const u64 n = B.ctr->nties < B.tie_cap ? B.ctr->nties : B.tie_cap;
+    u64 pr = 0;
+    for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {  // wave-uniform
+        const u64 t = t0 + threadIdx.x;
+        const bool live = t < n;
+        u64 w[S];
+        u32 m[K];
+        u64 pidx = 0;
+        int lane = 0;
+        Delta d;
+        int is_new = 0;
+        if (live) {
+            const u64 rec = B.ties[t];
+            pidx = rec & ((1ull << 56) - 1);
+            lane = (int)(rec >> 56);
+            load_state<S, K>(B.store + pidx * (u64)NW, w, m);
+            lane_delta<S, K>(w, m, lane, P, d);
+            u64 base[S];
+#pragma unroll
+            for (int i = 0; i < S; ++i) base[i] = sig_base<S>(w[i], (u32)i);
+            u64 key = canon_delta<S, K>(w, m, base, d, PT.code, PT.np);
+            key = key ? key : 1ull;
+            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        } else {
+#pragma unroll
+            for (int i = 0; i < S; ++i) w[i] = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) m[q] = 0;
+            d.srv = -1; d.rm = -1; d.has_add = 0; d.add = 0; d.en = 0; d.w_new = 0;
+        }
+        pr += (u64)__popcll(__ballot(live));
+        commit_new<S, K>(is_new, w, m, d, P, B, B.ref_tag | pidx, lane);
+    }
+    if (__lane_id() == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+}
+
 // Probe-rate microbenchmark (the roofline ceiling for k_expand): every thread
 // issues `iters` rounds of BATCH independent random 8-byte accesses into a
 // table of `mask + 1` slots — plain loads (mode 0) or CAS (mode 1) — the
@@ -821,7 +869,6 @@ template <int S, int K, bool SYM>
 __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT, const DevBufs B, const u32* staged,
                                               u64 n) {
     constexpr int NW = 2 * S + K;
-    constexpr int NP = SYM ? NPerm<S>::v : 1;
     const u64 t = (u64)blockIdx.x * 256ull + threadIdx.x;
     const bool live = t < n;
     u64 w[S];
@@ -836,14 +883,7 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
     }
     int is_new = 0;
     if (live) {
-        u64 key = state_fp<S, K>(w, m);
-        if constexpr (SYM) {
-            u64 hp[NP];
-            perm_fps<S, K, NP>(w, m, PT, hp);
-            key = ~0ull;
-#pragma unroll
-            for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
-        }
+        u64 key = SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m);
         key &= P.fp_mask;  // ~0 unless a verification test weakens the fingerprint
         key = key ? key : 1ull;
         // sharded mode: only the owner of an initial state stores it
@@ -859,19 +899,11 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
 template <int S, int K, bool SYM>
 __global__ __launch_bounds__(256) void k_rehash(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
-    constexpr int NP = SYM ? NPerm<S>::v : 1;
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u64 w[S];
         u32 m[K];
         load_state<S, K>(B.store + i * (u64)NW, w, m);
-        u64 key = state_fp<S, K>(w, m);
-        if constexpr (SYM) {
-            u64 hp[NP];
-            perm_fps<S, K, NP>(w, m, PT, hp);
-            key = ~0ull;
-#pragma unroll
-            for (int p = 0; p < NP; ++p) key = hp[p] < key ? hp[p] : key;
-        }
+        u64 key = SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m);
         key &= P.fp_mask;
         key = key ? key : 1ull;
         if (!fp_insert(B.table, B.tmask, key, &B.ctr->table_full)) atomicOr(&B.ctr->overflow, 8u);  // duplicate
@@ -883,7 +915,6 @@ template <int S, int K, bool SYM>
 __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT, const u32* in, u64 n, u32* out,
                                               u64 cap, unsigned long long* count) {
     constexpr int NW = 2 * S + K;
-    constexpr int NP = SYM ? NPerm<S>::v : 1;
     constexpr int RW = 6 + NW;  // record: parent(2) lane(1) flags(1) fp(2) + state
     const u64 t = (u64)blockIdx.x * 256ull + threadIdx.x;
     if (t >= n) return;
@@ -891,8 +922,9 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
     u32 m[K];
     load_state<S, K>(in + t * (u64)NW, w, m);
     const u64 h0 = state_fp<S, K>(w, m);
-    u64 hp[NP];
-    if constexpr (SYM) perm_fps<S, K, NP>(w, m, PT, hp);
+    u64 sbase[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) sbase[i] = sig_base<S>(w[i], (u32)i);
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
 #pragma unroll 1
     for (int lane = 0; lane < nl; ++lane) {
@@ -902,7 +934,7 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
         u64 h = 0;
         const int in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
         if (in_model) {
-            if constexpr (SYM) h = canon_key<S, K, NP>(w, m, hp, d, PT);
+            if constexpr (SYM) h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
         }
         const u64 o = atomicAdd(count, 1ull);
         if (o >= cap) continue;
@@ -1047,7 +1079,7 @@ template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, bool verify, const Params& P, const PermTable& PT, const DevBufs& B, u64 a,
                            u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
     const u64 n = (which == 0 || which == 3 || which == 5 || which == 7) ? (b - a)
-                : which == 8 ? a * (u64)B.world : a;
+                : which == 8 ? a * (u64)B.world : which == 10 ? 1 : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
@@ -1055,8 +1087,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
     if (which == 0) {
         if constexpr (SYM) {
-            if (verify) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((k_expand_sym<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+            if (verify)
+                hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+                                   PT, B, a, b);
+            else
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         } else if (verify) {
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
@@ -1079,12 +1114,14 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                            reinterpret_cast<const uint8_t*>(in), a, b);
     } else if (which == 9) {
         hipLaunchKernelGGL((k_store_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, in, a);
+    } else if (which == 10) {
+        if constexpr (SYM) hipLaunchKernelGGL((k_ties<S, K>), dim3(1024), dim3(256), 0, st, P, PT, B);
     } else if (which == 5) {
-        hipLaunchKernelGGL((k_publish<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
+        hipLaunchKernelGGL((k_publish<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 7) {
         hipLaunchKernelGGL((k_rehash<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 6) {
-        hipLaunchKernelGGL((k_verify<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a);
+        hipLaunchKernelGGL((k_verify<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a);
     } else if (which == 1) {
         hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
     } else {
@@ -1098,11 +1135,7 @@ template <int S, int K>
 static hipError_t launch_sk(bool sym, bool verify, int which, const Params& P, const PermTable& PT, const DevBufs& B,
                             u64 a, u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count,
                             hipStream_t st) {
-    if constexpr (S <= 4) {
-        if (sym) return launch_t<S, K, true>(which, verify, P, PT, B, a, b, in, out, cap, count, st);
-    } else {
-        if (sym) return hipErrorInvalidValue;
-    }
+    if (sym) return launch_t<S, K, true>(which, verify, P, PT, B, a, b, in, out, cap, count, st);
     return launch_t<S, K, false>(which, verify, P, PT, B, a, b, in, out, cap, count, st);
 }
 

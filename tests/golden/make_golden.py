@@ -54,6 +54,10 @@ CONFIGS = {
     "bug_quorum_log": (3, 2, 2, 1, 1, 1, 1, 128, 0, 0),
     "bug_more_up_to_date": (3, 2, 2, 1, 1, 1, 1, 256, 0, 0),
     "bug_leader_complete": (3, 2, 2, 1, 1, 1, 1, 512, 0, 0),
+    # SYMMETRY Permutations(Server) with 4 and 5 servers (signature-sorted canonical keys)
+    "s4_sym_prefix16": (4, 1, 2, 1, 2, 1, 0, 1, 1, 16),
+    "s5_sym_prefix16": (5, 2, 2, 1, 2, 1, 0, 1, 1, 16),
+    "sym_bug_one_leader": (3, 2, 3, 1, 3, 1, 1, 2, 1, 0),
     # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
     "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }

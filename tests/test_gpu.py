@@ -51,7 +51,7 @@ def test_kat_first_levels():
 
 BFS_CASES = ["bounded_full", "tiny2", "messages_tiny2", "elections_small", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
              "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9", "isprefix_small",
-             "isprefix_s3v1_log2"]
+             "isprefix_s3v1_log2", "s4_sym_prefix16", "s5_sym_prefix16"]
 
 
 @pytest.mark.parametrize("name", BFS_CASES)
@@ -77,7 +77,8 @@ def test_fingerprint_salt_does_not_change_counts():
     assert levels == g["level_new"]
 
 
-@pytest.mark.parametrize("name", ["small", "s5_prefix9", "bug_log_matching", "bounded_full"])
+@pytest.mark.parametrize("name", ["small", "s5_prefix9", "bug_log_matching", "bounded_full", "small_sym",
+                                  "s4_sym_prefix16", "sym_bug_one_leader"])
 def test_full_state_verification_is_exact(name):
     """RMC_FLAG_VERIFY_STATES: every fingerprint hit is compared with the stored
     state; with 64-bit fingerprints no hit differs, so the counts are certified
@@ -94,12 +95,13 @@ def test_full_state_verification_is_exact(name):
     assert res.verified == res.probes - (res.distinct - 1)
 
 
-@pytest.mark.parametrize("bits", [16, 20])
-def test_full_state_verification_reports_collisions(bits):
-    """A fingerprint cut to `bits` bits must collide on a 2.5 M-state model: the
-    search loses states (as TLC would, silently) and the verification reports
-    the colliding hits."""
-    g = GOLDEN["small"]
+@pytest.mark.parametrize("bits,name", [(16, "small"), (20, "small"), (14, "small_sym")])
+def test_full_state_verification_reports_collisions(bits, name):
+    """A fingerprint cut to `bits` bits must collide: the search loses states
+    (as TLC would, silently) and the verification reports the colliding hits;
+    under SYMMETRY a hit is a collision when no server permutation maps the
+    successor onto the stored state."""
+    g = GOLDEN[name]
     cfg = cfg_from(g["params"], capacity=1 << 22)
     cfg.flags |= rmc.FLAG_VERIFY_STATES
     with rmc.Checker(cfg) as ck:
@@ -111,7 +113,7 @@ def test_full_state_verification_reports_collisions(bits):
     assert res.verified == res.probes - (res.distinct - 1)
 
 
-@pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "bug_both", "bug_messages",
+@pytest.mark.parametrize("name", ["bug_one_leader", "sym_bug_one_leader", "bug_log_matching", "bug_both", "bug_messages",
                                   "messages_small", "bug_leader_votes", "bug_cand_term", "votes_granted_small",
                                   "bug_votes_granted", "bug_quorum_log", "bug_more_up_to_date",
                                   "bug_leader_complete"])
