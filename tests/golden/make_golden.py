@@ -58,6 +58,8 @@ CONFIGS = {
     "s4_sym_prefix16": (4, 1, 2, 1, 2, 1, 0, 1, 1, 16),
     "s5_sym_prefix16": (5, 2, 2, 1, 2, 1, 0, 1, 1, 16),
     "sym_bug_one_leader": (3, 2, 3, 1, 3, 1, 1, 2, 1, 0),
+    # config 3, wider bounds (specs/MCraft5Wide.cfg): the first 9 levels
+    "s5_wide_prefix9": (5, 2, 3, 2, 4, 1, 0, 1, 0, 9),
     # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
     "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }

@@ -52,7 +52,9 @@ def test_create_validates_config():
     ctx = C.c_void_p()
     bad = rmc.make_config(max_log_len=4)
     assert lib.rmc_create(C.byref(bad), C.byref(ctx)) == -22
-    bad = rmc.make_config(n_servers=5, symmetry=True)
+    bad = rmc.make_config(n_servers=6, symmetry=True)
+    assert lib.rmc_create(C.byref(bad), C.byref(ctx)) == -22
+    bad = rmc.make_config(invariants=1 << 10)
     assert lib.rmc_create(C.byref(bad), C.byref(ctx)) == -22
 
 

@@ -322,3 +322,34 @@ def test_cli_counterexample_is_tlc_format_and_replays(cfgname, golden, tmp_path)
     out = os.path.join(os.path.dirname(os.path.dirname(__file__)), "gpurun_out")
     if os.path.isdir(out):
         open(os.path.join(out, f"cli_{cfgname}.txt"), "w").write(r.stdout)
+
+
+@pytest.mark.parametrize("prefix,depth,at_least", [("s5_prefix9", 20, 1_348_000_000),
+                                                   ("s5_wide_prefix9", 14, 1_194_000_000)])
+def test_config3_full_size_is_exact_by_verification_and_salt(prefix, depth, at_least):
+    """BASELINE.json config 3 at full size: specs/MCraft5.cfg (5 servers) to BFS
+    depth 20, 1.35 G distinct states, and the wider-bound specs/MCraft5Wide.cfg
+    (MaxTerm 3, MaxLogLen 2, MaxMsgs 4) to depth 14, 1.19 G -- beyond the
+    oracles, so pinned by size-independent properties: (1) the first 9 levels
+    equal the oracle fixture level by level; (2) full-state verification
+    compares every fingerprint hit with the stored state and finds 0
+    collisions, so the count is exact; (3) another fingerprint salt gives the
+    same counts."""
+    g9 = GOLDEN[prefix]
+    p = dict(g9["params"], max_depth=depth)
+    cfg = cfg_from(p, capacity=0)
+    with rmc.Checker(cfg) as ck:
+        r1 = ck.run()
+        lv = [1] + [x[3] for x in ck.levels if x[3]]
+        ck.set_seed(0xFEED5)
+        r2 = ck.run()
+    assert r1.distinct > at_least and r1.depth == depth and r1.left_on_queue > 0
+    assert lv[:9] == g9["level_new"]
+    assert (r2.distinct, r2.generated, r2.depth, r2.left_on_queue) == \
+        (r1.distinct, r1.generated, r1.depth, r1.left_on_queue)
+    cfg.flags |= rmc.FLAG_VERIFY_STATES
+    with rmc.Checker(cfg) as ck:
+        r3 = ck.run()
+    assert (r3.distinct, r3.generated, r3.depth) == (r1.distinct, r1.generated, r1.depth)
+    assert r3.collisions == 0
+    assert r3.verified == r3.probes - (r3.distinct - 1)
