@@ -39,7 +39,7 @@ extern "C" {
 #define RMC_E_INVAL (-22)      /* config validation failed (TLC: semantic error) */
 #define RMC_E_NOMEM (-12)      /* device allocation failed */
 #define RMC_E_HIP (-5)         /* HIP runtime error */
-#define RMC_E_CAPACITY (-28)   /* fingerprint set / state store full (TLC spills to disk; we stop) */
+#define RMC_E_CAPACITY (-28)   /* fingerprint set full, or state store full without RMC_FLAG_SPILL */
 #define RMC_E_NOGPU (-19)      /* no usable gfx950 device */
 #define RMC_E_PARSE (-74)      /* .cfg / .tla front-end could not recognise the model */
 #define RMC_E_STATE (-71)      /* call out of order (e.g. rmc_trace before a violation) */
@@ -53,7 +53,15 @@ extern "C" {
 #define RMC_FLAG_VERIFY_STATES (1u << 3)   /* full-state verification: every fingerprint */
                                            /* hit is compared with the stored state;    */
                                            /* differences = collisions (no TLC analog;  */
-                                           /* single GPU, no SYMMETRY)                  */
+                                           /* single GPU)                               */
+#define RMC_FLAG_SPILL (1u << 4)           /* frontier spill (TLC's states/ directory): */
+                                           /* expanded levels move to pinned host memory */
+                                           /* when the device window fills, so a model  */
+                                           /* whose states outgrow HBM completes while  */
+                                           /* its fingerprints fit.  state_capacity then */
+                                           /* sizes the fingerprint set (all states),   */
+                                           /* device_window the resident states.  Single */
+                                           /* GPU; not with RMC_FLAG_VERIFY_STATES       */
 
 /* rmc_config.invariants — the INVARIANT names the engine knows (fused checks). */
 #define RMC_INV_TYPEOK (1u << 0)           /* raft.tla:482-492                          */
@@ -88,6 +96,8 @@ typedef struct rmc_config {
     uint64_t seed;            /* BFS: fingerprint salt (0 = default hash; two runs */
                               /* with different salts and equal counts rule out   */
                               /* fingerprint collisions); simulation: RNG seed     */
+    uint64_t device_window;   /* RMC_FLAG_SPILL: states resident on the device    */
+                              /* (frontier + the level being built); 0 = auto     */
 } rmc_config;
 
 /* End-of-run summary.  Replaces TLC's stdout summary lines:
@@ -116,6 +126,10 @@ typedef struct rmc_result {
     uint64_t chunks;           /* frontier chunks (exchange rounds)                        */
     double exchange_seconds;   /* wall time in collectives and count read-backs            */
     uint64_t stored_here;      /* distinct states this rank stores                         */
+    /* RMC_FLAG_SPILL */
+    uint64_t spilled;          /* states moved to host memory (all spills of the run)      */
+    uint64_t spills;           /* spill events                                              */
+    double spill_seconds;      /* wall time of the spills (device-to-host + window shift)   */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */

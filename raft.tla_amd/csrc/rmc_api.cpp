@@ -41,6 +41,9 @@ int validate(const rmc_config* c, std::string* why) {
     if (c->max_msgs < 0 || c->max_msgs > RMC_MAX_MSGS) return bad("max_msgs must be 0..8");
     if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
     if (c->invariants & ~1023u) return bad("unknown invariant bit");
+    if ((c->flags & RMC_FLAG_SPILL) && (c->flags & RMC_FLAG_VERIFY_STATES))
+        return bad("RMC_FLAG_SPILL does not combine with RMC_FLAG_VERIFY_STATES");
+    if (c->flags & ~31u) return bad("unknown flag bit");
     return 0;
 }
 
@@ -270,6 +273,96 @@ int read_counters(rmc_ctx* c) {
     return 0;
 }
 
+// ---- frontier spill (RMC_FLAG_SPILL) ---------------------------------------------
+// TLC writes its state queue to the states/ directory;
+// here the expanded levels move to pinned host memory.  Kernels index states by
+// their global index through device pointers biased by -base.
+void spill_rebase(rmc_ctx* c, u64 base) {
+    SpillState& X = c->spill;
+    X.base = base;
+    const uintptr_t nw = (uintptr_t)c->NW;
+    c->B.store = (u32*)((uintptr_t)X.store - (uintptr_t)base * nw * 4);
+    c->B.parent = (u64*)((uintptr_t)X.parent - (uintptr_t)base * 8);
+    c->B.act = (uint8_t*)((uintptr_t)X.act - (uintptr_t)base);
+    c->B.cap = base + X.win;
+}
+
+static void seg_free(SpillSeg& g) {
+    (void)hipHostFree(g.store);
+    (void)hipHostFree(g.parent);
+    (void)hipHostFree(g.act);
+    g = SpillSeg{};
+}
+
+void spill_free(rmc_ctx* c) {
+    for (auto& g : c->spill.segs) seg_free(g);
+    c->spill.segs.clear();
+}
+
+static int seg_alloc(rmc_ctx* c, SpillSeg* g, u64 first, u64 n) {
+    g->first = first;
+    g->n = n;
+    if (hipHostMalloc(&g->store, std::max<u64>(n, 1) * (u64)c->NW * 4, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&g->parent, std::max<u64>(n, 1) * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&g->act, std::max<u64>(n, 1), hipHostMallocDefault) != hipSuccess) {
+        seg_free(*g);
+        return fail(c, RMC_E_NOMEM, "spill: pinned host allocation of " + std::to_string(n) + " states failed");
+    }
+    return 0;
+}
+
+// Move the device-resident states [base, a) to a new host segment and shift
+// [a, count) to the start of the window.
+int spill_to(rmc_ctx* c, u64 a, u64 count) {
+    SpillState& X = c->spill;
+    const u64 n = a - X.base;
+    if (!n) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    const u64 W = (u64)c->NW * 4;
+    SpillSeg g;
+    if (int rc = seg_alloc(c, &g, X.base, n)) return rc;
+    X.segs.push_back(g);
+    HIPCHK(c, hipMemcpyAsync(g.store, X.store, n * W, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(g.parent, X.parent, n * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(g.act, X.act, n, hipMemcpyDeviceToHost, c->st));
+    // shift in pieces of at most n states: no piece overlaps its own destination,
+    // and stream order keeps every source read before a later piece overwrites it
+    const u64 m = count - a;
+    for (u64 off = 0; off < m; off += n) {
+        const u64 k = std::min(n, m - off);
+        HIPCHK(c, hipMemcpyAsync((char*)X.store + off * W, (char*)X.store + (n + off) * W, k * W,
+                                 hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipMemcpyAsync(X.parent + off, X.parent + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipMemcpyAsync(X.act + off, X.act + n + off, k, hipMemcpyDeviceToDevice, c->st));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    spill_rebase(c, a);
+    c->res.spilled += n;
+    c->res.spills += 1;
+    c->res.spill_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+// One stored state (any of state / parent / act may be null), wherever it lives.
+int read_stored(rmc_ctx* c, u64 idx, u32* state, u64* parent, uint8_t* act) {
+    const u64 W = (u64)c->NW * 4;
+    if (!c->spill.on || idx >= c->spill.base) {
+        if (state) HIPCHK(c, hipMemcpy(state, c->B.store + idx * (u64)c->NW, W, hipMemcpyDeviceToHost));
+        if (parent) HIPCHK(c, hipMemcpy(parent, c->B.parent + idx, 8, hipMemcpyDeviceToHost));
+        if (act) HIPCHK(c, hipMemcpy(act, c->B.act + idx, 1, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    for (const SpillSeg& g : c->spill.segs) {
+        if (idx < g.first || idx >= g.first + g.n) continue;
+        const u64 o = idx - g.first;
+        if (state) memcpy(state, (const char*)g.store + o * W, W);
+        if (parent) *parent = g.parent[o];
+        if (act) *act = g.act[o];
+        return 0;
+    }
+    return fail(c, RMC_E_STATE, "state " + std::to_string(idx) + " is in no spill segment");
+}
+
 }  // namespace rmc_host
 
 using namespace rmc_host;
@@ -321,28 +414,42 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
 
     // ---- capacity: state store + parents + lanes + fingerprint set (load <= 0.5)
     const u64 per_state = (u64)c->NW * 4 + 8 + 1;
+    const bool spill = (cfg->flags & RMC_FLAG_SPILL) != 0;
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    const u64 budget = (u64)((double)fr * 0.80);
     u64 cap = cfg->state_capacity;
     if (cap == 0) {
-        size_t fr = 0, tot = 0;
-        (void)hipMemGetInfo(&fr, &tot);
-        const u64 budget = (u64)((double)fr * 0.80);
-        // table <= 4 slots per state after pow2 rounding (+ as many sidx words when verifying)
-        cap = budget / (per_state + (c->sh.verify ? 64 : 32));
+        // table <= 4 slots per state after pow2 rounding (+ as many sidx words when verifying);
+        // spilling: the set takes 60 % of the budget, the device window the rest
+        cap = spill ? (u64)(budget * 0.6) / 32 : budget / (per_state + (c->sh.verify ? 64 : 32));
         cap = std::min<u64>(cap, 1ull << 36);
     }
     cap = std::max<u64>(cap, 1024);
     u64 slots = 1;
     while (slots < 2 * cap) slots <<= 1;
     c->table_slots = slots;
-    c->B.cap = cap;
+    u64 win = cap;  // states resident on the device
+    if (spill) {
+        win = cfg->device_window;
+        if (win == 0) win = (budget - std::min<u64>(budget, slots * 8)) / per_state;
+        win = std::max<u64>(std::min<u64>(win, cap), 1024);
+    }
+    c->B.cap = win;
     c->B.tmask = slots - 1;
-    if (hipMalloc(&c->B.store, cap * (u64)c->NW * 4) != hipSuccess ||
-        hipMalloc(&c->B.parent, cap * 8) != hipSuccess || hipMalloc(&c->B.act, cap) != hipSuccess ||
+    if (hipMalloc(&c->B.store, win * (u64)c->NW * 4) != hipSuccess ||
+        hipMalloc(&c->B.parent, win * 8) != hipSuccess || hipMalloc(&c->B.act, win) != hipSuccess ||
         hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
         hipMalloc(&c->d_staged, (size_t)c->NW * 4 * 64) != hipSuccess) {
-        c->err = "device allocation failed (capacity " + std::to_string(cap) + " states)";
+        c->err = "device allocation failed (capacity " + std::to_string(win) + " states)";
         return bail(RMC_E_NOMEM);
     }
+    c->spill.on = spill ? 1 : 0;
+    c->spill.win = win;
+    c->spill.total_cap = cap;
+    c->spill.store = c->B.store;
+    c->spill.parent = c->B.parent;
+    c->spill.act = c->B.act;
     if (hipHostMalloc(&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
         c->err = "pinned allocation failed";
         return bail(RMC_E_NOMEM);
@@ -372,9 +479,11 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
 void rmc_destroy(rmc_ctx* c) {
     if (!c) return;
     if (c->st) (void)hipStreamSynchronize(c->st);
-    (void)hipFree(c->B.store);
-    (void)hipFree(c->B.parent);
-    (void)hipFree(c->B.act);
+    spill_free(c);
+    // the unbiased allocations (B.* may be rebased by a spill)
+    (void)hipFree(c->spill.store ? c->spill.store : c->B.store);
+    (void)hipFree(c->spill.parent ? c->spill.parent : c->B.parent);
+    (void)hipFree(c->spill.act ? c->spill.act : c->B.act);
     (void)hipFree(c->B.table);
     (void)hipFree(c->B.ctr);
     (void)hipFree(c->d_staged);
@@ -409,6 +518,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     } else {
     c->res = rmc_result{};
     c->level_start.clear();
+    if (c->spill.on) {
+        spill_free(c);
+        spill_rebase(c, 0);
+    }
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
@@ -451,8 +564,28 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         // SYMMETRY: at most 2^24 states per launch, so the tied successors it
         // defers (~1 % of lanes) fit the tie buffer
         const u64 chunk = c->sh.verify ? (1ull << 20) : c->sh.sym ? (1ull << 24) : CHUNK;
-        for (u64 a = lo; a < hi; a += chunk) {
-            const u64 b = std::min(hi, a + chunk);
+        for (u64 a = lo, b = 0; a < hi; a = b) {
+            b = std::min(hi, a + chunk);
+            if (c->spill.on) {
+                // every lane yields at most one new state: a launch of n states
+                // stays inside the window when n * lanes <= room.  Launches
+                // shrink as the window fills; below 2^20 states the expanded
+                // states [base, a) move to the host first — once they are at
+                // least 1/8 of what the move shifts down (or nothing fits)
+                const u64 lanes = (u64)c->P.off[10];
+                const u64 count = c->h_ctr->count, fit = (c->B.cap - count) / lanes;
+                u64 want = b - a;
+                const u64 old = a - c->spill.base;
+                if (fit < std::min<u64>(want, 1ull << 20) && old && (old * 8 >= count - a || fit == 0))
+                    if (int rc = spill_to(c, a, count)) return rc;
+                want = std::min(want, (c->B.cap - count) / lanes);
+                if (want == 0)
+                    return fail(c, RMC_E_CAPACITY,
+                                "spill: the device window (" + std::to_string(c->spill.win) +
+                                    " states) cannot hold the frontier and the level being built; raise "
+                                    "rmc_config.device_window");
+                b = a + want;
+            }
             HIPCHK(c, launch(c->sh, 0, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
             c->res.expand_launches += 1;
             if (c->sh.sym && !c->sh.verify) {
@@ -469,6 +602,13 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                                  c->st));
                 HIPCHK(c, hipMemsetAsync(&c->B.ctr->vcount, 0, 8, c->st));
                 c->h_ctr->vcount = 0;
+            }
+            if (c->spill.on) {
+                if (int rc = read_counters(c)) return rc;
+                if (c->h_ctr->overflow || c->h_ctr->table_full) break;
+                if (c->h_ctr->count > c->spill.total_cap)
+                    return fail(c, RMC_E_CAPACITY, "spill: more states than rmc_config.state_capacity (" +
+                                                       std::to_string(c->spill.total_cap) + ")");
             }
         }
         HIPCHK(c, hipEventRecord(c->ev1, c->st));
@@ -565,7 +705,7 @@ const char kCkptMagic[8] = {'R', 'M', 'C', 'C', 'K', 'P', 'T', '1'};
 bool same_model(const rmc_config& a, const rmc_config& b) {
     return a.n_servers == b.n_servers && a.n_values == b.n_values && a.max_term == b.max_term &&
            a.max_log_len == b.max_log_len && a.max_msgs == b.max_msgs && a.max_dup == b.max_dup &&
-           a.flags == b.flags && a.invariants == b.invariants && a.seed == b.seed;
+           ((a.flags ^ b.flags) & ~RMC_FLAG_SPILL) == 0 && a.invariants == b.invariants && a.seed == b.seed;
 }
 
 // Copy n bytes between a device buffer and a file through a pinned bounce buffer.
@@ -603,7 +743,7 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!f) return fail(c, RMC_E_IO, std::string("checkpoint: cannot create ") + path);
     CkptHeader h{};
     memcpy(h.magic, kCkptMagic, 8);
-    h.version = 1;
+    h.version = 2;  // 2: rmc_config with device_window
     h.nw = (uint32_t)c->NW;
     h.cfg = c->cfg;
     h.count = c->level_start.back();
@@ -612,9 +752,17 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     h.res = c->res;
     int rc = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(c->level_start.data(), 8, h.nlevels, f) == h.nlevels
                  ? 0 : fail(c, RMC_E_IO, "checkpoint write failed");
-    if (!rc) rc = move_file(c, f, c->B.store, h.count * (u64)c->NW * 4, true);
-    if (!rc) rc = move_file(c, f, c->B.parent, h.count * 8, true);
-    if (!rc) rc = move_file(c, f, c->B.act, h.count, true);
+    // spilled states (host segments, in index order) precede the device-resident ones
+    const u64 W = (u64)c->NW * 4, base = c->spill.on ? c->spill.base : 0, nd = h.count - base;
+    auto put = [&](const void* p, u64 n) {
+        if (!rc && fwrite(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint write failed");
+    };
+    for (const SpillSeg& g : c->spill.segs) put(g.store, g.n * W);
+    if (!rc) rc = move_file(c, f, c->B.store + base * (u64)c->NW, nd * W, true);
+    for (const SpillSeg& g : c->spill.segs) put(g.parent, g.n * 8);
+    if (!rc) rc = move_file(c, f, c->B.parent + base, nd * 8, true);
+    for (const SpillSeg& g : c->spill.segs) put(g.act, g.n);
+    if (!rc) rc = move_file(c, f, c->B.act + base, nd, true);
     if (fclose(f) != 0 && !rc) rc = fail(c, RMC_E_IO, "checkpoint close failed");
     return rc;
 }
@@ -628,28 +776,68 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     CkptHeader h{};
     int rc = 0;
     std::vector<u64> ls;
-    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 1)
+    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 2)
         rc = fail(c, RMC_E_IO, "recover: not an rmc checkpoint");
     else if (h.nw != (uint32_t)c->NW || !same_model(h.cfg, c->cfg))
         rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another model (constants, bounds, flags or seed)");
-    else if (h.count > c->B.cap)
-        rc = fail(c, RMC_E_CAPACITY, "recover: the checkpoint holds more states than this ctx's capacity");
     else {
         ls.resize(h.nlevels);
         if (h.nlevels < 2 || fread(ls.data(), 8, h.nlevels, f) != h.nlevels || ls.back() != h.count)
             rc = fail(c, RMC_E_IO, "recover: corrupt level table");
     }
-    if (!rc) rc = move_file(c, f, c->B.store, h.count * (u64)c->NW * 4, false);
-    if (!rc) rc = move_file(c, f, c->B.parent, h.count * 8, false);
-    if (!rc) rc = move_file(c, f, c->B.act, h.count, false);
+    // states [0, s) go to a pinned host segment (spill mode, when they do not all
+    // fit the device window), [s, count) — at least the frontier — to the device
+    u64 s = 0;
+    if (!rc) {
+        const u64 frontier = ls[ls.size() - 2];
+        if (c->spill.on && h.count > c->spill.win) s = frontier;
+        const u64 room = c->spill.on ? c->spill.win : c->B.cap;
+        if (h.count - s > room || (c->spill.on && h.count > c->spill.total_cap))
+            rc = fail(c, RMC_E_CAPACITY, "recover: the checkpoint holds more states than this ctx's capacity");
+    }
+    if (!rc && c->spill.on) {
+        spill_free(c);
+        spill_rebase(c, 0);
+    }
+    SpillSeg g;
+    if (!rc && s) rc = seg_alloc(c, &g, 0, s);
+    const u64 W = (u64)c->NW * 4, nd = h.count - s;
+    auto get = [&](void* p, u64 n) {
+        if (!rc && fread(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint file truncated");
+    };
+    if (s) get(g.store, s * W);
+    if (!rc) rc = move_file(c, f, c->spill.on ? c->spill.store : c->B.store, nd * W, false);
+    if (s) get(g.parent, s * 8);
+    if (!rc) rc = move_file(c, f, c->spill.on ? c->spill.parent : c->B.parent, nd * 8, false);
+    if (s) get(g.act, s);
+    if (!rc) rc = move_file(c, f, c->spill.on ? c->spill.act : c->B.act, nd, false);
     fclose(f);
-    if (rc) return rc;
+    if (rc) {
+        seg_free(g);
+        return rc;
+    }
+    if (s) {
+        c->spill.segs.push_back(g);
+        spill_rebase(c, s);
+    }
     // rebuild the fingerprint set (and the verification slot map) from the states
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
-    HIPCHK(c, launch(c->sh, 7, c->P, c->PT, c->B, 0, h.count, nullptr, nullptr, 0, nullptr, c->st));
+    HIPCHK(c, launch(c->sh, 7, c->P, c->PT, c->B, s, h.count, nullptr, nullptr, 0, nullptr, c->st));
+    if (s) {  // the host segment streams through the free part of the window
+        const u64 free0 = nd, piece = c->spill.win - nd;
+        if (piece == 0) return fail(c, RMC_E_CAPACITY, "recover: the frontier fills the device window");
+        for (u64 p = 0; p < s; p += piece) {
+            const u64 k = std::min(piece, s - p);
+            u32* dst = c->spill.store + free0 * (u64)c->NW;
+            HIPCHK(c, hipMemcpyAsync(dst, (const char*)g.store + p * W, k * W, hipMemcpyHostToDevice, c->st));
+            DevBufs T = c->B;
+            T.store = (u32*)((uintptr_t)dst - (uintptr_t)p * W);
+            HIPCHK(c, launch(c->sh, 7, c->P, c->PT, T, p, p + k, nullptr, nullptr, 0, nullptr, c->st));
+        }
+    }
     if (c->sh.verify) HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, h.count, nullptr, nullptr, 0, nullptr, c->st));
     if (int r2 = read_counters(c)) return r2;
     if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "recover: fingerprint set full");
@@ -671,7 +859,7 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
     for (;;) {
         chain.push_back(idx);
         u64 p = 0;
-        HIPCHK(c, hipMemcpy(&p, c->B.parent + idx, 8, hipMemcpyDeviceToHost));
+        if (int rc = read_stored(c, idx, nullptr, &p, nullptr)) return rc;
         if (p == ~0ull || chain.size() > 100000) break;
         idx = p;
     }
@@ -679,9 +867,8 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
     *len = chain.size();
     std::vector<u32> buf((size_t)c->NW);
     for (size_t q = 0; q < chain.size() && q < cap; ++q) {
-        HIPCHK(c, hipMemcpy(buf.data(), c->B.store + chain[q] * (u64)c->NW, buf.size() * 4, hipMemcpyDeviceToHost));
         uint8_t a = 0;
-        HIPCHK(c, hipMemcpy(&a, c->B.act + chain[q], 1, hipMemcpyDeviceToHost));
+        if (int rc = read_stored(c, chain[q], buf.data(), nullptr, &a)) return rc;
         if (states) decode_state(c, buf.data(), &states[q]);
         if (families) families[q] = family_of(c->P, a);
         if (instances) instances[q] = a == 255 ? -1 : a;

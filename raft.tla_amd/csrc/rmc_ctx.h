@@ -34,6 +34,27 @@ struct DistState {
     double xfer_seconds = 0;        // wall time in collectives and count read-backs
 };
 
+// Frontier spill (RMC_FLAG_SPILL): the device holds the window of states
+// [base, base + win) — the frontier being expanded and the level being built;
+// states below base live in pinned host segments.  B.store / B.parent / B.act
+// are biased by -base, so kernels keep indexing states by their global index.
+struct SpillSeg {
+    rmc::u64 first = 0, n = 0;  // global indices [first, first + n)
+    rmc::u32* store = nullptr;
+    rmc::u64* parent = nullptr;
+    uint8_t* act = nullptr;
+};
+struct SpillState {
+    int on = 0;
+    rmc::u64 base = 0;          // first device-resident global index
+    rmc::u64 win = 0;           // device window (states)
+    rmc::u64 total_cap = 0;     // all states (fingerprint-set sizing)
+    rmc::u32* store = nullptr;  // the real device allocations
+    rmc::u64* parent = nullptr;
+    uint8_t* act = nullptr;
+    std::vector<SpillSeg> segs;
+};
+
 struct rmc_ctx {
     rmc_config cfg{};
     rmc::Shape sh{};
@@ -52,6 +73,7 @@ struct rmc_ctx {
     int have_target = 0;                // a violation / deadlock state to trace
     rmc::u64 target_idx = 0;            // sharded: global ref (rank << 48 | index)
     DistState dist;
+    SpillState spill;
     // recovery (rmc_recover): the next rmc_run_bfs continues from this level
     int resume = 0;
     int resume_depth = 0;
@@ -81,4 +103,9 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user);
 int trace_sharded(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* instances, size_t cap,
                   size_t* len);
 void free_dist(rmc_ctx* c);
+// frontier spill (rmc_api.cpp)
+void spill_rebase(rmc_ctx* c, rmc::u64 base);
+int spill_to(rmc_ctx* c, rmc::u64 a, rmc::u64 count);
+void spill_free(rmc_ctx* c);
+int read_stored(rmc_ctx* c, rmc::u64 idx, rmc::u32* state, rmc::u64* parent, uint8_t* act);
 }  // namespace rmc_host

@@ -416,6 +416,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     if (!rccl_id && !(host && host->alltoallv && host->allgather))
         return fail(c, RMC_E_INVAL, "rmc_shard needs an RCCL id or a host transport");
     if (c->sh.verify) return fail(c, RMC_E_INVAL, "sharded mode does not support full-state verification");
+    if (c->spill.on) return fail(c, RMC_E_INVAL, "sharded mode does not support RMC_FLAG_SPILL");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     free_dist(c);
     DistState& D = c->dist;

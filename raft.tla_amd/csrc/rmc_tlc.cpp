@@ -151,12 +151,15 @@ int usage() {
     fprintf(stderr,
             "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N]\n"
             "               [-verify] [-fpseed S] [-checkpoint F] [-recover F] [-simulate [num=N]] [-seed S]\n"
-            "               [-raft raft.tla] [-builtin-raft] [-gpus N] X.tla\n"
+            "               [-raft raft.tla] [-builtin-raft] [-gpus N] [-nospill] [-window N] X.tla\n"
             "  -gpus N        shard the search over N GPUs (one ctx and RCCL rank per GPU)\n"
             "  -raft F        the raft.tla to verify against the compiled-in spec (default: next to X.tla)\n"
             "  -builtin-raft  no raft.tla on disk: check the compiled-in lemmy/raft.tla (said in the output)\n"
             "  -depth N   stop after N BFS levels (level N is left on the queue)\n"
             "  -verify    full-state verification: compare every fingerprint hit with the stored state\n"
+            "  -nospill   keep every state on the device (stop with a capacity error when it fills);\n"
+            "             by default expanded levels spill to pinned host memory (single GPU)\n"
+            "  -window N  states kept on the device when spilling (default: what the set leaves)\n"
             "  -fpseed S  fingerprint salt (TLC -fp: another member of the fingerprint family)\n"
             "  -checkpoint F  write the search to F when it stops at -depth (TLC -checkpoint)\n"
             "  -recover F     continue the search saved in F (TLC -recover)\n"
@@ -226,7 +229,8 @@ int main(int argc, char** argv) {
     int simulate = 0, gpus = 1;
     std::string ckpt, recover, raft;
     uint32_t fopts = 0;
-    unsigned long long capacity = 0;
+    unsigned long long capacity = 0, window = 0;
+    int nospill = 0;
     for (int a = 1; a < argc; ++a) {
         std::string s = argv[a];
         auto next = [&]() -> const char* { return a + 1 < argc ? argv[++a] : nullptr; };
@@ -238,6 +242,8 @@ int main(int argc, char** argv) {
         else if (s == "-workers") { if (!next()) return usage(); }  // accepted for compatibility
         else if (s == "-gpus") { const char* v = next(); if (!v) return usage(); gpus = atoi(v); }
         else if (s == "-verify") verify = 1;
+        else if (s == "-nospill") nospill = 1;
+        else if (s == "-window") { const char* v = next(); if (!v) return usage(); window = strtoull(v, nullptr, 10); }
         else if (s == "-raft") { const char* v = next(); if (!v) return usage(); raft = v; }
         else if (s == "-builtin-raft") fopts |= RMC_FRONT_BUILTIN_RAFT;
         else if (s == "-checkpoint") { const char* v = next(); if (!v) return usage(); ckpt = v; }
@@ -270,6 +276,10 @@ int main(int argc, char** argv) {
     c.state_capacity = capacity;
     if (nodeadlock) c.flags &= ~RMC_FLAG_CHECK_DEADLOCK;
     if (verify) c.flags |= RMC_FLAG_VERIFY_STATES;
+    // like TLC's states/ directory, expanded levels leave the device when it fills
+    // (single GPU; full-state verification keeps every state resident)
+    if (!nospill && !verify && gpus == 1) c.flags |= RMC_FLAG_SPILL;
+    c.device_window = window;
     c.seed = fpseed;
     printf("Model: %d servers, %d values, CONSTRAINT MaxTerm=%d MaxLogLen=%d MaxMsgs=%d MaxDup=%d%s%s\n",
            c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,
@@ -353,6 +363,9 @@ int main(int argc, char** argv) {
     printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
            (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
     printf("The depth of the complete state graph search is %d.\n", r.depth);
+    if (r.spills)
+        printf("Spilled %llu expanded states to host memory in %llu spills (%.2fs).\n",
+               (unsigned long long)r.spilled, (unsigned long long)r.spills, r.spill_seconds);
     if (!ckpt.empty() && r.left_on_queue > 0 && !r.violated_inv && !r.deadlock) {
         if (rmc_checkpoint(ctx, ckpt.c_str())) printf("Error: %s\n", rmc_last_error(ctx));
         else printf("Checkpoint written to %s (%llu states on the queue).\n", ckpt.c_str(),

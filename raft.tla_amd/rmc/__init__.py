@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
 
 MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8
-FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES = 1, 2, 4, 8
+FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES, FLAG_SPILL = 1, 2, 4, 8, 16
 INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING, INV_MESSAGES = 1, 2, 4, 8
 INV_LEADER_VOTES, INV_CAND_TERM = 16, 32
 INV_VOTES_GRANTED, INV_QUORUM_LOG, INV_MORE_UP_TO_DATE, INV_LEADER_COMPLETE = 64, 128, 256, 512
@@ -38,7 +38,8 @@ class Config(C.Structure):
     _fields_ = [("n_servers", C.c_int32), ("n_values", C.c_int32), ("max_term", C.c_int32),
                 ("max_log_len", C.c_int32), ("max_msgs", C.c_int32), ("max_dup", C.c_int32),
                 ("flags", C.c_uint32), ("invariants", C.c_uint32), ("device", C.c_int32),
-                ("max_depth", C.c_int32), ("state_capacity", C.c_uint64), ("seed", C.c_uint64)]
+                ("max_depth", C.c_int32), ("state_capacity", C.c_uint64), ("seed", C.c_uint64),
+                ("device_window", C.c_uint64)]
 
 
 class Result(C.Structure):
@@ -49,7 +50,8 @@ class Result(C.Structure):
                 ("expand_launches", C.c_uint64), ("probes", C.c_uint64),
                 ("collisions", C.c_uint64), ("verified", C.c_uint64),
                 ("keys_sent", C.c_uint64), ("states_sent", C.c_uint64), ("chunks", C.c_uint64),
-                ("exchange_seconds", C.c_double), ("stored_here", C.c_uint64)]
+                ("exchange_seconds", C.c_double), ("stored_here", C.c_uint64),
+                ("spilled", C.c_uint64), ("spills", C.c_uint64), ("spill_seconds", C.c_double)]
 
 
 class LevelStats(C.Structure):
@@ -196,11 +198,12 @@ class RmcError(RuntimeError):
 
 def make_config(n_servers=3, n_values=2, max_term=2, max_log_len=1, max_msgs=2, max_dup=1,
                 symmetry=False, bug_quorum=False, invariants=INV_TYPEOK, check_deadlock=True,
-                device=0, max_depth=0, state_capacity=0, verify_states=False):
+                device=0, max_depth=0, state_capacity=0, verify_states=False, spill=False, device_window=0):
     flags = (FLAG_SYMMETRY if symmetry else 0) | (FLAG_BUG_QUORUM if bug_quorum else 0) | \
-        (FLAG_CHECK_DEADLOCK if check_deadlock else 0) | (FLAG_VERIFY_STATES if verify_states else 0)
+        (FLAG_CHECK_DEADLOCK if check_deadlock else 0) | (FLAG_VERIFY_STATES if verify_states else 0) | \
+        (FLAG_SPILL if spill else 0)
     return Config(n_servers, n_values, max_term, max_log_len, max_msgs, max_dup, flags,
-                  invariants, device, max_depth, state_capacity, 0)
+                  invariants, device, max_depth, state_capacity, 0, device_window)
 
 
 def model_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False, simulate=False):

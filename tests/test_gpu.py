@@ -353,3 +353,96 @@ def test_config3_full_size_is_exact_by_verification_and_salt(prefix, depth, at_l
     assert (r3.distinct, r3.generated, r3.depth) == (r1.distinct, r1.generated, r1.depth)
     assert r3.collisions == 0
     assert r3.verified == r3.probes - (r3.distinct - 1)
+
+
+# ---- frontier spill (RMC_FLAG_SPILL; TLC's states/ directory)
+
+def spill_cfg(name, slack, **kw):
+    """A config whose device window holds the largest two consecutive levels
+    plus `slack` states — far less than the whole search — so the expanded
+    levels must move to host memory for the search to complete."""
+    g = GOLDEN[name]
+    p = dict(g["params"], **kw)
+    L = g["level_new"]
+    cfg = cfg_from(p, capacity=max(1 << 20, int(g["distinct"] * 1.25)))
+    cfg.flags |= rmc.FLAG_SPILL
+    cfg.device_window = max(a + b for a, b in zip(L, L[1:])) + slack
+    return g, cfg
+
+
+@pytest.mark.parametrize("name,slack", [("bounded_full", 1 << 22), ("small", 1 << 16), ("small_sym", 1 << 14),
+                                        ("tiny2_v2", 4096), ("tiny2", 4096)])
+def test_spill_completes_with_the_oracle_counts(name, slack):
+    g, cfg = spill_cfg(name, slack)
+    assert cfg.device_window < g["distinct"]
+    res, levels, _ = run(cfg)
+    assert levels == g["level_new"]
+    assert (res.distinct, res.generated, res.depth, res.left_on_queue) == \
+        (g["distinct"], g["generated"], g["depth"], g["left_on_queue"])
+    assert res.spills > 0
+    assert res.distinct - res.spilled <= cfg.device_window
+
+
+@pytest.mark.parametrize("name", ["bug_one_leader", "messages_small", "sym_bug_one_leader"])
+def test_spill_trace_equals_the_resident_trace(name):
+    """The counterexample walks parents through host segments and the device
+    window; it must be a behaviour of the spec to a violating state at the
+    depth the resident run reports (which parent wins a race depends on the
+    launch sizes, so the two traces may differ state by state)."""
+    g, cfg = spill_cfg(name, 2048)
+    res, _, trace = run(cfg)
+    assert res.spills > 0
+    base, _, trace0 = run(cfg_from(g["params"]))
+    assert (res.violated_inv, res.violation_depth, res.distinct, res.generated) == \
+        (base.violated_inv, base.violation_depth, base.distinct, base.generated) == \
+        (g["violated_inv"], g["violation_depth"], g["distinct"], g["generated"])
+    assert len(trace) == len(trace0) == g["violation_depth"]
+    p = g["params"]
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
+                    bug_quorum=bool(p["bug_quorum"]))
+    check_trace(model, trace, res.violated_inv, res.violation_depth)
+
+
+@pytest.mark.parametrize("spill_again", [True, False])
+def test_spill_checkpoint_and_recover(spill_again, tmp_path):
+    """A spilled search checkpoints host segments + window in index order; it
+    recovers into a spilling context (old levels back in a host segment, set
+    rebuilt through the window) or into a resident one."""
+    g, cfg = spill_cfg("tiny2_v2", 4096, max_depth=30)
+    with rmc.Checker(cfg) as ck:
+        r1 = ck.run()
+        assert r1.depth == 30 and r1.spills > 0
+        ck.checkpoint(str(tmp_path / "ck"))
+    _, cfg2 = spill_cfg("tiny2_v2", 4096)
+    if not spill_again:
+        cfg2.flags &= ~rmc.FLAG_SPILL
+    with rmc.Checker(cfg2) as ck:
+        ck.recover(str(tmp_path / "ck"))
+        r2 = ck.run()
+        levels = [lv[3] for lv in ck.levels if lv[3]]
+    assert (r2.distinct, r2.generated, r2.depth, r2.left_on_queue) == (g["distinct"], g["generated"], g["depth"], 0)
+    assert levels == g["level_new"][30:]
+    # the recovered result carries the checkpointed run's statistics forward
+    assert (r2.spills > r1.spills) == spill_again and r2.spills >= r1.spills
+
+
+def test_spill_window_too_small_is_a_capacity_error():
+    g, cfg = spill_cfg("small", 0)
+    cfg.device_window = 4096
+    with rmc.Checker(cfg) as ck:
+        with pytest.raises(rmc.RmcError, match="device window"):
+            ck.run()
+
+
+def test_cli_spills_by_default_and_reports_it():
+    import subprocess
+    g = GOLDEN["tiny2"]
+    L = g["level_new"]
+    win = max(a + b for a, b in zip(L, L[1:])) + 4096
+    r = subprocess.run([CLI, "-builtin-raft", "-window", str(win), "-config", os.path.join(SPECS, "MCraftTiny2.cfg"),
+                        os.path.join(SPECS, "MCraftTiny2.tla")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"{g['generated']} states generated, {g['distinct']} distinct states found, 0 states left on queue." \
+        in r.stdout
+    assert "expanded states to host memory" in r.stdout
