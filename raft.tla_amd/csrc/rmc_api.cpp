@@ -13,7 +13,10 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include "rmc_ctx.h"
 
@@ -274,9 +277,11 @@ int read_counters(rmc_ctx* c) {
 }
 
 // ---- frontier spill (RMC_FLAG_SPILL) ---------------------------------------------
-// TLC writes its state queue to the states/ directory;
-// here the expanded levels move to pinned host memory.  Kernels index states by
-// their global index through device pointers biased by -base.
+// TLC keeps its state queue in the states/ directory and a trace file of
+// (parent, action) records from which it re-derives counterexample states
+// (SURVEY.md §8f rank 4).  Here the fingerprint set and the state window stay
+// in HBM; spilled states keep only their trace links in host memory.  Kernels
+// index states by their global index through device pointers biased by -base.
 void spill_rebase(rmc_ctx* c, u64 base) {
     SpillState& X = c->spill;
     X.base = base;
@@ -287,44 +292,64 @@ void spill_rebase(rmc_ctx* c, u64 base) {
     c->B.cap = base + X.win;
 }
 
-static void seg_free(SpillSeg& g) {
-    (void)hipHostFree(g.store);
-    (void)hipHostFree(g.parent);
-    (void)hipHostFree(g.act);
-    g = SpillSeg{};
-}
-
-void spill_free(rmc_ctx* c) {
-    for (auto& g : c->spill.segs) seg_free(g);
-    c->spill.segs.clear();
-}
-
-static int seg_alloc(rmc_ctx* c, SpillSeg* g, u64 first, u64 n) {
-    g->first = first;
-    g->n = n;
-    if (hipHostMalloc(&g->store, std::max<u64>(n, 1) * (u64)c->NW * 4, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&g->parent, std::max<u64>(n, 1) * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&g->act, std::max<u64>(n, 1), hipHostMallocDefault) != hipSuccess) {
-        seg_free(*g);
-        return fail(c, RMC_E_NOMEM, "spill: pinned host allocation of " + std::to_string(n) + " states failed");
+// Address space for the trace links of every state the set can hold; pages
+// are only backed once a spill touches them.
+int spill_reserve(rmc_ctx* c) {
+    SpillState& X = c->spill;
+    X.h_bytes = (size_t)X.total_cap * 9;
+    void* m = mmap(nullptr, X.h_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) {
+        X.h_bytes = 0;
+        return fail(c, RMC_E_NOMEM, "spill: cannot reserve host address space for the trace links");
     }
+    (void)madvise(m, X.h_bytes, MADV_HUGEPAGE);  // 2 MiB faults: fewer, cheaper first touches
+    X.h_parent = (u64*)m;
+    X.h_act = (uint8_t*)m + (size_t)X.total_cap * 8;
+    X.faulted = 0;
     return 0;
 }
 
-// Move the device-resident states [base, a) to a new host segment and shift
-// [a, count) to the start of the window.
+void spill_free(rmc_ctx* c) {
+    if (c->spill.ahead.joinable()) c->spill.ahead.join();
+    if (c->spill.h_bytes) munmap(c->spill.h_parent, c->spill.h_bytes);
+    c->spill.h_parent = nullptr;
+    c->spill.h_act = nullptr;
+    c->spill.h_bytes = 0;
+}
+
+// Touch fresh host pages from several threads: a device-to-host copy into
+// untouched pageable memory runs at page-fault speed (~13 GB/s measured),
+// into touched memory at ~48 GB/s (profiles/r02/host_link_rates.jsonl).
+static void prefault(void* p, size_t n) {
+    const int T = (int)std::min<size_t>(8, std::max<size_t>(1, n >> 26));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([=] {  // one store per 4 KiB page backs it (fresh pages read as zero)
+            volatile char* q = (volatile char*)p;
+            for (size_t o = n * t / T, hi = n * (t + 1) / T; o < hi; o += 4096) q[o] = 0;
+        });
+    for (auto& x : th) x.join();
+}
+
+// Move the trace links of the device-resident states [base, a) to the host
+// and shift [a, count) to the start of the window.
 int spill_to(rmc_ctx* c, u64 a, u64 count) {
     SpillState& X = c->spill;
     const u64 n = a - X.base;
     if (!n) return 0;
     const auto t0 = std::chrono::steady_clock::now();
     const u64 W = (u64)c->NW * 4;
-    SpillSeg g;
-    if (int rc = seg_alloc(c, &g, X.base, n)) return rc;
-    X.segs.push_back(g);
-    HIPCHK(c, hipMemcpyAsync(g.store, X.store, n * W, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipMemcpyAsync(g.parent, X.parent, n * 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipMemcpyAsync(g.act, X.act, n, hipMemcpyDeviceToHost, c->st));
+    u64* hp = X.h_parent + X.base;
+    uint8_t* ha = X.h_act + X.base;
+    if (X.ahead.joinable()) X.ahead.join();
+    if (a > X.faulted) {  // what the background touch did not reach
+        const u64 f0 = std::max(X.faulted, X.base);
+        prefault(X.h_parent + f0, (a - f0) * 8);
+        prefault(X.h_act + f0, a - f0);
+        X.faulted = a;
+    }
+    HIPCHK(c, hipMemcpyAsync(hp, X.parent, n * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(ha, X.act, n, hipMemcpyDeviceToHost, c->st));
     // shift in pieces of at most n states: no piece overlaps its own destination,
     // and stream order keeps every source read before a later piece overwrites it
     const u64 m = count - a;
@@ -337,30 +362,33 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
     }
     HIPCHK(c, hipStreamSynchronize(c->st));
     spill_rebase(c, a);
+    // the next spill takes at most a window's worth: back those pages while the
+    // device expands
+    const u64 f1 = std::min(X.total_cap, a + X.win);
+    if (f1 > X.faulted) {
+        const u64 f0 = X.faulted;
+        X.faulted = f1;
+        X.ahead = std::thread([&X, f0, f1] {
+            prefault(X.h_parent + f0, (f1 - f0) * 8);
+            prefault(X.h_act + f0, f1 - f0);
+        });
+    }
     c->res.spilled += n;
     c->res.spills += 1;
     c->res.spill_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return 0;
 }
 
-// One stored state (any of state / parent / act may be null), wherever it lives.
-int read_stored(rmc_ctx* c, u64 idx, u32* state, u64* parent, uint8_t* act) {
-    const u64 W = (u64)c->NW * 4;
-    if (!c->spill.on || idx >= c->spill.base) {
-        if (state) HIPCHK(c, hipMemcpy(state, c->B.store + idx * (u64)c->NW, W, hipMemcpyDeviceToHost));
-        if (parent) HIPCHK(c, hipMemcpy(parent, c->B.parent + idx, 8, hipMemcpyDeviceToHost));
-        if (act) HIPCHK(c, hipMemcpy(act, c->B.act + idx, 1, hipMemcpyDeviceToHost));
+// The trace link (parent index, action lane) of any stored state.
+int read_link(rmc_ctx* c, u64 idx, u64* parent, uint8_t* act) {
+    if (c->spill.on && idx < c->spill.base) {
+        *parent = c->spill.h_parent[idx];
+        *act = c->spill.h_act[idx];
         return 0;
     }
-    for (const SpillSeg& g : c->spill.segs) {
-        if (idx < g.first || idx >= g.first + g.n) continue;
-        const u64 o = idx - g.first;
-        if (state) memcpy(state, (const char*)g.store + o * W, W);
-        if (parent) *parent = g.parent[o];
-        if (act) *act = g.act[o];
-        return 0;
-    }
-    return fail(c, RMC_E_STATE, "state " + std::to_string(idx) + " is in no spill segment");
+    HIPCHK(c, hipMemcpy(parent, c->B.parent + idx, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(act, c->B.act + idx, 1, hipMemcpyDeviceToHost));
+    return 0;
 }
 
 }  // namespace rmc_host
@@ -450,6 +478,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     c->spill.store = c->B.store;
     c->spill.parent = c->B.parent;
     c->spill.act = c->B.act;
+    if (spill && spill_reserve(c)) return bail(RMC_E_NOMEM);
     if (hipHostMalloc(&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
         c->err = "pinned allocation failed";
         return bail(RMC_E_NOMEM);
@@ -519,8 +548,17 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res = rmc_result{};
     c->level_start.clear();
     if (c->spill.on) {
-        spill_free(c);
         spill_rebase(c, 0);
+        SpillState& X = c->spill;
+        const u64 f1 = std::min(X.total_cap, X.win);  // back the first spill's pages meanwhile
+        if (!X.ahead.joinable() && f1 > X.faulted) {
+            const u64 f0 = X.faulted;
+            X.faulted = f1;
+            X.ahead = std::thread([&X, f0, f1] {
+                prefault(X.h_parent + f0, (f1 - f0) * 8);
+                prefault(X.h_act + f0, f1 - f0);
+            });
+        }
     }
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
@@ -699,6 +737,8 @@ struct CkptHeader {
     uint64_t count, nlevels;
     int32_t depth, pad;
     rmc_result res;
+    uint64_t first;  // states are written from this index on (0: all; else the frontier)
+    uint64_t slots;  // fingerprint-set slots dumped after the states (first > 0), else 0
 };
 const char kCkptMagic[8] = {'R', 'M', 'C', 'C', 'K', 'P', 'T', '1'};
 
@@ -731,6 +771,9 @@ int move_file(rmc_ctx* c, FILE* f, void* dev, u64 n, bool to_file) {
 }
 }  // namespace
 
+// Layout: header, level table, parent[0, count), act[0, count), store[first,
+// count), then — when the states below `first` have spilled and no longer
+// exist — the fingerprint set itself (TLC checkpoints its FPSet too).
 int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
     if (c->dist.on) return fail(c, RMC_E_INVAL, "checkpoint: single-GPU runs only");
@@ -743,26 +786,28 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!f) return fail(c, RMC_E_IO, std::string("checkpoint: cannot create ") + path);
     CkptHeader h{};
     memcpy(h.magic, kCkptMagic, 8);
-    h.version = 2;  // 2: rmc_config with device_window
+    h.version = 2;  // 2: rmc_config with device_window, spilled checkpoints
     h.nw = (uint32_t)c->NW;
     h.cfg = c->cfg;
     h.count = c->level_start.back();
     h.nlevels = c->level_start.size();
     h.depth = c->res.depth;
     h.res = c->res;
+    const u64 base = c->spill.on ? c->spill.base : 0;
+    h.first = base ? c->level_start[h.nlevels - 2] : 0;  // >= base at a level boundary
+    h.slots = base ? c->table_slots : 0;
     int rc = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(c->level_start.data(), 8, h.nlevels, f) == h.nlevels
                  ? 0 : fail(c, RMC_E_IO, "checkpoint write failed");
-    // spilled states (host segments, in index order) precede the device-resident ones
-    const u64 W = (u64)c->NW * 4, base = c->spill.on ? c->spill.base : 0, nd = h.count - base;
     auto put = [&](const void* p, u64 n) {
-        if (!rc && fwrite(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint write failed");
+        if (!rc && n && fwrite(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint write failed");
     };
-    for (const SpillSeg& g : c->spill.segs) put(g.store, g.n * W);
-    if (!rc) rc = move_file(c, f, c->B.store + base * (u64)c->NW, nd * W, true);
-    for (const SpillSeg& g : c->spill.segs) put(g.parent, g.n * 8);
+    const u64 nd = h.count - base;
+    if (base) put(c->spill.h_parent, base * 8);
     if (!rc) rc = move_file(c, f, c->B.parent + base, nd * 8, true);
-    for (const SpillSeg& g : c->spill.segs) put(g.act, g.n);
+    if (base) put(c->spill.h_act, base);
     if (!rc) rc = move_file(c, f, c->B.act + base, nd, true);
+    if (!rc) rc = move_file(c, f, c->B.store + h.first * (u64)c->NW, (h.count - h.first) * (u64)c->NW * 4, true);
+    if (!rc && h.slots) rc = move_file(c, f, c->B.table, h.slots * 8, true);
     if (fclose(f) != 0 && !rc) rc = fail(c, RMC_E_IO, "checkpoint close failed");
     return rc;
 }
@@ -780,64 +825,71 @@ int rmc_recover(rmc_ctx* c, const char* path) {
         rc = fail(c, RMC_E_IO, "recover: not an rmc checkpoint");
     else if (h.nw != (uint32_t)c->NW || !same_model(h.cfg, c->cfg))
         rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another model (constants, bounds, flags or seed)");
+    else if (h.first && (!c->spill.on || h.slots != c->table_slots))
+        rc = fail(c, RMC_E_INVAL, "recover: a spilled checkpoint holds the fingerprint set, not the spilled "
+                                  "states; recover it with RMC_FLAG_SPILL and the same state_capacity");
     else {
         ls.resize(h.nlevels);
-        if (h.nlevels < 2 || fread(ls.data(), 8, h.nlevels, f) != h.nlevels || ls.back() != h.count)
+        if (h.nlevels < 2 || fread(ls.data(), 8, h.nlevels, f) != h.nlevels || ls.back() != h.count ||
+            h.first > h.count)
             rc = fail(c, RMC_E_IO, "recover: corrupt level table");
     }
-    // states [0, s) go to a pinned host segment (spill mode, when they do not all
-    // fit the device window), [s, count) — at least the frontier — to the device
+    // states [0, s) keep only their trace links, on the host (spill mode, when
+    // they do not all fit the window); [s, count) — at least the frontier — go
+    // to the device
     u64 s = 0;
     if (!rc) {
-        const u64 frontier = ls[ls.size() - 2];
-        if (c->spill.on && h.count > c->spill.win) s = frontier;
+        s = h.first ? h.first : (c->spill.on && h.count > c->spill.win) ? ls[ls.size() - 2] : 0;
         const u64 room = c->spill.on ? c->spill.win : c->B.cap;
         if (h.count - s > room || (c->spill.on && h.count > c->spill.total_cap))
             rc = fail(c, RMC_E_CAPACITY, "recover: the checkpoint holds more states than this ctx's capacity");
+        if (!rc && !h.first && s && h.count - s >= room)  // no room left to stream the rehash through
+            rc = fail(c, RMC_E_CAPACITY, "recover: the frontier fills the device window");
     }
-    if (!rc && c->spill.on) {
-        spill_free(c);
-        spill_rebase(c, 0);
-    }
-    SpillSeg g;
-    if (!rc && s) rc = seg_alloc(c, &g, 0, s);
-    const u64 W = (u64)c->NW * 4, nd = h.count - s;
-    auto get = [&](void* p, u64 n) {
-        if (!rc && fread(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint file truncated");
-    };
-    if (s) get(g.store, s * W);
-    if (!rc) rc = move_file(c, f, c->spill.on ? c->spill.store : c->B.store, nd * W, false);
-    if (s) get(g.parent, s * 8);
-    if (!rc) rc = move_file(c, f, c->spill.on ? c->spill.parent : c->B.parent, nd * 8, false);
-    if (s) get(g.act, s);
-    if (!rc) rc = move_file(c, f, c->spill.on ? c->spill.act : c->B.act, nd, false);
-    fclose(f);
     if (rc) {
-        seg_free(g);
+        fclose(f);
         return rc;
     }
-    if (s) {
-        c->spill.segs.push_back(g);
-        spill_rebase(c, s);
+    if (c->spill.on) {
+        if (c->spill.ahead.joinable()) c->spill.ahead.join();  // it may be touching [0, s)
+        spill_rebase(c, 0);
+        c->spill.faulted = std::max(c->spill.faulted, s);  // fread backs the links it writes
     }
-    // rebuild the fingerprint set (and the verification slot map) from the states
+    const u64 NW = (u64)c->NW, W = NW * 4;
+    u32* dstore = c->spill.on ? c->spill.store : c->B.store;
+    u64* dparent = c->spill.on ? c->spill.parent : c->B.parent;
+    uint8_t* dact = c->spill.on ? c->spill.act : c->B.act;
+    auto get = [&](void* p, u64 n) {
+        if (!rc && n && fread(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint file truncated");
+    };
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
-    HIPCHK(c, launch(c->sh, 7, c->P, c->PT, c->B, s, h.count, nullptr, nullptr, 0, nullptr, c->st));
-    if (s) {  // the host segment streams through the free part of the window
-        const u64 free0 = nd, piece = c->spill.win - nd;
-        if (piece == 0) return fail(c, RMC_E_CAPACITY, "recover: the frontier fills the device window");
-        for (u64 p = 0; p < s; p += piece) {
+    if (s) get(c->spill.h_parent, s * 8);
+    if (!rc) rc = move_file(c, f, dparent, (h.count - s) * 8, false);
+    if (s) get(c->spill.h_act, s);
+    if (!rc) rc = move_file(c, f, dact, h.count - s, false);
+    if (!h.first && s && !rc) {
+        // no set in the file: rehash the states below s through the free part
+        // of the window (the frontier is loaded after them, at its start)
+        const u64 piece = c->spill.win - (h.count - s);
+        u32* area = dstore + (h.count - s) * NW;
+        for (u64 p = 0; p < s && !rc; p += piece) {
             const u64 k = std::min(piece, s - p);
-            u32* dst = c->spill.store + free0 * (u64)c->NW;
-            HIPCHK(c, hipMemcpyAsync(dst, (const char*)g.store + p * W, k * W, hipMemcpyHostToDevice, c->st));
+            rc = move_file(c, f, area, k * W, false);
             DevBufs T = c->B;
-            T.store = (u32*)((uintptr_t)dst - (uintptr_t)p * W);
-            HIPCHK(c, launch(c->sh, 7, c->P, c->PT, T, p, p + k, nullptr, nullptr, 0, nullptr, c->st));
+            T.store = (u32*)((uintptr_t)area - (uintptr_t)(p * W));
+            if (!rc) HIPCHK(c, launch(c->sh, 7, c->P, c->PT, T, p, p + k, nullptr, nullptr, 0, nullptr, c->st));
+            if (!rc) HIPCHK(c, hipStreamSynchronize(c->st));
         }
     }
+    if (!rc) rc = move_file(c, f, dstore, (h.count - s) * W, false);
+    if (!rc && h.slots) rc = move_file(c, f, c->B.table, h.slots * 8, false);
+    fclose(f);
+    if (rc) return rc;
+    if (s) spill_rebase(c, s);
+    if (!h.slots) HIPCHK(c, launch(c->sh, 7, c->P, c->PT, c->B, s, h.count, nullptr, nullptr, 0, nullptr, c->st));
     if (c->sh.verify) HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, h.count, nullptr, nullptr, 0, nullptr, c->st));
     if (int r2 = read_counters(c)) return r2;
     if (c->h_ctr->table_full) return fail(c, RMC_E_CAPACITY, "recover: fingerprint set full");
@@ -849,31 +901,79 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     return 0;
 }
 
+// The counterexample: parent links back to Init, then the states.  States
+// whose store was spilled are re-derived by replaying the recorded lanes from
+// the last state still known (Init at worst) with the listing kernel — the
+// stored successor of a parent through a lane is exactly what it lists.
 int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* instances, size_t cap, size_t* len) {
     if (!c || !len) return RMC_E_INVAL;
     if (!c->have_target) return fail(c, RMC_E_STATE, "no violation or deadlock to trace");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->dist.on) return trace_sharded(c, states, families, instances, cap, len);
     std::vector<u64> chain;
+    std::vector<uint8_t> acts;
     u64 idx = c->target_idx;
     for (;;) {
-        chain.push_back(idx);
         u64 p = 0;
-        if (int rc = read_stored(c, idx, nullptr, &p, nullptr)) return rc;
+        uint8_t a = 0;
+        if (int rc = read_link(c, idx, &p, &a)) return rc;
+        chain.push_back(idx);
+        acts.push_back(a);
         if (p == ~0ull || chain.size() > 100000) break;
         idx = p;
     }
     std::reverse(chain.begin(), chain.end());
+    std::reverse(acts.begin(), acts.end());
     *len = chain.size();
-    std::vector<u32> buf((size_t)c->NW);
-    for (size_t q = 0; q < chain.size() && q < cap; ++q) {
-        uint8_t a = 0;
-        if (int rc = read_stored(c, chain[q], buf.data(), nullptr, &a)) return rc;
-        if (states) decode_state(c, buf.data(), &states[q]);
-        if (families) families[q] = family_of(c->P, a);
-        if (instances) instances[q] = a == 255 ? -1 : a;
+    const u64 NW = (u64)c->NW, RW = 6 + NW, lanes = (u64)c->P.off[10];
+    std::vector<u32> cur(NW);
+    u32 *d_in = nullptr, *d_out = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    int rc = 0;
+    for (size_t q = 0; q < chain.size() && !rc; ++q) {
+        if (!c->spill.on || chain[q] >= c->spill.base) {
+            HIPCHK(c, hipMemcpy(cur.data(), c->B.store + chain[q] * NW, NW * 4, hipMemcpyDeviceToHost));
+        } else if (q == 0) {  // Init (raft.tla:125-129), the one initial state
+            rmc_state_view iv;
+            init_view(c->cfg, &iv);
+            std::string why;
+            if (encode_view(c, iv, cur.data(), &why)) return fail(c, RMC_E_INVAL, why);
+        } else {  // replay lane acts[q] from the previous state on the device
+            if (!d_in) {
+                if (hipMalloc(&d_in, NW * 4) != hipSuccess || hipMalloc(&d_out, lanes * RW * 4) != hipSuccess ||
+                    hipMalloc(&d_cnt, 8) != hipSuccess)
+                    rc = fail(c, RMC_E_NOMEM, "trace: replay buffers");
+            }
+            std::vector<u32> recs(lanes * RW);
+            unsigned long long n = 0;
+            if (!rc && (hipMemcpy(d_in, cur.data(), NW * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                        hipMemset(d_cnt, 0, 8) != hipSuccess ||
+                        launch(c->sh, 2, c->P, c->PT, c->B, 1, 0, d_in, d_out, lanes, d_cnt, c->st) != hipSuccess ||
+                        hipStreamSynchronize(c->st) != hipSuccess ||
+                        hipMemcpy(&n, d_cnt, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+                        hipMemcpy(recs.data(), d_out, std::min<u64>(n, lanes) * RW * 4, hipMemcpyDeviceToHost) != hipSuccess))
+                rc = fail(c, RMC_E_HIP, "trace: replay launch failed");
+            bool found = false;
+            for (u64 r = 0; !rc && r < std::min<u64>(n, lanes); ++r) {
+                const u32* rec = &recs[r * RW];
+                if (rec[2] == acts[q] && rec[3]) {
+                    memcpy(cur.data(), rec + 6, NW * 4);
+                    found = true;
+                    break;
+                }
+            }
+            if (!rc && !found) rc = fail(c, RMC_E_STATE, "trace: a recorded lane is not enabled on replay");
+        }
+        if (!rc && q < cap) {
+            if (states) decode_state(c, cur.data(), &states[q]);
+            if (families) families[q] = family_of(c->P, acts[q]);
+            if (instances) instances[q] = acts[q] == 255 ? -1 : acts[q];
+        }
     }
-    return 0;
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cnt);
+    return rc;
 }
 
 }  // extern "C"

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rmc.h"
@@ -34,16 +35,13 @@ struct DistState {
     double xfer_seconds = 0;        // wall time in collectives and count read-backs
 };
 
-// Frontier spill (RMC_FLAG_SPILL): the device holds the window of states
-// [base, base + win) — the frontier being expanded and the level being built;
-// states below base live in pinned host segments.  B.store / B.parent / B.act
-// are biased by -base, so kernels keep indexing states by their global index.
-struct SpillSeg {
-    rmc::u64 first = 0, n = 0;  // global indices [first, first + n)
-    rmc::u32* store = nullptr;
-    rmc::u64* parent = nullptr;
-    uint8_t* act = nullptr;
-};
+// Frontier spill (RMC_FLAG_SPILL): the device holds the fingerprint set and
+// the window of states [base, base + win) — the frontier being expanded and the
+// level being built.  Below base only the trace links survive, in host memory:
+// parent index + action lane per state (9 B, TLC's trace file), and a
+// counterexample re-derives those states by replaying the lanes from Init.
+// B.store / B.parent / B.act are biased by -base, so kernels keep indexing
+// states by their global index.
 struct SpillState {
     int on = 0;
     rmc::u64 base = 0;          // first device-resident global index
@@ -52,7 +50,11 @@ struct SpillState {
     rmc::u32* store = nullptr;  // the real device allocations
     rmc::u64* parent = nullptr;
     uint8_t* act = nullptr;
-    std::vector<SpillSeg> segs;
+    rmc::u64* h_parent = nullptr;  // host, [total_cap], reserved address space,
+    uint8_t* h_act = nullptr;      // pages touched as levels spill
+    size_t h_bytes = 0;
+    rmc::u64 faulted = 0;          // links [0, faulted) have backed pages
+    std::thread ahead;             // backs the next window's pages during expansion
 };
 
 struct rmc_ctx {
@@ -105,7 +107,8 @@ int trace_sharded(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t
 void free_dist(rmc_ctx* c);
 // frontier spill (rmc_api.cpp)
 void spill_rebase(rmc_ctx* c, rmc::u64 base);
+int spill_reserve(rmc_ctx* c);
 int spill_to(rmc_ctx* c, rmc::u64 a, rmc::u64 count);
 void spill_free(rmc_ctx* c);
-int read_stored(rmc_ctx* c, rmc::u64 idx, rmc::u32* state, rmc::u64* parent, uint8_t* act);
+int read_link(rmc_ctx* c, rmc::u64 idx, rmc::u64* parent, uint8_t* act);
 }  // namespace rmc_host

@@ -404,27 +404,53 @@ def test_spill_trace_equals_the_resident_trace(name):
     check_trace(model, trace, res.violated_inv, res.violation_depth)
 
 
-@pytest.mark.parametrize("spill_again", [True, False])
-def test_spill_checkpoint_and_recover(spill_again, tmp_path):
-    """A spilled search checkpoints host segments + window in index order; it
-    recovers into a spilling context (old levels back in a host segment, set
-    rebuilt through the window) or into a resident one."""
-    g, cfg = spill_cfg("tiny2_v2", 4096, max_depth=30)
+@pytest.mark.parametrize("first,second", [("spill", "spill"), ("resident", "spill"), ("spill", "resident")])
+def test_spill_checkpoint_and_recover(first, second, tmp_path):
+    """A spilled search checkpoints its trace links, frontier and fingerprint
+    set (the spilled states no longer exist) and recovers into a spilling
+    context; a resident checkpoint recovers into a spilling context by
+    streaming the old states through the window to rebuild the set; a spilled
+    checkpoint cannot become resident."""
+    g, scfg = spill_cfg("tiny2_v2", 4096, max_depth=30)
+    cfg = scfg if first == "spill" else cfg_from(dict(g["params"], max_depth=30),
+                                                 capacity=scfg.state_capacity)
     with rmc.Checker(cfg) as ck:
         r1 = ck.run()
-        assert r1.depth == 30 and r1.spills > 0
+        assert r1.depth == 30 and (r1.spills > 0) == (first == "spill")
         ck.checkpoint(str(tmp_path / "ck"))
     _, cfg2 = spill_cfg("tiny2_v2", 4096)
-    if not spill_again:
+    if second == "resident":
         cfg2.flags &= ~rmc.FLAG_SPILL
+        with rmc.Checker(cfg2) as ck:
+            with pytest.raises(rmc.RmcError, match="spilled checkpoint"):
+                ck.recover(str(tmp_path / "ck"))
+        return
     with rmc.Checker(cfg2) as ck:
         ck.recover(str(tmp_path / "ck"))
         r2 = ck.run()
         levels = [lv[3] for lv in ck.levels if lv[3]]
     assert (r2.distinct, r2.generated, r2.depth, r2.left_on_queue) == (g["distinct"], g["generated"], g["depth"], 0)
     assert levels == g["level_new"][30:]
-    # the recovered result carries the checkpointed run's statistics forward
-    assert (r2.spills > r1.spills) == spill_again and r2.spills >= r1.spills
+    assert r2.spills > r1.spills  # the recovered result carries the checkpointed statistics forward
+
+
+def test_spill_recover_to_the_violation_replays_the_trace(tmp_path):
+    g, cfg = spill_cfg("bug_one_leader", 2048, max_depth=9)
+    with rmc.Checker(cfg) as ck:
+        ck.run()
+        ck.checkpoint(str(tmp_path / "ck"))
+    _, cfg = spill_cfg("bug_one_leader", 2048)
+    with rmc.Checker(cfg) as ck:
+        ck.recover(str(tmp_path / "ck"))
+        res = ck.run()
+        trace = ck.trace()
+    assert res.spills > 0  # levels 10-11 outgrow the window: the trace replays spilled states
+    assert (res.violated_inv, res.violation_depth, res.distinct, res.generated) == \
+        (g["violated_inv"], g["violation_depth"], g["distinct"], g["generated"])
+    p = g["params"]
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"], bug_quorum=True)
+    check_trace(model, trace, res.violated_inv, res.violation_depth)
 
 
 def test_spill_window_too_small_is_a_capacity_error():
