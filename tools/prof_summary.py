@@ -3,6 +3,9 @@
   kernel_stats_<cfg>.csv     per-kernel calls / total / average (kernel-trace pass)
   pmc_traffic_<cfg>.json     HBM bytes per k_expand launch (FETCH_SIZE and
                              WRITE_SIZE passes, one counter per pass)
+  pmc_counters_<cfg>.json    every counter of the other passes present
+                             (insts / stall / tcc: tools/gpu/prof_r02.sh) for
+                             the same kernel, totals and per launch
 
     python tools/prof_summary.py gpurun_out/prof r01 MCraftBench
 """
@@ -62,6 +65,22 @@ def main():
     }
     json.dump(rec, open(os.path.join(out, f"pmc_traffic_{stem}.json"), "w"), indent=1)
     print(json.dumps(rec, indent=1))
+    extra = {}
+    for pas in ("insts", "stall", "tcc"):
+        d = os.path.join(src, pas)
+        if not os.path.isdir(d):
+            continue
+        db = one_db(d)
+        for (cname,) in db.execute("select distinct counter_name from counters_collection where kernel_name = ?",
+                                   (name,)).fetchall():
+            v = counter(db, cname)
+            extra[cname] = {"pass": pas, "total": sum(v), "launches": len(v), "per_launch": sum(v) / max(1, len(v))}
+    if extra:
+        json.dump({"kernel": name, "workload": rec["workload"], "counters": extra,
+                   "note": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md)"},
+                  open(os.path.join(out, f"pmc_counters_{stem}.json"), "w"), indent=1)
+        for k, v in sorted(extra.items()):
+            print(f"{k:24s} {v['per_launch']:.4g} per launch")
 
 
 if __name__ == "__main__":
