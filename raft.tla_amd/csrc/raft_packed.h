@@ -822,24 +822,58 @@ RMC_HD u64 sig_base(u64 w, u32 i) {
     return s | ((u64)selfp << 36) | ((u64)(others & 0xFFFFu) << 40);
 }
 // Signature, part 2: the messages a server sends and receives, ids masked,
-// summed order-free.
+// summed order-free.  Servers are ranked by (part 1, part 2) lexicographically:
+// part 1 leads, so an action that only adds, duplicates or drops a message
+// (RequestVote, AppendEntries, Duplicate, Drop: over half of the lanes) can
+// reorder only servers whose part 1 ties — which keeps most successors in
+// their parent's order (canon_delta_inc's cheap path).
 RMC_HD u32 sig_src(u32 sl) { return (sl & ~0xFCu) * 0x9E3779B1u + 0x7F4A7C15u; }
 RMC_HD u32 sig_dst(u32 sl) { return (sl & ~0xFCu) * 0x85EBCA77u + 0xC2B2AE3Du; }
+template <int S>
+struct Sig {
+    u64 b[S];  // part 1 (sig_base)
+    u32 m[S];  // part 2 (message sums)
+};
 template <int S, int K1>
-RMC_HD void signatures(const u64 (&base)[S], const u32 (&m)[K1], u64 (&sig)[S]) {
-    u32 ms[S];
+RMC_HD void signatures(const u64 (&base)[S], const u32 (&m)[K1], Sig<S>& sg) {
 #pragma unroll
-    for (int i = 0; i < S; ++i) ms[i] = 0;
+    for (int i = 0; i < S; ++i) {
+        sg.b[i] = base[i];
+        sg.m[i] = 0;
+    }
 #pragma unroll
     for (int q = 0; q < K1; ++q) {
         const u32 sl = m[q];
         const u32 a = sl ? sig_src(sl) : 0u, b = sl ? sig_dst(sl) : 0u;
         const u32 src = m_src(sl), dst = m_dst(sl);
 #pragma unroll
-        for (int i = 0; i < S; ++i) ms[i] += (src == (u32)i ? a : 0u) + (dst == (u32)i ? b : 0u);
+        for (int i = 0; i < S; ++i) sg.m[i] += (src == (u32)i ? a : 0u) + (dst == (u32)i ? b : 0u);
     }
+}
+// Rank of every server by signature (3 bits each in *lo: server i -> its rank,
+// the sorting permutation when nothing ties), the size of its tie class in
+// *tc, and whether any two servers tie.
+template <int S>
+RMC_HD bool sig_rank(const Sig<S>& sg, u32* lo, u32* tc) {
+    u32 l = 0, c = 0;
+    bool tie = false;
 #pragma unroll
-    for (int i = 0; i < S; ++i) sig[i] = base[i] + ((u64)ms[i] << 29);
+    for (int i = 0; i < S; ++i) {
+        u32 r = 0, n = 0;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const bool lt = sg.b[j] < sg.b[i] || (sg.b[j] == sg.b[i] && sg.m[j] < sg.m[i]);
+            const bool eq = sg.b[j] == sg.b[i] && sg.m[j] == sg.m[i];
+            r += lt ? 1u : 0u;
+            n += eq ? 1u : 0u;
+        }
+        l |= r << (3 * i);
+        c |= n << (3 * i);
+        tie |= n > 1;
+    }
+    *lo = l;
+    *tc = c;
+    return tie;
 }
 // Fingerprint of pi(s) (any slot order; empty slots are 0).
 template <int S, int K1>
@@ -884,22 +918,10 @@ RMC_HD u64 canon_ties(const SymState<S, K1> t, u32 lo, u32 tc, const u32* codes,
 // single-GPU SYMMETRY kernel defers those lanes to k_ties, so its hot loop
 // carries no permutation enumeration).
 template <int S, int K1, bool NOTIE = false>
-RMC_HD u64 canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const u64 (&sig)[S], const u32* codes, int np,
+RMC_HD u64 canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const Sig<S>& sg, const u32* codes, int np,
                         int* tied = nullptr) {
-    u32 lo = 0, tc = 0;
-    bool tie = false;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        u32 l = 0, n = 0;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            l += sig[j] < sig[i] ? 1u : 0u;
-            n += sig[j] == sig[i] ? 1u : 0u;
-        }
-        lo |= l << (3 * i);
-        tc |= n << (3 * i);
-        tie |= n > 1;
-    }
+    u32 lo, tc;
+    const bool tie = sig_rank<S>(sg, &lo, &tc);
     if (!tie) return fp_perm<S, K1>(w, m, lo);  // the sorting permutation: server i -> its rank
     if constexpr (NOTIE) {
         *tied = 1;
@@ -915,11 +937,12 @@ RMC_HD u64 canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const u64 (&sig)[
 // The canonical key of a stored (materialised) state.
 template <int S, int K>
 RMC_HD u64 canon_state(const u64 (&w)[S], const u32 (&m)[K], const u32* codes, int np) {
-    u64 base[S], sig[S];
+    u64 base[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) base[i] = sig_base<S>(w[i], (u32)i);
-    signatures<S, K>(base, m, sig);
-    return canon_sorted<S, K>(w, m, sig, codes, np);
+    Sig<S> sg;
+    signatures<S, K>(base, m, sg);
+    return canon_sorted<S, K>(w, m, sg, codes, np);
 }
 // The canonical key of the successor a delta makes of (w, m): the successor's
 // words and slots (unsorted: fingerprints are order-free), the parent's
@@ -927,7 +950,7 @@ RMC_HD u64 canon_state(const u64 (&w)[S], const u32 (&m)[K], const u32* codes, i
 template <int S, int K, bool NOTIE = false>
 RMC_HD u64 canon_delta(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], const Delta& d, const u32* codes,
                        int np, int* tied = nullptr) {
-    u64 ws[S], bs[S], sig[S];
+    u64 ws[S], bs[S];
     u32 ms[K + 1];
 #pragma unroll
     for (int i = 0; i < S; ++i) {
@@ -948,8 +971,101 @@ RMC_HD u64 canon_delta(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S
         for (int q = 0; q < K; ++q) ms[q] += q == found ? CNT_ONE : 0u;
         ms[K] = found < 0 ? (d.add | CNT_ONE) : 0u;
     }
-    signatures<S, K + 1>(bs, ms, sig);
-    return canon_sorted<S, K + 1, NOTIE>(ws, ms, sig, codes, np, tied);
+    Sig<S> sg;
+    signatures<S, K + 1>(bs, ms, sg);
+    return canon_sorted<S, K + 1, NOTIE>(ws, ms, sg, codes, np, tied);
+}
+
+// ---- incremental canonical keys (the single-GPU SYMMETRY hot loop) ------------------
+// A delta changes one server word and at most two bag slots, and most deltas
+// leave the servers' signature order alone.  The parent's frame is computed
+// once per expanded state: its per-server message signature sums, its
+// sorting permutation `lo` and the mixes of its components under `lo`.  A lane
+// then updates the signatures of the servers its delta touches, re-ranks them,
+// and — when the successor sorts by the same permutation — gets its key from
+// the parent's as canon_delta would (the same sum of the same mixes, mod 2^64),
+// re-mixing only the changed components: 1-3 mixes instead of S + K + 1.
+template <int S, int K>
+struct SymParent {
+    u64 hw[S];   // hS(perm_word(w[i], lo), pe(lo, i))
+    u64 h0;      // with the slots' hM(perm_slot(m[q], lo)): the fingerprint of lo(parent)
+    u32 ms[S];   // per-server message signature sums (Sig::m)
+    u32 lo;      // the parent's sorting permutation; ~0u when its signatures tie
+};
+template <int S, int K>
+RMC_HD void sym_parent(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], SymParent<S, K>& sp) {
+    Sig<S> sg;
+    signatures<S, K>(base, m, sg);
+#pragma unroll
+    for (int i = 0; i < S; ++i) sp.ms[i] = sg.m[i];
+    u32 tc;
+    const bool tie = sig_rank<S>(sg, &sp.lo, &tc);
+    if (tie) sp.lo = ~0u;
+    const u32 c = tie ? 0u : sp.lo;  // mixes unused when tied
+    sp.h0 = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) { sp.hw[i] = hS(perm_word<S>(w[i], c), pe(c, (u32)i)); sp.h0 += sp.hw[i]; }
+#pragma unroll
+    for (int q = 0; q < K; ++q) sp.h0 += hM(perm_slot(m[q], c));
+}
+// Signature sums of one slot moved in (sgn = +1) or out (-1); 0 = no slot.
+template <int S>
+RMC_HD void sig_slot(u32 (&ms)[S], u32 sl, u32 sgn) {
+    const u32 a = sl ? sig_src(sl) * sgn : 0u, b = sl ? sig_dst(sl) * sgn : 0u;
+#pragma unroll
+    for (int i = 0; i < S; ++i) ms[i] += (m_src(sl) == (u32)i ? a : 0u) + (m_dst(sl) == (u32)i ? b : 0u);
+}
+// canon_delta<S, K, true> computed from the parent's frame.  Same result: the
+// key when the successor's signatures do not tie, *tied = 1 when they do.
+template <int S, int K>
+RMC_HD u64 canon_delta_inc(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], const SymParent<S, K>& sp,
+                           const Delta& d, const u32* codes, int np, int* tied) {
+    // the slots the delta changes: rm (old -> new) and the add (old -> new;
+    // old = 0 when the message is not in the bag yet)
+    const u32 rm_old = d.rm >= 0 ? selm<K>(m, d.rm) : 0u;
+    const u32 rm_new = m_cnt(rm_old) > 1 ? rm_old - CNT_ONE : 0u;
+    int found = -1;
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        const u32 sl = q == d.rm ? rm_new : m[q];
+        found = (d.has_add && sl && (sl & MSG_MASK) == d.add) ? q : found;
+    }
+    const u32 add_old = found < 0 ? 0u : found == d.rm ? rm_new : selm<K>(m, found);
+    const u32 add_new = d.has_add ? (found >= 0 ? add_old + CNT_ONE : (d.add | CNT_ONE)) : 0u;
+    Sig<S> sg;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        sg.b[i] = d.srv == i ? sig_base<S>(d.w_new, (u32)i) : base[i];
+        sg.m[i] = sp.ms[i];
+    }
+    sig_slot<S>(sg.m, rm_old, ~0u);
+    sig_slot<S>(sg.m, rm_new, 1u);
+    sig_slot<S>(sg.m, add_old, ~0u);
+    sig_slot<S>(sg.m, add_new, 1u);
+    u32 lo, tc;
+    if (sig_rank<S>(sg, &lo, &tc)) {
+        *tied = 1;
+        return 0;
+    }
+    if (lo == sp.lo && found != d.rm) {  // same frame (rm and add never share a slot; guarded anyway)
+        u64 h = sp.h0;
+        if (d.srv >= 0) h += hS(perm_word<S>(d.w_new, lo), pe(lo, (u32)d.srv)) - sel64<S>(sp.hw, d.srv);
+        // slot mixes are not kept per parent (registers): the old slots are re-mixed
+        h += hM(perm_slot(rm_new, lo)) - hM(perm_slot(rm_old, lo));
+        h += hM(perm_slot(add_new, lo)) - hM(perm_slot(add_old, lo));
+        return h;
+    }
+    // another order: the whole successor under its own sorting permutation
+    u64 ws[S];
+    u32 mq[K + 1];
+#pragma unroll
+    for (int i = 0; i < S; ++i) ws[i] = d.srv == i ? d.w_new : w[i];
+#pragma unroll
+    for (int q = 0; q < K; ++q) mq[q] = q == found ? add_new : q == d.rm ? rm_new : m[q];
+    mq[K] = (d.has_add && found < 0) ? add_new : 0u;
+    (void)codes;
+    (void)np;
+    return fp_perm<S, K + 1>(ws, mq, lo);
 }
 
 }  // namespace rmc

@@ -436,7 +436,8 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // DIST: sharded mode — successors owned by another rank are looked up in the
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
-template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false>
+template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
+          bool ROLL = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
@@ -490,14 +491,19 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
 #pragma unroll
             for (int i = 0; i < S; ++i) sbase[i] = sig_base<S>(w[i], (u32)i);
         }
+        SymParent<S, K> spar;  // SYMMETRY, incremental keys: the parent's frame
+        if constexpr (SYMINC) sym_parent<S, K>(w, m, sbase, spar);
         u32 g = 0;
         for (int lane0 = 0; lane0 < nl; lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
-            // Rolled under SYMMETRY: one copy of the canonicalisation in flight.
-#pragma unroll(SYM ? 1 : BATCH)
+            // Rolled under SYMMETRY (one copy of the canonicalisation in flight) and
+            // with ROLL (one copy of the lane code: 8 unrolled copies of the family
+            // branch tree make a ~50 KB kernel).
+#pragma unroll((SYM || ROLL) ? 1 : BATCH)
             for (int b = 0; b < BATCH; ++b) {
                 const int lane = lane0 + b;
                 u64 key = 0;
+                int tied = 0;  // SYMMETRY: signatures tie, deferred to k_ties
                 if (lane < nl) {
                     Delta d;
                     lane_delta<S, K>(w, m, lane, P, d);
@@ -511,14 +517,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         if (en && !stutter && delta_in_model<S, K>(m, d, P)) {
                             in_model = 1;
                             if constexpr (TIEDEFER) {  // tied signatures: k_ties canonicalises it after this launch
-                                int tied = 0;
-                                h = canon_delta<S, K, true>(w, m, sbase, d, PT.code, PT.np, &tied);
-                                if (tied) {
-                                    in_model = 0;
-                                    const u64 q = atomicAdd((unsigned long long*)&B.ctr->nties, 1ull);
-                                    if (q < B.tie_cap) B.ties[q] = (lo + rel) | ((u64)lane << 56);
-                                    else atomicOr(&B.ctr->overflow, 16u);
-                                }
+                                if constexpr (SYMINC)
+                                    h = canon_delta_inc<S, K>(w, m, sbase, spar, d, PT.code, PT.np, &tied);
+                                else
+                                    h = canon_delta<S, K, true>(w, m, sbase, d, PT.code, PT.np, &tied);
+                                if (tied) in_model = 0;
                             } else {
                                 h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
                             }
@@ -535,6 +538,20 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     }
                 }
                 s_key[b][threadIdx.x] = key;
+                if constexpr (TIEDEFER) {  // one queue atomic per wave and lane, not per tied successor
+                    const u64 bal = __ballot(tied);
+                    if (bal) {
+                        const int leader = __ffsll((long long)bal) - 1;
+                        u64 q0 = 0;
+                        if (me == leader) q0 = atomicAdd((unsigned long long*)&B.ctr->nties, (unsigned long long)__popcll(bal));
+                        q0 = bcast64(q0, leader);
+                        if (tied) {
+                            const u64 q = q0 + (u64)__popcll(bal & lt_mask);
+                            if (q < B.tie_cap) B.ties[q] = (lo + rel) | ((u64)lane << 56);
+                            else atomicOr(&B.ctr->overflow, 16u);
+                        }
+                    }
+                }
             }
             // (b) BATCH independent first-slot probes in flight at once
             u64 key[BATCH], cur[BATCH];
@@ -685,13 +702,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     expand_body<S, K, false, BATCH, false, false, true>(P, PT, B, lo, hi);
 }
 
-// SYMMETRY expansion: each lane fingerprints its successor under the
-// permutation that sorts the servers by signature (canon_delta), all S! only
-// on ties.
+// Precomputed parent mixes, the delta loop rolled (one copy of the lane code).
 template <int S, int K, int BATCH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? 5 : 1))) void k_expand_sym(
+__global__ __launch_bounds__(256) void k_expand_roll(const Params P, const PermTable PT, const DevBufs B, u64 lo,
+                                                     u64 hi) {
+    expand_body<S, K, false, BATCH, false, false, true, false, true>(P, PT, B, lo, hi);
+}
+
+// SYMMETRY expansion: each lane fingerprints its successor under the
+// permutation that sorts the servers by signature, all S! only on ties
+// (deferred to k_ties).  INC: keys from the parent's frame (canon_delta_inc);
+// otherwise every lane hashes its whole permuted successor (canon_delta).
+template <int S, int K, int BATCH, bool INC, int WPE = 5>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? WPE : 1))) void k_expand_sym(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    expand_body<S, K, true, BATCH, false, false>(P, PT, B, lo, hi);
+    expand_body<S, K, true, BATCH, false, false, false, INC>(P, PT, B, lo, hi);
 }
 
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
@@ -1063,10 +1088,22 @@ static const u64 kExpandGrid = 2048;
 // Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs):
 // 1 (default) = the parent's per-component mixes precomputed once per state
 // (91 VGPRs, 5 waves/SIMD; 2.5 % faster on MCraftBench than 0, profiles/r02),
-// 0 = every lane recomputes them (77 VGPRs, 6 waves), 2 = 1 capped at 6 waves.
+// 0 = every lane recomputes them (77 VGPRs, 6 waves), 2 = 1 capped at 6 waves,
+// 3 = 1 with the delta loop rolled.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
+// SYMMETRY expansion variant (RMC_SYM_VARIANT, same-box A/B): 1 (default) =
+// incremental keys from the parent's frame, 0 = whole permuted successor,
+// 2 = 1 at 4 waves/SIMD (no spills) instead of 5.
+static int sym_variant() {
+    static int v = [] {
+        const char* e = getenv("RMC_SYM_VARIANT");
         return e ? atoi(e) : 1;
     }();
     return v;
@@ -1090,11 +1127,20 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
+            else if (sym_variant() == 1)
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
+                                   a, b);
+            else if (sym_variant() == 2)
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true, 4>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+                                   B, a, b);
             else
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
+                                   a, b);
         } else if (verify) {
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
+        } else if (expand_variant() == 3) {
+            hipLaunchKernelGGL((k_expand_roll<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         } else if (expand_variant() == 2) {
             hipLaunchKernelGGL((k_expand_pre6<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         } else if (expand_variant() == 1) {

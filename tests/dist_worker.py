@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--keys-per-dest", type=int, default=1 << 18)
     ap.add_argument("--capacity", type=int, default=0)
     ap.add_argument("--rerun", type=int, default=1)
+    ap.add_argument("--sent-cache", type=int, default=1 << 22, help="sent-cache slots per rank")
     args = ap.parse_args()
     dev = args.device if args.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "nccl":
@@ -54,7 +55,7 @@ def main():
         cfg.state_capacity = args.capacity or (1 << 26)
     with rmc.Checker(cfg) as ck:
         info = rdist.shard(ck, transport=args.transport, keys_per_dest=args.keys_per_dest,
-                           sent_cache_slots=1 << 22)
+                           sent_cache_slots=args.sent_cache)
         t0 = time.time()
         r = ck.run()  # collective: the global result on every rank
         wall = time.time() - t0

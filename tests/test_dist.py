@@ -20,11 +20,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))
 
 
-def _torchrun(nproc, args, port):
+def _torchrun(nproc, args, port, timeout=150):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
 
 TRANSPORT_WORKER = r"""
@@ -118,3 +118,23 @@ def test_sharded_violation_and_trace(case, nproc, tmp_path):
                     bug_quorum=bool(p["bug_quorum"]))
     trace = [(f, i, rmc.StateView.from_buffer_copy(bytes.fromhex(h))) for f, i, h in res["trace"]]
     check_trace(model, trace, res["violated_inv"], res["violation_depth"])
+
+
+@pytest.mark.gpu
+def test_sharded_full_bench_model_equals_single_gpu(tmp_path):
+    """The 1.23 G-state bench model (specs/MCraftBench.cfg) is beyond the
+    oracles, so the sharded search is pinned against the single-GPU one: 2
+    ranks sharing the GPU (host transport), different owner partitions and
+    table layouts, must find exactly the single-GPU counts (bench.py's
+    fp_salt_crosscheck and the verification mode pin those:
+    1,227,465,177 distinct, 21,130,972,267 generated, depth 56)."""
+    out = tmp_path / "r.json"
+    r = _torchrun(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--cfg",
+                      os.path.join(ROOT, "specs", "MCraftBench.cfg"), "--out", str(out), "--device", "0",
+                      "--backend", "gloo", "--capacity", "800000000", "--keys-per-dest", str(1 << 24),
+                      "--rerun", "0", "--sent-cache", str(1 << 28)], 29660, timeout=220)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert (res["distinct"], res["generated"], res["depth"]) == (1_227_465_177, 21_130_972_267, 56)
+    assert sum(p["stored"] for p in res["per_rank"]) == 1_227_465_177
+    assert res["keys_sent"] > 0 and res["states_sent"] > 0
