@@ -505,6 +505,79 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
     return 1;
 }
 
+// ---- wave homogeneity (the single-GPU expansion kernel) ------------------------------
+// A wave walks every action lane that ANY of its 64 states enables, so states
+// of one kind (same roles, same number of messages) should sit together.
+// succ_class: a byte that groups successors by the servers' roles and the
+// number of messages after the delta; the kernel's flush writes each batch
+// of new states sorted by it, so the next level's waves are mostly of one
+// kind.  lane_superset: the lanes a state can possibly enable (role and slot
+// occupancy only; a superset of the enabled lanes); OR-ed over a wave it is
+// the set of lanes the wave must walk.  Both are layout hints: the search is
+// the same whatever they return, as long as lane_superset is a superset.
+template <int S, int K>
+RMC_HD u32 succ_class(const u64 (&w)[S], const u32 (&m)[K], const Delta& d) {
+    int nmsg = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
+    if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
+    if (d.has_add) {
+        bool found = false;
+#pragma unroll
+        for (int q = 0; q < K; ++q) found |= m[q] && (m[q] & MSG_MASK) == d.add;
+        nmsg += found ? 0 : 1;
+    }
+    u32 roles = 0, lead = 0, cand = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const u32 st = w_st(d.srv == i ? d.w_new : w[i]);
+        roles = roles * 3u + st;
+        lead |= (st == LEADER ? 1u : 0u) << i;
+        cand |= st == CANDIDATE ? 1u : 0u;
+    }
+    if constexpr (S <= 3) return roles * 9u + (u32)(nmsg < 8 ? nmsg : 8);  // <= 242
+    return lead | (cand << S) | ((u32)(nmsg < 3 ? nmsg : 3) << (S + 1));    // S + 3 <= 8 bits
+}
+// The class of a stored state (the window sort of the expansion kernel): the
+// servers' roles, < 64 values (S <= 3: base-3 digits; else leader mask and
+// whether some server is a candidate).
+template <int S>
+RMC_HD u32 state_class(const u64* ws) {
+    u32 roles = 0, lead = 0, cand = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const u32 st = w_st(ws[i]);
+        roles = roles * 3u + st;
+        lead |= (st == LEADER ? 1u : 0u) << i;
+        cand |= st == CANDIDATE ? 1u : 0u;
+    }
+    if constexpr (S <= 3) return roles;
+    return lead | (cand << S);
+}
+template <int S, int K>
+RMC_HD u64 lane_superset(const u64 (&w)[S], const u32 (&m)[K], int V) {
+    typedef Lanes<S, K> L;
+    static_assert(L::N <= 64, "lane mask needs <= 64 lanes");
+    // constant expressions: off() is recursive, so a plain call is not folded
+    constexpr int O1 = L::off(1), O2 = L::off(2), O3 = L::off(3), O4 = L::off(4), O5 = L::off(5), O6 = L::off(6),
+                  O7 = L::off(7), O8 = L::off(8), O9 = L::off(9);
+    constexpr u64 SM = (1ull << S) - 1;
+    u64 mk = SM;  // Restart(i): always enabled
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const u32 st = w_st(w[i]);
+        if (st != LEADER) mk |= 1ull << (O1 + i);                               // Timeout
+        if (st == CANDIDATE) mk |= (SM << (O2 + i * S)) | (1ull << (O3 + i));  // RequestVote, BecomeLeader
+        if (st == LEADER)
+            mk |= (((1ull << V) - 1) << (O4 + i * VMAX)) | (1ull << (O5 + i)) |  // ClientRequest, AdvanceCommitIndex
+                  (SM << (O6 + i * S));                                        // AppendEntries
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+        if (m[q]) mk |= (1ull << (O7 + q)) | (1ull << (O8 + q)) | (1ull << (O9 + q));
+    return mk;
+}
+
 // CONSTRAINT of a delta without its fingerprint (the SYMMETRY kernels hash the
 // canonical form instead).
 template <int S, int K>

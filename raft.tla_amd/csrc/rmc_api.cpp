@@ -587,7 +587,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         c->target_idx = c->h_ctr->viol >> 4;
     }
     }  // !resume
-    const u64 CHUNK = 1ull << 26;
+    const u64 CHUNK = 1ull << 24;  // k_expand_sort keeps relative indices in 24 bits
     while (!c->have_target) {
         const u64 lo = c->level_start[depth - 1], hi = c->level_start[depth];
         if (lo == hi) break;  // fixpoint

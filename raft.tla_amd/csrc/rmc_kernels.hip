@@ -182,6 +182,82 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
     wave_sync_lds();
 }
 
+// flush_new with the batch written in succ_class order (a counting sort over
+// 256 classes in LDS, two 16-bit counters per word): consecutive new states
+// then share their roles and message count, so the waves that expand them at
+// the next level walk fewer lanes (lane_superset).  The class of each listed
+// successor rides in the top byte of its l_rel entry (launches are at most
+// 2^24 states).  Positions inside a class follow LDS atomic order; the search
+// does not depend on the layout.
+template <int S, int K>
+__device__ __forceinline__ void flush_new_sorted(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                                 const uint8_t* l_lane, u32* bins, u32 n) {
+    constexpr int NW = 2 * S + K;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    bins[me] = 0;
+    bins[me + 64] = 0;
+    wave_sync_lds();
+    for (u32 e = (u32)me; e < n; e += 64) {
+        const u32 c = l_rel[e] >> 24;
+        atomicAdd(&bins[c >> 1], 1u << (16 * (c & 1u)));
+    }
+    wave_sync_lds();
+    // exclusive scan: lane me owns counters 4me .. 4me+3 (words 2me, 2me+1)
+    const u32 wa = bins[2 * me], wb = bins[2 * me + 1];
+    const u32 c0 = wa & 0xFFFFu, c1 = wa >> 16, c2 = wb & 0xFFFFu, c3 = wb >> 16;
+    const u32 tot = c0 + c1 + c2 + c3;
+    u32 incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 v = (u32)__shfl_up((int)incl, off);
+        if (me >= off) incl += v;
+    }
+    const u32 ex = incl - tot;
+    bins[2 * me] = ex | ((ex + c0) << 16);
+    bins[2 * me + 1] = (ex + c0 + c1) | ((ex + c0 + c1 + c2) << 16);
+    wave_sync_lds();
+    u64 base = 0;
+    if (me == 0) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)n);
+    base = bcast64(base, 0);
+    for (u32 e = (u32)me; e < n; e += 64) {
+        const u32 rc = l_rel[e];
+        const u32 c = rc >> 24, sh = 16 * (c & 1u);
+        const u32 pos = (atomicAdd(&bins[c >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        const u64 rel = rc & 0xFFFFFFu;
+        const int lane = l_lane[e];
+        const u64 ni = base + pos;
+        if (ni >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, d, wo, mo);
+        store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
+        B.parent[ni] = B.ref_tag | (lo + rel);
+        B.act[ni] = (uint8_t)lane;
+        const int v = check_invariants<S, K>(wo, mo, P);
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
+    }
+    wave_sync_lds();
+}
+
+__device__ __forceinline__ u64 wave_or64(u64 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v |= (u64)(u32)__shfl_xor((int)(u32)v, off) | ((u64)(u32)__shfl_xor((int)(u32)(v >> 32), off) << 32);
+    // the same on every lane: make it a scalar so the lane dispatch stays scalar branches
+    const u32 lo = (u32)__builtin_amdgcn_readfirstlane((int)(u32)v);
+    const u32 hi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(v >> 32));
+    return ((u64)hi << 32) | lo;
+}
+
 // ---- full-state verification (RMC_FLAG_VERIFY_STATES) ---------------------------
 // TLC trusts its 64-bit fingerprints; this mode checks them.  Every successor
 // whose fingerprint is already in the set is compared, field for field, with
@@ -437,10 +513,20 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool ROLL = false>
+          bool ROLL = false, bool SORT = false, bool WSORT = false, bool FSORT = true>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
+    // SORT: class-sorted flushes + the wave walks only lane_superset's lanes
+    // WSORT: each block takes windows of 8 tiles and walks their states in
+    // state_class order (a counting sort in LDS), so its waves hold states of
+    // one kind; FSORT: flushes write new states class-sorted (flush_new_sorted)
+    static_assert(!SORT || (!SYM && !DIST && !VERIFY && !ROLL), "SORT is the plain single-GPU kernel");
+    static_assert(!WSORT || SORT, "WSORT needs SORT");
+    constexpr int WT = WSORT ? 8 : 1;  // tiles per window
+    __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
+    __shared__ uint8_t s_wcls[WSORT ? 256 * WT : 1];  // WSORT: class of each window position
+    __shared__ u32 s_wbin[WSORT ? 64 : 1];            // WSORT: class counters / cursors
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
@@ -451,6 +537,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     __shared__ u64 s_lkey[DIST ? 4 : 1][DIST ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
     __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
+    __shared__ u32 s_bins[SORT && FSORT ? 4 : 1][SORT && FSORT ? 128 : 1];  // FSORT: 256 16-bit class counters
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
     const u64 lt_mask = (1ull << me) - 1ull;
@@ -464,9 +551,50 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
     const u64 nf = hi - lo;
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
-    for (u64 tile = (u64)blockIdx.x * 256ull; tile < nf; tile += (u64)gridDim.x * 256ull) {
-        const u64 rel = tile + threadIdx.x;
-        const bool live = rel < nf;
+    for (u64 win = (u64)blockIdx.x * 256ull * WT; win < nf; win += (u64)gridDim.x * 256ull * WT) {  // block-uniform
+    u32 wn = 0;  // WSORT: states in this window
+    if constexpr (WSORT) {
+        wn = (u32)((nf - win) < 256ull * WT ? (nf - win) : 256ull * WT);
+        __syncthreads();  // the previous window's s_ord is consumed
+        if (threadIdx.x < 64) s_wbin[threadIdx.x] = 0;
+        __syncthreads();
+        for (int k = 0; k < WT; ++k) {
+            const u32 p = (u32)k * 256u + threadIdx.x;
+            if (p < wn) {
+                const u32 c = state_class<S>(reinterpret_cast<const u64*>(B.store + (lo + win + p) * (u64)NW));
+                s_wcls[p] = (uint8_t)c;
+                atomicAdd(&s_wbin[c], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 64 counters (wave 0)
+            const u32 v = s_wbin[threadIdx.x];
+            u32 incl = v;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const u32 t = (u32)__shfl_up((int)incl, off);
+                if ((int)threadIdx.x >= off) incl += t;
+            }
+            s_wbin[threadIdx.x] = incl - v;
+        }
+        __syncthreads();
+        for (int k = 0; k < WT; ++k) {
+            const u32 p = (u32)k * 256u + threadIdx.x;
+            if (p < wn) s_ord[atomicAdd(&s_wbin[s_wcls[p]], 1u)] = (uint16_t)p;
+        }
+        __syncthreads();
+    }
+    for (int wk = 0; wk < WT; ++wk) {
+        u64 rel;
+        bool live;
+        if constexpr (WSORT) {
+            const u32 p = (u32)wk * 256u + threadIdx.x;
+            live = p < wn;
+            rel = win + (live ? s_ord[p] : 0u);
+        } else {
+            rel = win + threadIdx.x;
+            live = rel < nf;
+        }
         u64 w[S];
         u32 m[K];
         if (live) {
@@ -494,14 +622,27 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         SymParent<S, K> spar;  // SYMMETRY, incremental keys: the parent's frame
         if constexpr (SYMINC) sym_parent<S, K>(w, m, sbase, spar);
         u32 g = 0;
-        for (int lane0 = 0; lane0 < nl; lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
+        // SORT: the lanes some state of this wave can enable (wave-uniform, scalar)
+        u64 wm = 0;
+        if constexpr (SORT) wm = wave_or64(live ? lane_superset<S, K>(w, m, P.V) : 0ull);
+        for (int lane0 = 0; SORT ? (wm != 0) : (lane0 < nl); lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
+            u64 lp = 0;  // SORT: this batch's lanes, 7 bits each (127 = none), a scalar
+            u64 cp = 0;  // SORT: the succ_class of each lane's successor, 8 bits each
+            if constexpr (SORT) {
+#pragma unroll
+                for (int b = 0; b < BATCH; ++b) {
+                    const u64 ln = wm ? (u64)__builtin_ctzll(wm) : 127ull;
+                    wm &= wm - 1;
+                    lp |= ln << (7 * b);
+                }
+            }
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
             // Rolled under SYMMETRY (one copy of the canonicalisation in flight) and
             // with ROLL (one copy of the lane code: 8 unrolled copies of the family
             // branch tree make a ~50 KB kernel).
 #pragma unroll((SYM || ROLL) ? 1 : BATCH)
             for (int b = 0; b < BATCH; ++b) {
-                const int lane = lane0 + b;
+                const int lane = SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b;
                 u64 key = 0;
                 int tied = 0;  // SYMMETRY: signatures tie, deferred to k_ties
                 if (lane < nl) {
@@ -529,6 +670,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     } else if (en) {
                         if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h);
                         else in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
+                        if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
                     }
                     if (in_model && (SYM || h != h0)) {
                         key = h;
@@ -652,8 +794,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 if (bal) {
                     if (is_new) {
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
-                        l_rel[pos] = (u32)rel;
-                        l_lane[pos] = (uint8_t)(lane0 + b);
+                        l_rel[pos] = (SORT && FSORT) ? (u32)rel | ((u32)(cp >> (8 * b)) << 24) : (u32)rel;
+                        l_lane[pos] = (uint8_t)(SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b);
                         if constexpr (DIST) {
                             l_dest[pos] = s_own[b][threadIdx.x];
                             l_key[pos] = key[b];
@@ -662,6 +804,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
                         if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
+                        else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
                     }
@@ -671,8 +814,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         if (live && g == 0) atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)(lo + rel));
         gen += g;
     }
+    }
     if (n) {
         if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
+        else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
     // wave reductions of the generated and probe counts, one atomic each per wave
@@ -707,6 +852,15 @@ template <int S, int K, int BATCH>
 __global__ __launch_bounds__(256) void k_expand_roll(const Params P, const PermTable PT, const DevBufs B, u64 lo,
                                                      u64 hi) {
     expand_body<S, K, false, BATCH, false, false, true, false, true>(P, PT, B, lo, hi);
+}
+
+// Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
+// class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
+template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
+    const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    if constexpr (Lanes<S, K>::N <= 64)
+        expand_body<S, K, false, BATCH, false, false, true, false, false, true, WS, FS>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1089,7 +1243,10 @@ static const u64 kExpandGrid = 2048;
 // 1 (default) = the parent's per-component mixes precomputed once per state
 // (91 VGPRs, 5 waves/SIMD; 2.5 % faster on MCraftBench than 0, profiles/r02),
 // 0 = every lane recomputes them (77 VGPRs, 6 waves), 2 = 1 capped at 6 waves,
-// 3 = 1 with the delta loop rolled.
+// 3 = 1 with the delta loop rolled, 4 = 1 with class-sorted flushes and the
+// lane-superset walk (shapes with <= 64 lanes; others run 1), 5 = 4 capped
+// at 5 waves/SIMD, 6 = the lane-superset walk over class-sorted windows of
+// 2048 states, 7 = 6 with class-sorted flushes too.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
@@ -1138,6 +1295,16 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                    a, b);
         } else if (verify) {
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+                               B, a, b);
+        } else if (expand_variant() == 4 && Lanes<S, K>::N <= 64) {
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 0>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        } else if (expand_variant() == 5 && Lanes<S, K>::N <= 64) {
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 5>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+                               B, a, b);
+        } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
         } else if (expand_variant() == 3) {
             hipLaunchKernelGGL((k_expand_roll<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
