@@ -195,7 +195,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-            "kernel": "k_expand", "kernel_ms_per_step": ks * 1e3,
+            "kernel": "k_expand_sort (librmc's default expansion kernel, RMC_EXPAND_VARIANT 6)",
+            "kernel_ms_per_step": ks * 1e3,
             "launches_per_step": nlaunch, "alg_bytes_per_launch": b_alg / nlaunch,
             "alg_bytes_per_step": b_alg, "probes_per_step": NP,
             "probe_rate_per_s": NP / ks if ks > 0 else 0.0,

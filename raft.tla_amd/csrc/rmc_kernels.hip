@@ -521,7 +521,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // WSORT: each block takes windows of 8 tiles and walks their states in
     // state_class order (a counting sort in LDS), so its waves hold states of
     // one kind; FSORT: flushes write new states class-sorted (flush_new_sorted)
-    static_assert(!SORT || (!SYM && !DIST && !VERIFY && !ROLL), "SORT is the plain single-GPU kernel");
+    static_assert(!SORT || (!DIST && !VERIFY && !ROLL), "SORT is for the single-GPU kernels");
+    static_assert(!(SORT && FSORT && SYM), "class-sorted flushes are not built for SYMMETRY");
     static_assert(!WSORT || SORT, "WSORT needs SORT");
     constexpr int WT = WSORT ? 8 : 1;  // tiles per window
     __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
@@ -551,14 +552,21 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
     const u64 nf = hi - lo;
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
-    for (u64 win = (u64)blockIdx.x * 256ull * WT; win < nf; win += (u64)gridDim.x * 256ull * WT) {  // block-uniform
+    // WSORT: tiles per window, fewer when the launch has too few states to
+    // give every block a full window (small levels would idle most blocks)
+    u64 wt = WT;
+    if constexpr (WSORT) {
+        const u64 per_block = (nf + (u64)gridDim.x * 256ull - 1) / ((u64)gridDim.x * 256ull);
+        wt = per_block < (u64)WT ? (per_block ? per_block : 1ull) : (u64)WT;
+    }
+    for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {  // block-uniform
     u32 wn = 0;  // WSORT: states in this window
     if constexpr (WSORT) {
-        wn = (u32)((nf - win) < 256ull * WT ? (nf - win) : 256ull * WT);
+        wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
         __syncthreads();  // the previous window's s_ord is consumed
         if (threadIdx.x < 64) s_wbin[threadIdx.x] = 0;
         __syncthreads();
-        for (int k = 0; k < WT; ++k) {
+        for (int k = 0; k < (int)wt; ++k) {
             const u32 p = (u32)k * 256u + threadIdx.x;
             if (p < wn) {
                 const u32 c = state_class<S>(reinterpret_cast<const u64*>(B.store + (lo + win + p) * (u64)NW));
@@ -578,13 +586,13 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             s_wbin[threadIdx.x] = incl - v;
         }
         __syncthreads();
-        for (int k = 0; k < WT; ++k) {
+        for (int k = 0; k < (int)wt; ++k) {
             const u32 p = (u32)k * 256u + threadIdx.x;
             if (p < wn) s_ord[atomicAdd(&s_wbin[s_wcls[p]], 1u)] = (uint16_t)p;
         }
         __syncthreads();
     }
-    for (int wk = 0; wk < WT; ++wk) {
+    for (int wk = 0; wk < (int)wt; ++wk) {
         u64 rel;
         bool live;
         if constexpr (WSORT) {
@@ -867,10 +875,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE :
 // permutation that sorts the servers by signature, all S! only on ties
 // (deferred to k_ties).  INC: keys from the parent's frame (canon_delta_inc);
 // otherwise every lane hashes its whole permuted successor (canon_delta).
-template <int S, int K, int BATCH, bool INC, int WPE = 5>
+// WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
+template <int S, int K, int BATCH, bool INC, int WPE = 5, bool WS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? WPE : 1))) void k_expand_sym(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    expand_body<S, K, true, BATCH, false, false, false, INC>(P, PT, B, lo, hi);
+    if constexpr (WS && Lanes<S, K>::N <= 64)
+        expand_body<S, K, true, BATCH, false, false, false, INC, false, true, true, false>(P, PT, B, lo, hi);
+    else
+        expand_body<S, K, true, BATCH, false, false, false, INC>(P, PT, B, lo, hi);
 }
 
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
@@ -1239,29 +1251,32 @@ hipError_t set_fp_salt(u64 seed, hipStream_t st) {
 
 static const u64 kExpandGrid = 2048;
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs):
-// 1 (default) = the parent's per-component mixes precomputed once per state
-// (91 VGPRs, 5 waves/SIMD; 2.5 % faster on MCraftBench than 0, profiles/r02),
-// 0 = every lane recomputes them (77 VGPRs, 6 waves), 2 = 1 capped at 6 waves,
-// 3 = 1 with the delta loop rolled, 4 = 1 with class-sorted flushes and the
-// lane-superset walk (shapes with <= 64 lanes; others run 1), 5 = 4 capped
-// at 5 waves/SIMD, 6 = the lane-superset walk over class-sorted windows of
-// 2048 states, 7 = 6 with class-sorted flushes too.
+// Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
+// profiles/r02/ab_*): 6 (default) = the lane-superset walk over class-sorted
+// windows of up to 2048 states (k_expand_sort, 4 waves/SIMD; 317 vs 343 ms per
+// MCraftBench BFS against 1; shapes with > 64 lanes run 1), 1 = the parent's
+// per-component mixes precomputed once per state (95 VGPRs, 5 waves/SIMD),
+// 0 = every lane recomputes them, 2 = 1 capped at 6 waves, 3 = 1 with the
+// delta loop rolled, 4 = the lane-superset walk with class-sorted flushes,
+// 5 = 4 capped at 5 waves, 7 = 6 with class-sorted flushes too.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 6;
     }();
     return v;
 }
 
-// SYMMETRY expansion variant (RMC_SYM_VARIANT, same-box A/B): 1 (default) =
-// incremental keys from the parent's frame, 0 = whole permuted successor,
-// 2 = 1 at 4 waves/SIMD (no spills) instead of 5.
+// SYMMETRY expansion variant (RMC_SYM_VARIANT, same-box A/B): 4 (default) =
+// whole permuted successor keys, the lane-superset walk over class-sorted
+// windows, 4 waves/SIMD (86 vs 93.5 ms on the MCraftBench bounds against 0);
+// 0 = whole permuted successor keys, every lane; 1 = incremental keys from the
+// parent's frame (canon_delta_inc; 97 ms: its registers cost more than the
+// mixes it saves), 2 = 1 at 4 waves/SIMD, 3 = 4 uncapped (3 waves/SIMD).
 static int sym_variant() {
     static int v = [] {
         const char* e = getenv("RMC_SYM_VARIANT");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 4;
     }();
     return v;
 }
@@ -1290,6 +1305,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             else if (sym_variant() == 2)
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true, 4>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                    B, a, b);
+            else if (sym_variant() == 3)
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 5, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+                                   PT, B, a, b);
+            else if (sym_variant() == 4)
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+                                   PT, B, a, b);
             else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);

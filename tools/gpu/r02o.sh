@@ -1,0 +1,11 @@
+# Round-2 checkpoint of the default build (k_expand_sort, sym variant 4):
+# full GPU suite, smoke, SYMMETRY bench, bench line, rocprof passes.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02o
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/sym_bench.py default 300000000 > $O/sym.jsonl 2> $O/sym.err || exit 1
+timeout -k 10 300 python -u bench.py > $O/bench_full.json 2> $O/bench_full.err || exit 1
+bash tools/gpu/prof_r02.sh || exit 1

@@ -35,7 +35,7 @@ def main():
         w.writerow(["Name", "Calls", "TotalDurationUs", "AverageUs", "Percentage"])
         for r in rows:
             w.writerow(r)
-    expand = [r for r in rows if "k_expand<" in r[0]]
+    expand = [r for r in rows if "k_expand" in r[0]]  # k_expand<...>, k_expand_sort<...>
     name, calls, total_us, avg_us, _pct = max(expand, key=lambda r: r[2])
 
     def counter(db, cname):
