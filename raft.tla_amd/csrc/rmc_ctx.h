@@ -28,8 +28,11 @@ struct DistState {
     rmc::u32* st_in = nullptr;      // accepted states received, blocks by source
     rmc::u64 in_cap = 0;            // keys / states receivable per chunk (all sources)
     rmc::u64* h_cnt = nullptr;      // pinned scratch: per-destination counts (2 x world)
+    void* ag_dev = nullptr;         // RCCL all-gathers of small host rows: device staging,
+    rmc::u64 ag_cap = 0;            // (world + 1) x ag_cap bytes, allocated once per shard
     std::vector<uint8_t> stage_send, stage_recv;  // host transport staging
     rmc::u64 sent_slots = 0;
+    int debug = 0;                  // RMC_DIST_DEBUG: one stderr line per chunk
     // statistics of the last run
     rmc::u64 keys_sent = 0, states_sent = 0, chunks = 0;
     double xfer_seconds = 0;        // wall time in collectives and count read-backs

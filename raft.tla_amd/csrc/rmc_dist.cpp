@@ -84,13 +84,14 @@ int allgather(rmc_ctx* c, const void* mine, u64 bytes, void* all) {
         if (D.host.allgather(D.host.user, mine, bytes, all)) return fail(c, RMC_E_HIP, "host transport allgather failed");
         return 0;
     }
-    void* d_buf = nullptr;
-    HIPCHK(c, hipMallocAsync(&d_buf, bytes * (u64)(D.world + 1), c->st));
+    const bool big = bytes > D.ag_cap;  // rows are small: the staging buffer is allocated once
+    void* d_buf = D.ag_dev;
+    if (big) HIPCHK(c, hipMallocAsync(&d_buf, bytes * (u64)(D.world + 1), c->st));
     char* d_in = (char*)d_buf + bytes * (u64)D.world;
     HIPCHK(c, hipMemcpyAsync(d_in, mine, bytes, hipMemcpyHostToDevice, c->st));
     NCCLCHK(c, ncclAllGather(d_in, d_buf, bytes, ncclUint8, D.comm, c->st));
     HIPCHK(c, hipMemcpyAsync(all, d_buf, bytes * (u64)D.world, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(c, hipFreeAsync(d_buf, c->st));
+    if (big) HIPCHK(c, hipFreeAsync(d_buf, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
     return 0;
 }
@@ -112,6 +113,9 @@ void free_dist(rmc_ctx* c) {
     (void)hipFree(D.rep_in);
     (void)hipFree(D.st_in);
     if (D.h_cnt) (void)hipHostFree(D.h_cnt);
+    (void)hipFree(D.ag_dev);
+    D.ag_dev = nullptr;
+    D.ag_cap = 0;
     if (D.comm) (void)ncclCommDestroy(D.comm);
     c->B.sent = nullptr; c->B.key_out = nullptr; c->B.tick_out = nullptr; c->B.ocount = nullptr;
     c->B.st_out = nullptr; c->B.scount = nullptr;
@@ -151,12 +155,12 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     int depth = 1;
     // level statistics, all-gathered: new, generated, probes, viol (index << 4 | bit, ~0 none),
     // deadlock index (~0 none), error flags
-    struct LevelRow { u64 nnew, gen, probes, viol, dead, err; };
+    struct LevelRow { u64 nnew, gen, probes, viol, dead, err, stored; };
     std::vector<LevelRow> rows((size_t)W);
     auto level_end = [&](u64 hi) -> int {
         const Counters& k = *c->h_ctr;
         LevelRow mine{k.count - hi, k.generated, k.probes, k.viol, k.deadlock,
-                      (u64)(k.overflow | (k.table_full ? 16u : 0u))};
+                      (u64)(k.overflow | (k.table_full ? 16u : 0u)), k.count};
         const double tx = now_s();
         if (int rc = allgather(c, &mine, sizeof mine, rows.data())) return rc;
         D.xfer_seconds += now_s() - tx;
@@ -218,6 +222,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             u64 mx = 0;
             for (int d = 0; d < W; ++d) { row[(size_t)d] = D.h_cnt[d]; if (d != me) mx = std::max(mx, D.h_cnt[d]); }
             row[(size_t)W] = (b < hi ? 1u : 0u) | (mx > kcap ? 2u : 0u);
+            if (D.debug)
+                fprintf(stderr, "[rmc rank %d] level %d chunk [%llu, %llu) of [%llu, %llu): most keys to one owner %llu (cap %llu), rho %.3f\n",
+                        me, depth, (unsigned long long)a, (unsigned long long)b, (unsigned long long)lo,
+                        (unsigned long long)hi, (unsigned long long)mx, (unsigned long long)kcap, rho);
             if (int rc = allgather(c, row.data(), 8 * ((u64)W + 1), M.data())) return rc;
             bool more = false;
             u64 ph2 = 0;  // most keys one rank sent one owner: bounds the phase-2 rounds
@@ -228,8 +236,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 more |= (f & 1u) != 0;
                 for (int d = 0; d < W; ++d) if (d != r) ph2 = std::max(ph2, M[(size_t)r * (W + 1) + d]);
             }
-            if (a < b) {  // adapt the chunk: the fullest outbox stays at most half full
-                rho = std::max(0.05, (double)std::max<u64>(mx, 1) / (double)(b - a));
+            if (a < b) {  // adapt the chunk: the fullest outbox stays at most half full; rho falls
+                          // at most by half per chunk (a chunk of one kind of state says little
+                          // about the next), and rises at once
+                rho = std::max({0.05, rho * 0.5, (double)std::max<u64>(mx, 1) / (double)(b - a)});
             }
             // ---- phase 1: keys to their owners, replies back
             u64 tot_in = 0;
@@ -308,13 +318,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 }
         {  // progress: the same collectives on every rank, with or without a callback;
            // all ranks stop together when rank 0's callback asks to
-            u64 mine = c->h_ctr->count;
-            std::vector<u64> all((size_t)W);
-            if (int rc = allgather(c, &mine, 8, all.data())) return rc;
             rmc_level_stats ls{};
             ls.level = nnew ? depth - 1 : depth;
             ls.generated = generated;
-            for (u64 x : all) ls.distinct += x;
+            for (const auto& r : rows) ls.distinct += r.stored;
             ls.new_states = nnew;
             ls.seconds = now_s() - t0;
             const int stop = (cb && cb(&ls, user)) ? 1 : 0;
@@ -437,10 +444,13 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
         hipMalloc(&c->B.st_out, W * scap * RB) != hipSuccess || hipMalloc(&c->B.scount, 8 * W) != hipSuccess ||
         hipMalloc(&D.key_in, W * kcap * 8) != hipSuccess || hipMalloc(&D.rep_out, W * kcap) != hipSuccess ||
         hipMalloc(&D.rep_in, W * kcap) != hipSuccess || hipMalloc(&D.st_in, W * scap * RB) != hipSuccess ||
-        hipHostMalloc(&D.h_cnt, 16 * W, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&D.h_cnt, 16 * W, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&D.ag_dev, 4096 * (W + 1)) != hipSuccess) {
         free_dist(c);
         return fail(c, RMC_E_NOMEM, "sharded-mode buffers do not fit (lower keys_per_dest / sent_cache_slots)");
     }
+    D.ag_cap = 4096;
+    D.debug = getenv("RMC_DIST_DEBUG") != nullptr;
     c->B.smask = slots - 1;
     c->B.kcap = kcap;
     c->B.scap = scap;

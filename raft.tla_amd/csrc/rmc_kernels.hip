@@ -521,8 +521,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // WSORT: each block takes windows of 8 tiles and walks their states in
     // state_class order (a counting sort in LDS), so its waves hold states of
     // one kind; FSORT: flushes write new states class-sorted (flush_new_sorted)
-    static_assert(!SORT || (!DIST && !VERIFY && !ROLL), "SORT is for the single-GPU kernels");
-    static_assert(!(SORT && FSORT && SYM), "class-sorted flushes are not built for SYMMETRY");
+    static_assert(!SORT || (!VERIFY && !ROLL), "SORT: not with verification or the rolled loop");
+    static_assert(!(SORT && FSORT && (SYM || DIST)), "class-sorted flushes are built for the plain kernel only");
     static_assert(!WSORT || SORT, "WSORT needs SORT");
     constexpr int WT = WSORT ? 8 : 1;  // tiles per window
     __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
@@ -886,10 +886,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K
 }
 
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
-template <int S, int K, int BATCH>
+// WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
+template <int S, int K, int BATCH, bool WS>
 __global__ __launch_bounds__(256) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
+    if constexpr (WS && Lanes<S, K>::N <= 64)
+        expand_body<S, K, false, BATCH, true, false, false, false, false, true, true, false>(P, PT, B, lo, hi);
+    else
+        expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
 
 // Sharded mode, phase 1, owner side: insert the keys other ranks sent;
@@ -1281,6 +1285,16 @@ static int sym_variant() {
     return v;
 }
 
+// Sharded expansion variant (RMC_DIST_VARIANT): 1 (default) = the lane-superset
+// walk over class-sorted windows, 0 = every lane.
+static int dist_variant() {
+    static int v = [] {
+        const char* e = getenv("RMC_DIST_VARIANT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 // Probes in flight per thread: 8 (measured best of 4/8 on MI355X).
 constexpr int kBatch = 8;
 
@@ -1342,7 +1356,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         if constexpr (SYM)
             hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         else
-            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+            if (dist_variant() == 1)
+                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                                   b);
+            else
+                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                                   b);
     } else if (which == 8) {  // a = keys per destination block (max); out = replies
         hipLaunchKernelGGL((k_materialize_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B,
                            reinterpret_cast<const uint8_t*>(in), a, b);
