@@ -188,7 +188,13 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     std::vector<u64> M((size_t)W * (W + 1)), soff((size_t)W), scnt((size_t)W), roff((size_t)W), rcnt((size_t)W);
     std::vector<u64> row((size_t)W + 1);
     const u64 nl = (u64)c->P.off[10];
-    double rho = (double)nl;  // most keys for one owner per expanded state (adapted)
+    // Chunk sizing: rho = most keys one chunk sends one owner, per expanded
+    // state.  It varies along a frontier (states received from other ranks are
+    // appended after the local ones, and are of another kind) by up to ~1.6x
+    // within a level (RMC_DIST_DEBUG logs of the bench model), so a chunk is sized
+    // from the worst rho of the previous level and of this level so far, for an
+    // outbox at most 40 % full.  An overflow is an error, never a silent drop.
+    double rho_prev = (double)nl;
     while (!c->have_target) {
         const u64 lo = c->level_start[(size_t)depth - 1], hi = c->level_start[(size_t)depth];
         if (c->cfg.max_depth > 0 && depth >= c->cfg.max_depth) {
@@ -201,8 +207,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         }
         if (int rc = reset_counters(c, true)) return rc;
         u64 cursor = lo;
+        double rho_lvl = 0;
         for (;;) {  // chunks: every rank takes part until no rank has frontier left
-            const u64 chunk = std::max<u64>(1, (u64)((double)kcap / (2.0 * rho + 1e-9)));
+            const double rho = std::max({0.05, rho_prev, rho_lvl});
+            const u64 chunk = std::max<u64>(1, (u64)((double)kcap / (2.5 * rho)));
             const u64 a = cursor, b = std::min(hi, a + chunk);
             HIPCHK(c, hipMemsetAsync(c->B.ocount, 0, 8 * (u64)W, c->st));
             if (a < b) {
@@ -236,11 +244,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 more |= (f & 1u) != 0;
                 for (int d = 0; d < W; ++d) if (d != r) ph2 = std::max(ph2, M[(size_t)r * (W + 1) + d]);
             }
-            if (a < b) {  // adapt the chunk: the fullest outbox stays at most half full; rho falls
-                          // at most by half per chunk (a chunk of one kind of state says little
-                          // about the next), and rises at once
-                rho = std::max({0.05, rho * 0.5, (double)std::max<u64>(mx, 1) / (double)(b - a)});
-            }
+            if (a < b) rho_lvl = std::max(rho_lvl, (double)std::max<u64>(mx, 1) / (double)(b - a));
             // ---- phase 1: keys to their owners, replies back
             u64 tot_in = 0;
             for (int p = 0; p < W; ++p) {
@@ -294,6 +298,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             cursor = b;
             if (!more) break;
         }
+        if (rho_lvl > 0) rho_prev = rho_lvl;
         if (int rc = read_counters(c)) return rc;
         if (int rc = level_end(hi)) return rc;
         u64 nnew = 0, gen = 0, pr = 0;
