@@ -513,7 +513,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool ROLL = false, bool SORT = false, bool WSORT = false, bool FSORT = true>
+          bool ROLL = false, bool SORT = false, bool WSORT = false, bool FSORT = true, bool WCAP5 = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
@@ -531,7 +531,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
-    constexpr int LCAP = DIST ? 256 : WCAP;
+    constexpr int LCAP = DIST ? 256 : (WSORT && WCAP5) ? 384 : WCAP;
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
     __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? LCAP : 1];
@@ -867,8 +867,10 @@ __global__ __launch_bounds__(256) void k_expand_roll(const Params P, const PermT
 template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+    // at 5 waves/SIMD the window-sorted kernel keeps 384-entry lists (LDS for 5 blocks per CU)
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, false, true, WS, FS>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, false, true, WS, FS, WS && WPE == 5>(P, PT, B, lo,
+                                                                                                      hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1262,7 +1264,8 @@ static const u64 kExpandGrid = 2048;
 // per-component mixes precomputed once per state (95 VGPRs, 5 waves/SIMD),
 // 0 = every lane recomputes them, 2 = 1 capped at 6 waves, 3 = 1 with the
 // delta loop rolled, 4 = the lane-superset walk with class-sorted flushes,
-// 5 = 4 capped at 5 waves, 7 = 6 with class-sorted flushes too.
+// 5 = 4 capped at 5 waves, 7 = 6 with class-sorted flushes too, 8 = 6 capped
+// at 5 waves/SIMD with 384-entry lists.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
@@ -1337,6 +1340,9 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 5>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+                               B, a, b);
+        } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 5, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
