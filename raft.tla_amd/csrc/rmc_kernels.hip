@@ -513,7 +513,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool ROLL = false, bool SORT = false, bool WSORT = false, bool FSORT = true, bool WCAP5 = false>
+          bool SORT = false, bool WSORT = false, bool FSORT = true>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     constexpr int NW = 2 * S + K;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
@@ -521,7 +521,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // WSORT: each block takes windows of 8 tiles and walks their states in
     // state_class order (a counting sort in LDS), so its waves hold states of
     // one kind; FSORT: flushes write new states class-sorted (flush_new_sorted)
-    static_assert(!SORT || (!VERIFY && !ROLL), "SORT: not with verification or the rolled loop");
+    static_assert(!SORT || !VERIFY, "SORT: not with verification");
     static_assert(!(SORT && FSORT && (SYM || DIST)), "class-sorted flushes are built for the plain kernel only");
     static_assert(!WSORT || SORT, "WSORT needs SORT");
     constexpr int WT = WSORT ? 8 : 1;  // tiles per window
@@ -531,7 +531,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
-    constexpr int LCAP = DIST ? 256 : (WSORT && WCAP5) ? 384 : WCAP;
+    constexpr int LCAP = DIST ? 256 : WCAP;
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
     __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? LCAP : 1];
@@ -645,10 +645,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 }
             }
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
-            // Rolled under SYMMETRY (one copy of the canonicalisation in flight) and
-            // with ROLL (one copy of the lane code: 8 unrolled copies of the family
-            // branch tree make a ~50 KB kernel).
-#pragma unroll((SYM || ROLL) ? 1 : BATCH)
+            // Rolled under SYMMETRY: one copy of the canonicalisation in flight.
+            // (Rolling the plain kernel too, one copy of the lane code instead of
+            // 8, measured no difference: instruction-cache misses are ~1e-5.)
+#pragma unroll(SYM ? 1 : BATCH)
             for (int b = 0; b < BATCH; ++b) {
                 const int lane = SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b;
                 u64 key = 0;
@@ -848,29 +848,13 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
     expand_body<S, K, SYM, BATCH, DIST, VERIFY, PRE>(P, PT, B, lo, hi);
 }
 
-// Precomputed parent mixes at 6 waves/SIMD (91 VGPRs unconstrained = 5 waves).
-template <int S, int K, int BATCH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_expand_pre6(
-    const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    expand_body<S, K, false, BATCH, false, false, true>(P, PT, B, lo, hi);
-}
-
-// Precomputed parent mixes, the delta loop rolled (one copy of the lane code).
-template <int S, int K, int BATCH>
-__global__ __launch_bounds__(256) void k_expand_roll(const Params P, const PermTable PT, const DevBufs B, u64 lo,
-                                                     u64 hi) {
-    expand_body<S, K, false, BATCH, false, false, true, false, true>(P, PT, B, lo, hi);
-}
-
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
 template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    // at 5 waves/SIMD the window-sorted kernel keeps 384-entry lists (LDS for 5 blocks per CU)
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, false, true, WS, FS, WS && WPE == 5>(P, PT, B, lo,
-                                                                                                      hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -882,7 +866,7 @@ template <int S, int K, int BATCH, bool INC, int WPE = 5, bool WS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? WPE : 1))) void k_expand_sym(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, true, BATCH, false, false, false, INC, false, true, true, false>(P, PT, B, lo, hi);
+        expand_body<S, K, true, BATCH, false, false, false, INC, true, true, false>(P, PT, B, lo, hi);
     else
         expand_body<S, K, true, BATCH, false, false, false, INC>(P, PT, B, lo, hi);
 }
@@ -893,7 +877,7 @@ template <int S, int K, int BATCH, bool WS>
 __global__ __launch_bounds__(256) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, false, false, false, true, true, false>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, false, false, true, true, false>(P, PT, B, lo, hi);
     else
         expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
@@ -1258,14 +1242,14 @@ hipError_t set_fp_salt(u64 seed, hipStream_t st) {
 static const u64 kExpandGrid = 2048;
 
 // Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
-// profiles/r02/ab_*): 6 (default) = the lane-superset walk over class-sorted
+// profiles/r02/ab/): 6 (default) = the lane-superset walk over class-sorted
 // windows of up to 2048 states (k_expand_sort, 4 waves/SIMD; 317 vs 343 ms per
-// MCraftBench BFS against 1; shapes with > 64 lanes run 1), 1 = the parent's
-// per-component mixes precomputed once per state (95 VGPRs, 5 waves/SIMD),
-// 0 = every lane recomputes them, 2 = 1 capped at 6 waves, 3 = 1 with the
-// delta loop rolled, 4 = the lane-superset walk with class-sorted flushes,
-// 5 = 4 capped at 5 waves, 7 = 6 with class-sorted flushes too, 8 = 6 capped
-// at 5 waves/SIMD with 384-entry lists.
+// MCraftBench BFS against 1; shapes with > 64 lanes run 1), 1 = every lane of
+// every state, the parent's per-component mixes precomputed (k_expand, 95
+// VGPRs, 5 waves/SIMD), 4 = the lane-superset walk with class-sorted flushes
+// instead of windows (322 ms).  Measured and removed: mixes recomputed per lane
+// (−2.5 %), 6 waves/SIMD, the delta loop rolled, 5-wave caps of 4 and 6 (spills),
+// flushes and windows both sorted.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
@@ -1277,9 +1261,9 @@ static int expand_variant() {
 // SYMMETRY expansion variant (RMC_SYM_VARIANT, same-box A/B): 4 (default) =
 // whole permuted successor keys, the lane-superset walk over class-sorted
 // windows, 4 waves/SIMD (86 vs 93.5 ms on the MCraftBench bounds against 0);
-// 0 = whole permuted successor keys, every lane; 1 = incremental keys from the
-// parent's frame (canon_delta_inc; 97 ms: its registers cost more than the
-// mixes it saves), 2 = 1 at 4 waves/SIMD, 3 = 4 uncapped (3 waves/SIMD).
+// 0 = whole permuted successor keys, every lane (5 waves/SIMD); 1 = incremental
+// keys from the parent's frame (canon_delta_inc; 97 ms: its registers cost more
+// than the mixes it saves).
 static int sym_variant() {
     static int v = [] {
         const char* e = getenv("RMC_SYM_VARIANT");
@@ -1319,12 +1303,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             else if (sym_variant() == 1)
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
-            else if (sym_variant() == 2)
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true, 4>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
-                                   B, a, b);
-            else if (sym_variant() == 3)
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 5, true>), dim3((unsigned)g), dim3(256), 0, st, P,
-                                   PT, B, a, b);
             else if (sym_variant() == 4)
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
@@ -1336,27 +1314,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                B, a, b);
         } else if (expand_variant() == 4 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 0>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 5 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 5>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
         } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
-        } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 5, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
-                               B, a, b);
-        } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
-                               B, a, b);
-        } else if (expand_variant() == 3) {
-            hipLaunchKernelGGL((k_expand_roll<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 2) {
-            hipLaunchKernelGGL((k_expand_pre6<S, K, kBatch>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 1) {
+        } else {  // 1, and shapes with more than 64 lanes
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3((unsigned)g), dim3(256), 0, st,
                                P, PT, B, a, b);
-        } else {
-            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
-                               b);
         }
     } else if (which == 3) {
         if constexpr (SYM)
