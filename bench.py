@@ -118,6 +118,7 @@ def main():
             dist.barrier()
 
     last = [None]
+    transport_used = [None]  # sharded: "rccl" (librmc's communicator) or "host" (gloo)
 
     def one_run(ck, first):
         # sharded: rmc_run_bfs is a collective inside librmc (two-phase
@@ -129,7 +130,9 @@ def main():
     with rmc.Checker(cfg) as ck:
         if sharded:
             from rmc import dist as rdist
-            rdist.shard(ck, transport=a.transport, keys_per_dest=a.keys_per_dest, sent_cache_slots=a.sent_cache)
+            info = rdist.shard(ck, transport=a.transport, keys_per_dest=a.keys_per_dest,
+                               sent_cache_slots=a.sent_cache)
+            transport_used[0] = info.transport
         first = True
         for _ in range(a.warmup):
             one_run(ck, first)
@@ -189,7 +192,9 @@ def main():
                         f"{cfg.max_log_len} MaxMsgs={cfg.max_msgs} MaxDup={cfg.max_dup}, BFS to fixpoint",
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
-            "parallelism": f"state-space sharded x{world} (librmc two-phase exchange, RCCL)" if sharded else "single GPU",
+            "parallelism": (f"state-space sharded x{world} (librmc two-phase exchange, "
+                            f"{'RCCL' if transport_used[0] == 'rccl' else 'host transport over gloo'})")
+                           if sharded else "single GPU",
             "fp_salt_crosscheck": salt_check,
         },
         "roofline": {
@@ -207,7 +212,7 @@ def main():
     if sharded:
         ld = last[0]
         out["sharded"] = {"in_library": "rmc_shard + rmc_run_bfs (two-phase fingerprint-first exchange)",
-                          "transport": a.transport, "chunks_rank0": ld.chunks, "keys_sent_rank0": ld.keys_sent,
+                          "transport": transport_used[0], "chunks_rank0": ld.chunks, "keys_sent_rank0": ld.keys_sent,
                           "states_sent_rank0": ld.states_sent, "stored_rank0": ld.stored_here,
                           "exchange_s_rank0": round(ld.exchange_seconds, 6), "keys_per_dest": a.keys_per_dest}
         out["roofline"]["note"] = "per-rank kernel time of rank 0; achieved is rank 0's share"
