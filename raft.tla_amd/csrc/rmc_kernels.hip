@@ -522,6 +522,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // state_class order (a counting sort in LDS), so its waves hold states of
     // one kind; FSORT: flushes write new states class-sorted (flush_new_sorted)
     static_assert(!SORT || !VERIFY, "SORT: not with verification");
+    static_assert(!SORT || BATCH * 7 <= 64, "SORT packs a batch's lanes 7 bits each into one u64");
     static_assert(!(SORT && FSORT && (SYM || DIST)), "class-sorted flushes are built for the plain kernel only");
     static_assert(!WSORT || SORT, "WSORT needs SORT");
     constexpr int WT = WSORT ? 8 : 1;  // tiles per window
