@@ -1240,7 +1240,15 @@ hipError_t set_fp_salt(u64 seed, hipStream_t st) {
     return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &salt, sizeof salt, 0, hipMemcpyHostToDevice, st);
 }
 
-static const u64 kExpandGrid = 2048;
+// Blocks of the grid-stride kernels (RMC_EXPAND_GRID for A/B runs; default 2048).
+static u64 expand_grid() {
+    static u64 v = [] {
+        const char* e = getenv("RMC_EXPAND_GRID");
+        const long long x = e ? atoll(e) : 0;
+        return x >= 64 && x <= (1 << 20) ? (u64)x : (u64)2048;
+    }();
+    return v;
+}
 
 // Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
 // profiles/r02/ab/): 6 (default) = the lane-superset walk over class-sorted
@@ -1295,7 +1303,8 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs
-    const u64 g = blocks < kExpandGrid ? blocks : kExpandGrid;
+    const u64 grid = expand_grid();
+    const u64 g = blocks < grid ? blocks : grid;
     if (which == 0) {
         if constexpr (SYM) {
             if (verify)
