@@ -8,10 +8,18 @@ With N > 1 ranks the state space is sharded over the GPUs inside librmc
 (rmc_shard: owner-routed successors, fingerprint-first two-phase exchange
 over librmc's own RCCL communicator) and the SAME model is searched, so
 scaling is strong.
+
+Launch: `python bench.py --gpus N` starts its own N rank processes (before
+anything touches a GPU) when no outer launcher set WORLD_SIZE; under
+`torch.distributed.run --nproc-per-node N` every process is one rank.  A line
+whose rank count differs from --gpus is refused.
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -19,13 +27,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "raft.tla_amd"))
 
-import rmc  # noqa: E402
-
 METRIC = "distinct states/sec (whole node) and time-to-fixpoint on MCraft BFS, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -33,40 +39,163 @@ def parse():
     ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBench.cfg"))
     ap.add_argument("--capacity", type=int, default=0,
                     help="state capacity per GPU (0 = 1.5e9 / world * 1.3 for the bench model)")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
-    ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK (one GPU per rank)")
-    ap.add_argument("--keys-per-dest", type=int, default=1 << 25,
-                    help="sharded mode: phase-1 keys one chunk may send one owner")
+    ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK modulo the visible GPUs")
+    ap.add_argument("--keys-per-dest", type=int, default=0,
+                    help="sharded mode: phase-1 keys one chunk may send one owner (0 = librmc's choice)")
     ap.add_argument("--sent-cache", type=int, default=1 << 30,
                     help="sharded mode: slots of the per-rank cache of fingerprints already sent")
-    ap.add_argument("--transport", default="auto", help="sharded mode: rccl | host | auto")
+    ap.add_argument("--transport", default="auto",
+                    help="sharded mode: rccl | host | auto (rccl when every rank has its own GPU, "
+                         "else the host transport over gloo)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the sharded path even at one rank (measures its overhead)")
     ap.add_argument("--no-probe-ceiling", action="store_true",
                     help="skip the random-probe microbenchmark (roofline ceiling)")
     ap.add_argument("--cpu-levels", type=int, default=22,
                     help="BFS levels of the same model timed on the host CPU oracle")
+    ap.add_argument("--cpu-fixpoint", default=os.path.join(ROOT, "specs", "MCraftBounded.cfg"),
+                    help="model timed to its fixpoint on the host CPU oracle AND on the GPU "
+                         "('' to skip)")
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch logic only: ranks rendezvous over gloo and report, no GPU, no librmc")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="self-launch: seconds before the rank processes are killed")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(cfg, levels):
-    """C oracle (test infrastructure, kind "port") on a bounded sample of the
-    same model: its first `levels` BFS levels, on the host's cores."""
+# ---- self-launch ---------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a, argv):
+    """Start N rank processes of this script (torchrun's env contract: RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT) and relay rank 0's JSON line.
+    Runs before anything in this process touches a GPU or loads librmc."""
+    n = a.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), RMC_BENCH_LAUNCHER="bench.py --gpus (self-launch)")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+    t0 = time.time()
+    out = b""
+    try:
+        out = procs[0].communicate(timeout=a.launch_timeout)[0]
+        for p in procs[1:]:
+            p.wait(timeout=max(10.0, a.launch_timeout - (time.time() - t0)))
+    except subprocess.TimeoutExpired:
+        pass
+    rcs = [p.poll() for p in procs]
+    if any(rc is None for rc in rcs) or any(rcs):
+        for p in procs:  # end every rank's process group: a failed rank leaves the others in a collective
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, 9)
+                except ProcessLookupError:
+                    pass
+            p.wait()
+        sys.stderr.write(f"bench.py: rank exit codes {rcs}; no result line\n")
+        return 1
+    lines = [ln for ln in out.decode().splitlines() if ln.startswith("{")]
+    if len(lines) != 1:
+        sys.stderr.write("bench.py: rank 0 printed no result line\n")
+        return 1
+    rec = json.loads(lines[0])
+    if rec.get("n_gpus") != n:
+        sys.stderr.write(f"bench.py: rank 0 reports {rec.get('n_gpus')} ranks, --gpus {n}: refused\n")
+        return 1
+    sys.stdout.write(json.dumps(rec) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+# ---- CPU baseline ----------------------------------------------------------------
+def host_cpu_info():
+    """Cores this process may use (affinity, then the cgroup quota), plus what
+    the machine shows: SURVEY.md §8d asks for nproc, physical cores and model."""
+    nproc = os.cpu_count() or 1
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = nproc
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    usable = min(allowed, quota) if quota else allowed
+    model, phys = platform.processor() or "?", set()
+    try:
+        cur = {}
+        for ln in open("/proc/cpuinfo"):
+            if ":" in ln:
+                k, v = (x.strip() for x in ln.split(":", 1))
+                if k == "model name":
+                    model = v
+                cur[k] = v
+            elif cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity_cpus": allowed, "cgroup_quota_cpus": quota, "usable": usable,
+            "physical_cores": len(phys) or None, "model": model}
+
+
+def cpu_baseline(cfg, levels, fix_cfg, gpu_fix):
+    """C oracle (test infrastructure, kind "port") on the host cores this job
+    may use: (1) the first `levels` BFS levels of the bench model, (2) a
+    complete fixpoint of `fix_cfg` timed next to the GPU on the same model."""
+    import rmc
     from tests import oracle_c
-    threads = max(1, min(16, os.cpu_count() or 1))
-    r, _ln, _lg = oracle_c.bfs(cfg.n_servers, cfg.n_values, cfg.max_term, cfg.max_log_len,
-                               cfg.max_msgs, cfg.max_dup, bug=int(bool(cfg.flags & rmc.FLAG_BUG_QUORUM)),
-                               inv=cfg.invariants, sym=int(bool(cfg.flags & rmc.FLAG_SYMMETRY)),
-                               threads=threads, max_levels=levels, capacity=1 << 27)
-    return {"value": r.distinct / r.seconds, "unit": "distinct states/s", "cores": threads,
-            "kind": "port",
-            "sample": f"C oracle (oracle/rmc_oracle.c, exact state set) BFS levels 1..{r.depth} of the "
-                      f"same model: {r.distinct} distinct / {r.generated} generated in {r.seconds:.2f} s"}
+    info = host_cpu_info()
+    threads = info["usable"]
+
+    def run(c, max_levels, capacity):
+        return oracle_c.bfs(c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,
+                            bug=int(bool(c.flags & rmc.FLAG_BUG_QUORUM)), inv=c.invariants,
+                            sym=int(bool(c.flags & rmc.FLAG_SYMMETRY)), threads=threads,
+                            max_levels=max_levels, capacity=capacity)[0]
+
+    r = run(cfg, levels, 1 << 27)
+    out = {"value": r.distinct / r.seconds, "unit": "distinct states/s", "cores": threads, "kind": "port",
+           "host": info,
+           "sample": f"C oracle (oracle/rmc_oracle.c, exact state set, {threads} threads) BFS levels 1..{r.depth} "
+                     f"of the same model: {r.distinct} distinct / {r.generated} generated in {r.seconds:.2f} s"}
+    if fix_cfg is not None:
+        f = run(fix_cfg, 0, 1 << 27)
+        gd, gg, gdep, gt = gpu_fix
+        out["fixpoint"] = {
+            "model": gpu_fix_name(fix_cfg), "cpu_distinct": f.distinct, "cpu_generated": f.generated,
+            "cpu_depth": f.depth, "cpu_seconds": f.seconds, "cpu_rate": f.distinct / f.seconds,
+            "gpu_distinct": gd, "gpu_generated": gg, "gpu_depth": gdep, "gpu_seconds": gt,
+            "gpu_rate": gd / gt if gt > 0 else None,
+            "agree": (f.distinct, f.generated, f.depth) == (gd, gg, gdep),
+            "gpu_over_cpu": (f.seconds / gt) if gt > 0 else None}
+    return out
+
+
+def gpu_fix_name(c):
+    return (f"S={c.n_servers} V={c.n_values} MaxTerm={c.max_term} MaxLogLen={c.max_log_len} "
+            f"MaxMsgs={c.max_msgs} MaxDup={c.max_dup}")
 
 
 def pmc_traffic(config_path):
-    """HBM bytes per k_expand launch from the committed rocprofv3 PMC profile
+    """HBM bytes per expansion launch from the committed rocprofv3 PMC profile
     of this same command (profiles/<round>/pmc_traffic_<cfg>.json): PMC
     counters cannot be read live inside the timed run."""
     stem = os.path.splitext(os.path.basename(config_path))[0]
@@ -80,19 +209,59 @@ def pmc_traffic(config_path):
     return None, None
 
 
-def main():
-    a = parse()
+# ---- one rank ------------------------------------------------------------------
+def dry_run(a, world, rank):
+    """Rendezvous + the timing collectives of a real run, without a GPU."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid(),
+                                       "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+        t = torch.tensor([0.001 * (rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.destroy_process_group()
+    else:
+        ranks, dt = [{"rank": 0, "pid": os.getpid(), "local_rank": 0}], 0.001
+    return {"metric": METRIC, "value": 0.0, "unit": "distinct states/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u64", "data": "dry run: launch logic only, nothing measured",
+            "config": {"workload": "dry run"}, "dry_run": True, "ranks_seen": ranks,
+            "launcher": os.environ.get("RMC_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                       else "single process")}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return self_launch(a, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        sys.stderr.write(f"bench.py: {world} ranks but --gpus {a.gpus}: refused (no line printed)\n")
+        return 2
     # The JSON line is the only thing on stdout: libraries that print banners
     # there (RCCL prints its version block at communicator init) are sent to
     # stderr by pointing fd 1 at fd 2 for the rest of the run.
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        out = dry_run(a, world, rank)
+        if rank == 0:
+            os.write(json_fd, (json.dumps(out) + "\n").encode())
+        return 0
+
+    import rmc
     dist = None
     sharded = world > 1 or a.force_dist
+    ndev = 1
+    transport = "none"
+    backend = None
     if sharded:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -100,70 +269,90 @@ def main():
         os.environ.setdefault("WORLD_SIZE", "1")
         import torch
         import torch.distributed as dist
-        dev = a.device if a.device >= 0 else local
-        torch.cuda.set_device(dev)
-        dist.init_process_group(a.dist_backend, init_method="env://")
+        ndev = max(1, torch.cuda.device_count())  # does not initialise the GPU on this image
+        shared = ndev < world
+        transport = a.transport
+        if transport == "auto":
+            transport = "host" if shared else "rccl"
+        if transport == "rccl" and shared:
+            sys.stderr.write(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
+                             "(use --transport host)\n")
+            return 2
+        dev = a.device if a.device >= 0 else local % ndev
+        backend = "nccl" if transport == "rccl" else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(dev)
+        dist.init_process_group(backend, init_method="env://")
+    else:
+        dev = max(a.device, 0)
     # the GPU box has no raft.tla: the bench model checks the compiled-in lemmy/raft.tla
     cfg = rmc.config_from_files(a.config, builtin_raft=True)
-    cfg.device = (a.device if a.device >= 0 else local) if sharded else max(a.device, 0)
+    cfg.device = dev
+    ranks_per_gpu = max(1, -(-world // ndev)) if sharded else 1
     cfg.state_capacity = a.capacity or int(1.5e9 / world * (1.3 if sharded else 1.0))
     W = rmc.native().rmc_state_bytes(cfg)
     # roofline ceiling of the fingerprint set: random 8-B probes over 64 GB
     r_max = None
-    if not a.no_probe_ceiling and world == 1:
-        r_max = rmc.probe_bench(device=cfg.device, table_bytes=64 << 30, accesses=1 << 32, mode=0)
+    if not a.no_probe_ceiling and ranks_per_gpu == 1 and rank == 0:
+        r_max = rmc.probe_bench(device=cfg.device, table_bytes=(64 << 30) // ranks_per_gpu,
+                                accesses=1 << 32, mode=0)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     last = [None]
-    transport_used = [None]  # sharded: "rccl" (librmc's communicator) or "host" (gloo)
 
-    def one_run(ck, first):
-        # sharded: rmc_run_bfs is a collective inside librmc (two-phase
-        # exchange over its own RCCL communicator); the result is global
-        r = ck.run()
+    def one_run(ck):
+        # sharded: rmc_run_bfs is a collective inside librmc; the result is global
+        r = ck.run(record_levels=False)
         last[0] = r
         return r.distinct, r.generated, r.depth, r.probes, r.expand_kernel_seconds, r.expand_launches
 
     with rmc.Checker(cfg) as ck:
         if sharded:
             from rmc import dist as rdist
-            info = rdist.shard(ck, transport=a.transport, keys_per_dest=a.keys_per_dest,
+            info = rdist.shard(ck, transport=transport, keys_per_dest=a.keys_per_dest,
                                sent_cache_slots=a.sent_cache)
-            transport_used[0] = info.transport
-        first = True
+            transport = info.transport
         for _ in range(a.warmup):
-            one_run(ck, first)
-            first = False
+            one_run(ck)
         barrier()
         if dist is not None:
             import torch
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         kern = 0.0
         launches = 0
         for _ in range(a.steps):
-            D, G, depth, NP, ks, nl = one_run(ck, first)
-            first = False
+            D, G, depth, NP, ks, nl = one_run(ck)
             kern += ks
             launches += nl
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize(dev)
         barrier()
         dt = time.perf_counter() - t0
         salt_check = None
         if not sharded:  # untimed: same search under another fingerprint salt
             ck.set_seed(0x5A17ED)
-            r2 = ck.run()
+            r2 = ck.run(record_levels=False)
             ck.set_seed(0)
             salt_check = {"salt": 0x5A17ED, "distinct": r2.distinct, "generated": r2.generated,
                           "depth": r2.depth,
                           "agrees": (r2.distinct, r2.generated, r2.depth) == (D, G, depth)}
+    per_rank = None
     if dist is not None:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        ld = last[0]
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "device": dev, "stored": ld.stored_here,
+                                          "keys_sent": ld.keys_sent, "states_sent": ld.states_sent,
+                                          "chunks": ld.chunks, "exchange_s": round(ld.exchange_seconds, 6),
+                                          "kernel_s": round(ld.expand_kernel_seconds, 6)})
     per_step = dt / a.steps
     # algorithmic bytes per run (DESIGN.md "Roofline"): one random 64-B granule
     # per fingerprint probe + the new state written, read back as frontier,
@@ -193,14 +382,20 @@ def main():
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
             "parallelism": (f"state-space sharded x{world} (librmc two-phase exchange, "
-                            f"{'RCCL' if transport_used[0] == 'rccl' else 'host transport over gloo'})")
+                            f"{'RCCL over xGMI' if transport == 'rccl' else 'host transport over gloo'})")
                            if sharded else "single GPU",
             "fp_salt_crosscheck": salt_check,
         },
+        "world": {"ranks": world, "transport": transport, "torch_backend": backend,
+                  "gpus_visible": ndev if sharded else 1, "ranks_per_gpu": ranks_per_gpu,
+                  "launcher": os.environ.get("RMC_BENCH_LAUNCHER",
+                                             "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                             else "single process")},
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-            "kernel": "k_expand_sort (librmc's default expansion kernel, RMC_EXPAND_VARIANT 6)",
+            "kernel": "k_expand_sort (librmc's default expansion kernel)" if not sharded
+                      else "k_expand_dist (librmc's sharded expansion kernel)",
             "kernel_ms_per_step": ks * 1e3,
             "launches_per_step": nlaunch, "alg_bytes_per_launch": b_alg / nlaunch,
             "alg_bytes_per_step": b_alg, "probes_per_step": NP,
@@ -212,19 +407,30 @@ def main():
     if sharded:
         ld = last[0]
         out["sharded"] = {"in_library": "rmc_shard + rmc_run_bfs (two-phase fingerprint-first exchange)",
-                          "transport": transport_used[0], "chunks_rank0": ld.chunks, "keys_sent_rank0": ld.keys_sent,
+                          "transport": transport, "chunks_rank0": ld.chunks, "keys_sent_rank0": ld.keys_sent,
                           "states_sent_rank0": ld.states_sent, "stored_rank0": ld.stored_here,
-                          "exchange_s_rank0": round(ld.exchange_seconds, 6), "keys_per_dest": a.keys_per_dest}
-        out["roofline"]["note"] = "per-rank kernel time of rank 0; achieved is rank 0's share"
+                          "exchange_s_rank0": round(ld.exchange_seconds, 6), "keys_per_dest": a.keys_per_dest,
+                          "per_rank": per_rank}
+        out["roofline"]["note"] = ("per-rank kernel time of rank 0; achieved = the job's algorithmic bytes / "
+                                   "world / rank 0's kernel time")
         out["roofline"]["achieved"] = (b_alg / world) / ks / 1e9 if ks > 0 else 0.0
         out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
     if rank == 0 and not a.no_cpu and world == 1:
-        out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_levels)
+        fix_cfg, gpu_fix = None, None
+        if a.cpu_fixpoint:
+            fix_cfg = rmc.config_from_files(a.cpu_fixpoint, builtin_raft=True)
+            fix_cfg.device = dev
+            with rmc.Checker(fix_cfg) as fk:
+                fk.run(record_levels=False)  # warm
+                fr = fk.run(record_levels=False)
+            gpu_fix = (fr.distinct, fr.generated, fr.depth, fr.seconds)
+        out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_levels, fix_cfg, gpu_fix)
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -300,7 +300,10 @@ class Checker:
         if rc:
             raise RmcError(rc, self.lib.rmc_last_error(self.ctx).decode())
 
-    def run(self, progress=None) -> Result:
+    def run(self, progress=None, record_levels=True) -> Result:
+        """rmc_run_bfs.  record_levels=False (and no progress callback) passes
+        no callback at all, as a Java caller without a progress listener
+        would: a sharded search then skips the per-level stop vote."""
         levels = []
 
         def cb(p, _u):
@@ -308,7 +311,7 @@ class Checker:
             levels.append((s.level, s.generated, s.distinct, s.new_states, s.seconds))
             return int(bool(progress and progress(s)))
 
-        fn = PROGRESS_FN(cb)
+        fn = PROGRESS_FN(cb) if (record_levels or progress) else PROGRESS_FN()
         self._check(self.lib.rmc_run_bfs(self.ctx, fn, None))
         res = Result()
         self._check(self.lib.rmc_get_result(self.ctx, C.byref(res)))
