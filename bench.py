@@ -77,27 +77,29 @@ def self_launch(a, argv):
     """Start N rank processes of this script (torchrun's env contract: RANK,
     LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT) and relay rank 0's JSON line.
     Runs before anything in this process touches a GPU or loads librmc."""
+    import tempfile
     n = a.gpus
     port = _free_port()
     procs = []
+    out_f = tempfile.TemporaryFile()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), RMC_BENCH_LAUNCHER="bench.py --gpus (self-launch)")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      stdout=out_f if r == 0 else subprocess.DEVNULL,
                                       start_new_session=True))
+    # poll every rank: one that fails leaves the others blocked in a collective,
+    # so the first failure (or the time limit) ends them all
     t0 = time.time()
-    out = b""
-    try:
-        out = procs[0].communicate(timeout=a.launch_timeout)[0]
-        for p in procs[1:]:
-            p.wait(timeout=max(10.0, a.launch_timeout - (time.time() - t0)))
-    except subprocess.TimeoutExpired:
-        pass
-    rcs = [p.poll() for p in procs]
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs) or any(rc not in (None, 0) for rc in rcs) \
+                or time.time() - t0 > a.launch_timeout:
+            break
+        time.sleep(0.2)
     if any(rc is None for rc in rcs) or any(rcs):
-        for p in procs:  # end every rank's process group: a failed rank leaves the others in a collective
+        for p in procs:
             if p.poll() is None:
                 try:
                     os.killpg(p.pid, 9)
@@ -106,6 +108,8 @@ def self_launch(a, argv):
             p.wait()
         sys.stderr.write(f"bench.py: rank exit codes {rcs}; no result line\n")
         return 1
+    out_f.seek(0)
+    out = out_f.read()
     lines = [ln for ln in out.decode().splitlines() if ln.startswith("{")]
     if len(lines) != 1:
         sys.stderr.write("bench.py: rank 0 printed no result line\n")

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 2
+#define RMC_ABI_VERSION 3
 
 /* Capacity of the packed encoding (DESIGN.md "Packed state"). */
 #define RMC_MAX_SERVERS 5
@@ -123,13 +123,18 @@ typedef struct rmc_result {
     /* sharded mode (rmc_shard): this rank's exchange */
     uint64_t keys_sent;        /* phase-1 keys sent to other owners                        */
     uint64_t states_sent;      /* phase-2 accepted states shipped                          */
-    uint64_t chunks;           /* frontier chunks (exchange rounds)                        */
-    double exchange_seconds;   /* wall time in collectives and count read-backs            */
+    uint64_t chunks;           /* exchange rounds (frontier chunks and drains of parked keys) */
+    double exchange_seconds;   /* device time of the exchange rounds (exchange stream),    */
+                               /* overlapped with the next round's expansion or not        */
     uint64_t stored_here;      /* distinct states this rank stores                         */
     /* RMC_FLAG_SPILL */
     uint64_t spilled;          /* states moved to host memory (all spills of the run)      */
     uint64_t spills;           /* spill events                                              */
     double spill_seconds;      /* wall time of the spills (device-to-host + window shift)   */
+    /* sharded mode, continued */
+    uint64_t parked;           /* keys parked because an owner's outbox was full; sent in   */
+                               /* further rounds of the same level (never dropped)          */
+    double exchange_wait_seconds; /* host wall time blocked on count read-backs and level ends */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */
@@ -291,22 +296,26 @@ int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, r
  * rank.  A state is owned by the rank given by a hash of its servers 0 and 1
  * words (RMC_OWNER=2, default; 1: server 0 only; 0: by fingerprint, always
  * under SYMMETRY); each rank stores and expands the states it owns.
- * Per frontier chunk the exchange is fingerprint-first (two phases):
+ * A level is expanded in rounds; each round's exchange is fingerprint-first
+ * (two phases):
  *   1. a successor owned elsewhere (and not in this rank's lossy sent-cache)
  *      sends only its 8-byte key; the owner inserts the keys it receives
  *      into its fingerprint set and answers new / seen (1 byte per key);
  *   2. for the keys answered "new" the sender re-derives the successor and
  *      ships the state and its global parent ref ((rank << 48) | index, lane
  *      in bits 40-47); the owner stores it for the next level.
- * Counts stay on the device until one read-back per phase; one all-gather
- * per level combines the level statistics.
+ * Rounds are pipelined: the next round's expansion runs while this round's
+ * exchange is on the wire (two outbox sets, an exchange stream).  Per round
+ * the host reads back two small count rows; one all-gather of the device
+ * counters per level combines the level statistics.  A key whose owner's
+ * outbox is full is parked and sent in a further round of the same level.
  * Transport: RCCL over xGMI (rccl_id = an id from rmc_rccl_unique_id on rank
  * 0, given to every rank; host = NULL), or a caller-supplied host transport
  * (rccl_id = NULL) whose callbacks move host buffers: alltoallv sends
  * send_bytes[d] bytes to rank d (blocks back to back in `send`) and receives
  * recv_bytes[s] from rank s (back to back in `recv`); allgather gathers
  * `bytes` from every rank into recv (rank order).  They return 0 on success.
- * keys_per_dest bounds the keys one chunk sends to one owner (0 = auto);
+ * keys_per_dest bounds the keys one round sends to one owner (0 = auto);
  * sent_cache_slots sizes the sent-cache (0 = auto).  Checkpoints and
  * full-state verification are single-GPU only. */
 typedef struct rmc_transport {

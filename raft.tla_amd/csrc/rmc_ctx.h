@@ -21,21 +21,43 @@ struct DistState {
     int rccl = 0;                   // 1: RCCL communicator, 0: host transport
     ncclComm_t comm = nullptr;
     rmc_transport host{};
-    // device buffers (B.key_out / tick_out / st_out / ocount / scount live in DevBufs)
+    hipStream_t xs = nullptr;       // exchange stream: every collective, owner insert, phase 2
+    // Outbox sets, double-buffered: the expansion of round k + 1 (ctx stream)
+    // fills one set while round k's exchange (xs) drains the other.
+    struct Set {
+        rmc::u64* key_out = nullptr;             // [world][kcap] keys per owner
+        rmc::u64* tick_out = nullptr;            // [world][kcap] tickets (parent | lane << 56)
+        unsigned long long* ocount = nullptr;    // [world] keys written per owner
+        rmc::u64* cx = nullptr;                  // device count row: [2W + 1] sent, [2W] received
+        rmc::u64* h_cx = nullptr;                // pinned copy of cx
+        hipEvent_t ev_exp = nullptr;             // expansion (or drain) of this set's round done
+        hipEvent_t ev_free = nullptr;            // the round's exchange no longer reads the set
+        hipEvent_t k0 = nullptr, k1 = nullptr;   // expansion kernel time
+        hipEvent_t x0 = nullptr, x1 = nullptr;   // exchange time (xs) of the round
+        int timed = 0, xtimed = 0;
+    } set[2];
+    hipEvent_t ev_cnt = nullptr, ev_acc = nullptr, ev_c = nullptr, ev_x = nullptr;
+    // single buffers (used on xs only, rounds in order)
     rmc::u64* key_in = nullptr;     // keys received, blocks by source
     uint8_t* rep_out = nullptr;     // replies to the keys received (same layout)
     uint8_t* rep_in = nullptr;      // replies to the keys sent, [world][kcap]
     rmc::u32* st_in = nullptr;      // accepted states received, blocks by source
-    rmc::u64 in_cap = 0;            // keys / states receivable per chunk (all sources)
-    rmc::u64* h_cnt = nullptr;      // pinned scratch: per-destination counts (2 x world)
-    void* ag_dev = nullptr;         // RCCL all-gathers of small host rows: device staging,
+    unsigned long long* sa = nullptr;  // [2W]: states to send per owner (scount), states to receive per source
+    rmc::u64* h_sa = nullptr;       // pinned copy of sa
+    rmc::u64 in_cap = 0;            // keys / states receivable per round (all sources)
+    void* ag_dev = nullptr;         // RCCL all-gathers of small rows: device staging,
     rmc::u64 ag_cap = 0;            // (world + 1) x ag_cap bytes, allocated once per shard
     std::vector<uint8_t> stage_send, stage_recv;  // host transport staging
     rmc::u64 sent_slots = 0;
-    int debug = 0;                  // RMC_DIST_DEBUG: one stderr line per chunk
+    int debug = 0;                  // RMC_DIST_DEBUG: one stderr line per round
+    int split = 2;                  // RMC_DIST_SPLIT: rounds a large level is cut into at least
+    int overlap = 1;                // RMC_DIST_OVERLAP=0: the next expansion waits for the exchange
+    double fill = 0.5;              // RMC_DIST_FILL: expected fill of the fullest outbox a round aims at
+                                    // (> 1 forces parking: a test hook)
     // statistics of the last run
-    rmc::u64 keys_sent = 0, states_sent = 0, chunks = 0;
-    double xfer_seconds = 0;        // wall time in collectives and count read-backs
+    rmc::u64 keys_sent = 0, states_sent = 0, chunks = 0, parked = 0;
+    double xfer_seconds = 0;        // device time of the exchange rounds (xs), overlapped or not
+    double wait_seconds = 0;        // host wall time blocked on count read-backs and level ends
 };
 
 // Frontier spill (RMC_FLAG_SPILL): the device holds the fingerprint set and

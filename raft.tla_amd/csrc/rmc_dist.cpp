@@ -1,20 +1,28 @@
 // rmc_dist.cpp — sharded BFS over several GPUs behind the C ABI (rmc_shard).
 //
-// One ctx per GPU, each a rank of a fingerprint-space partition (SURVEY.md
-// §8e; replaces TLC's distributed mode).  Per BFS level every rank expands the
-// frontier it owns chunk by chunk; per chunk the exchange is two-phase:
+// One ctx per GPU, each a rank of a state-space partition (SURVEY.md §8e;
+// replaces TLC's distributed mode).  Per BFS level every rank expands the
+// frontier it owns in ROUNDS; a round's exchange is two-phase, fingerprint
+// first:
 //   phase 1  k_expand<DIST> puts the key of every successor owned elsewhere
-//            (and not in the sent-cache) in that owner's key outbox, with a
-//            local ticket (parent, lane); keys all-to-all; the owner inserts
-//            them (k_owner_insert) and answers new/seen, 1 byte per key;
-//            replies all-to-all (the reverse of the key exchange);
+//            (and not in the sent-cache) in that owner's key outbox with a
+//            local ticket (parent, lane); a count all-to-all tells every rank
+//            what it receives; keys all-to-all; the owner inserts them
+//            (k_owner_insert), answers new/seen with 1 byte per key and
+//            counts per source the states it will receive; replies
+//            all-to-all (the reverse of the key exchange);
 //   phase 2  k_materialize_remote re-derives the accepted successors from
-//            their tickets into per-owner state outboxes; states all-to-all;
-//            the owner stores them (k_store_remote).
-// Collectives run on RCCL over xGMI (one communicator per ctx, on the ctx's
-// stream) or on a caller-supplied host transport (gloo in the tests, where
-// several ranks share one GPU).  Per chunk the host reads back two count
-// vectors (the sizes RCCL's send/recv calls need) and all-gathers them.
+//            their tickets into per-owner state outboxes (counting them);
+//            states all-to-all; the owner stores them (k_store_remote).
+// Pipelining: two outbox sets.  The ctx stream expands round k + 1 into one
+// set while the exchange stream (xs) runs round k's exchange on the other, so
+// the host's two count read-backs per round wait while the GPU expands.  A
+// level ends with one all-gather of the device counters.  Keys that do not
+// fit an outbox are parked (B.ovf) and sent in later rounds of the same level:
+// an outbox overflow costs a round, never the run.
+// Collectives run on RCCL over xGMI (one communicator per ctx) or on a
+// caller-supplied host transport (gloo in the tests, where several ranks share
+// one GPU; every collective is then a synchronous host round trip).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -38,17 +46,21 @@ double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// All-to-all of per-peer byte blocks living on the device: block p of the send
-// side is sbuf + soff[p] (scnt[p] bytes) for rank p; block p of the receive
-// side lands at rbuf + roff[p] (rcnt[p] bytes) from rank p.
+// All-to-all of per-peer byte blocks living on the device, on the exchange
+// stream: block p of the send side is sbuf + soff[p] (scnt[p] bytes) for rank
+// p; block p of the receive side lands at rbuf + roff[p] (rcnt[p] bytes) from
+// rank p.
 int a2a(rmc_ctx* c, const void* sbuf, const u64* soff, const u64* scnt, void* rbuf, const u64* roff, const u64* rcnt) {
     DistState& D = c->dist;
     const int W = D.world;
     if (D.rccl) {
+        bool any = false;
+        for (int p = 0; p < W; ++p) any |= scnt[p] || rcnt[p];
+        if (!any) return 0;
         NCCLCHK(c, ncclGroupStart());
         for (int p = 0; p < W; ++p) {
-            if (scnt[p]) NCCLCHK(c, ncclSend((const char*)sbuf + soff[p], scnt[p], ncclUint8, p, D.comm, c->st));
-            if (rcnt[p]) NCCLCHK(c, ncclRecv((char*)rbuf + roff[p], rcnt[p], ncclUint8, p, D.comm, c->st));
+            if (scnt[p]) NCCLCHK(c, ncclSend((const char*)sbuf + soff[p], scnt[p], ncclUint8, p, D.comm, D.xs));
+            if (rcnt[p]) NCCLCHK(c, ncclRecv((char*)rbuf + roff[p], rcnt[p], ncclUint8, p, D.comm, D.xs));
         }
         NCCLCHK(c, ncclGroupEnd());
         return 0;
@@ -61,20 +73,32 @@ int a2a(rmc_ctx* c, const void* sbuf, const u64* soff, const u64* scnt, void* rb
     for (int p = 0; p < W; ++p) {
         if (scnt[p])
             HIPCHK(c, hipMemcpyAsync(D.stage_send.data() + o, (const char*)sbuf + soff[p], scnt[p], hipMemcpyDeviceToHost,
-                                     c->st));
+                                     D.xs));
         o += scnt[p];
     }
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    HIPCHK(c, hipStreamSynchronize(D.xs));
     if (D.host.alltoallv(D.host.user, D.stage_send.data(), scnt, D.stage_recv.data(), rcnt))
         return fail(c, RMC_E_HIP, "host transport alltoallv failed");
     o = 0;
     for (int p = 0; p < W; ++p) {
         if (rcnt[p])
-            HIPCHK(c, hipMemcpyAsync((char*)rbuf + roff[p], D.stage_recv.data() + o, rcnt[p], hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync((char*)rbuf + roff[p], D.stage_recv.data() + o, rcnt[p], hipMemcpyHostToDevice, D.xs));
         o += rcnt[p];
     }
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    HIPCHK(c, hipStreamSynchronize(D.xs));
     return 0;
+}
+
+// All-to-all of `per` u64 per peer between device buffers (the count rows).
+int a2a_u64(rmc_ctx* c, const u64* send, u64* recv, u64 per) {
+    DistState& D = c->dist;
+    if (D.rccl) {
+        NCCLCHK(c, ncclAllToAll(send, recv, per, ncclUint64, D.comm, D.xs));
+        return 0;
+    }
+    std::vector<u64> off((size_t)D.world), cnt((size_t)D.world, per * 8);
+    for (int p = 0; p < D.world; ++p) off[(size_t)p] = (u64)p * per * 8;
+    return a2a(c, send, off.data(), cnt.data(), recv, off.data(), cnt.data());
 }
 
 // All-gather of `bytes` host bytes per rank into all (world * bytes, rank order).
@@ -86,14 +110,39 @@ int allgather(rmc_ctx* c, const void* mine, u64 bytes, void* all) {
     }
     const bool big = bytes > D.ag_cap;  // rows are small: the staging buffer is allocated once
     void* d_buf = D.ag_dev;
-    if (big) HIPCHK(c, hipMallocAsync(&d_buf, bytes * (u64)(D.world + 1), c->st));
+    if (big) HIPCHK(c, hipMallocAsync(&d_buf, bytes * (u64)(D.world + 1), D.xs));
     char* d_in = (char*)d_buf + bytes * (u64)D.world;
-    HIPCHK(c, hipMemcpyAsync(d_in, mine, bytes, hipMemcpyHostToDevice, c->st));
-    NCCLCHK(c, ncclAllGather(d_in, d_buf, bytes, ncclUint8, D.comm, c->st));
-    HIPCHK(c, hipMemcpyAsync(all, d_buf, bytes * (u64)D.world, hipMemcpyDeviceToHost, c->st));
-    if (big) HIPCHK(c, hipFreeAsync(d_buf, c->st));
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    HIPCHK(c, hipMemcpyAsync(d_in, mine, bytes, hipMemcpyHostToDevice, D.xs));
+    NCCLCHK(c, ncclAllGather(d_in, d_buf, bytes, ncclUint8, D.comm, D.xs));
+    HIPCHK(c, hipMemcpyAsync(all, d_buf, bytes * (u64)D.world, hipMemcpyDeviceToHost, D.xs));
+    if (big) HIPCHK(c, hipFreeAsync(d_buf, D.xs));
+    HIPCHK(c, hipStreamSynchronize(D.xs));
     return 0;
+}
+
+// All-gather of this rank's device counters (the level statistics), after
+// every kernel of the level on both streams.
+int allgather_counters(rmc_ctx* c, Counters* rows) {
+    DistState& D = c->dist;
+    HIPCHK(c, hipEventRecord(D.ev_c, c->st));
+    HIPCHK(c, hipStreamWaitEvent(D.xs, D.ev_c, 0));
+    const u64 bytes = sizeof(Counters);
+    if (D.rccl) {
+        NCCLCHK(c, ncclAllGather(c->B.ctr, D.ag_dev, bytes, ncclUint8, D.comm, D.xs));
+        HIPCHK(c, hipMemcpyAsync(rows, D.ag_dev, bytes * (u64)D.world, hipMemcpyDeviceToHost, D.xs));
+        HIPCHK(c, hipStreamSynchronize(D.xs));
+        return 0;
+    }
+    Counters mine;
+    HIPCHK(c, hipMemcpyAsync(&mine, c->B.ctr, bytes, hipMemcpyDeviceToHost, D.xs));
+    HIPCHK(c, hipStreamSynchronize(D.xs));
+    if (D.host.allgather(D.host.user, &mine, bytes, rows)) return fail(c, RMC_E_HIP, "host transport allgather failed");
+    return 0;
+}
+
+float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
 }
 
 }  // namespace
@@ -102,38 +151,52 @@ namespace rmc_host {
 
 void free_dist(rmc_ctx* c) {
     DistState& D = c->dist;
+    if (D.xs) (void)hipStreamSynchronize(D.xs);
     (void)hipFree(c->B.sent);
-    (void)hipFree(c->B.key_out);
-    (void)hipFree(c->B.tick_out);
-    (void)hipFree(c->B.ocount);
-    (void)hipFree(c->B.st_out);
-    (void)hipFree(c->B.scount);
+    (void)hipFree(c->B.ovf);
+    for (auto& S : D.set) {
+        (void)hipFree(S.key_out);
+        (void)hipFree(S.tick_out);
+        (void)hipFree(S.ocount);
+        (void)hipFree(S.cx);
+        if (S.h_cx) (void)hipHostFree(S.h_cx);
+        for (hipEvent_t* e : {&S.ev_exp, &S.ev_free, &S.k0, &S.k1, &S.x0, &S.x1})
+            if (*e) (void)hipEventDestroy(*e);
+        S = DistState::Set{};
+    }
+    for (hipEvent_t* e : {&D.ev_cnt, &D.ev_acc, &D.ev_c, &D.ev_x})
+        if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
     (void)hipFree(D.key_in);
     (void)hipFree(D.rep_out);
     (void)hipFree(D.rep_in);
     (void)hipFree(D.st_in);
-    if (D.h_cnt) (void)hipHostFree(D.h_cnt);
+    (void)hipFree(c->B.st_out);
+    (void)hipFree(D.sa);
+    if (D.h_sa) (void)hipHostFree(D.h_sa);
     (void)hipFree(D.ag_dev);
+    if (D.comm) (void)ncclCommDestroy(D.comm);
+    if (D.xs) (void)hipStreamDestroy(D.xs);
+    c->B.sent = nullptr; c->B.key_out = nullptr; c->B.tick_out = nullptr; c->B.ocount = nullptr;
+    c->B.st_out = nullptr; c->B.scount = nullptr; c->B.ovf = nullptr; c->B.ovf_cap = 0;
+    D.key_in = nullptr; D.rep_out = nullptr; D.rep_in = nullptr; D.st_in = nullptr; D.sa = nullptr; D.h_sa = nullptr;
     D.ag_dev = nullptr;
     D.ag_cap = 0;
-    if (D.comm) (void)ncclCommDestroy(D.comm);
-    c->B.sent = nullptr; c->B.key_out = nullptr; c->B.tick_out = nullptr; c->B.ocount = nullptr;
-    c->B.st_out = nullptr; c->B.scount = nullptr;
-    D.key_in = nullptr; D.rep_out = nullptr; D.rep_in = nullptr; D.st_in = nullptr; D.h_cnt = nullptr;
     D.comm = nullptr;
+    D.xs = nullptr;
     D.on = 0;
 }
 
 int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     DistState& D = c->dist;
     const int W = D.world, me = D.rank;
-    const int RW = c->NW + 2;  // state record: packed state + global parent ref
+    const u64 RB = (u64)(c->NW + 2) * 4;  // state record: packed state + global parent ref
+    const u64 kcap = c->B.kcap;
     const double t0 = now_s();
     c->res = rmc_result{};
     c->level_start.clear();
     c->have_target = 0;
-    D.keys_sent = D.states_sent = D.chunks = 0;
-    D.xfer_seconds = 0;
+    D.keys_sent = D.states_sent = D.chunks = D.parked = 0;
+    D.xfer_seconds = D.wait_seconds = 0;
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
@@ -148,53 +211,53 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, hipMemcpyAsync(c->d_staged, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
         HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
     }
-    if (int rc = read_counters(c)) return rc;
-    c->level_start.push_back(0);
-    c->level_start.push_back(c->h_ctr->count);
-    u64 generated = 1, probes = 0;
-    int depth = 1;
-    // level statistics, all-gathered: new, generated, probes, viol (index << 4 | bit, ~0 none),
-    // deadlock index (~0 none), error flags
-    struct LevelRow { u64 nnew, gen, probes, viol, dead, err, stored; };
-    std::vector<LevelRow> rows((size_t)W);
-    auto level_end = [&](u64 hi) -> int {
-        const Counters& k = *c->h_ctr;
-        LevelRow mine{k.count - hi, k.generated, k.probes, k.viol, k.deadlock,
-                      (u64)(k.overflow | (k.table_full ? 16u : 0u)), k.count};
-        const double tx = now_s();
-        if (int rc = allgather(c, &mine, sizeof mine, rows.data())) return rc;
-        D.xfer_seconds += now_s() - tx;
+    std::vector<Counters> rows((size_t)W);
+    // level end: the all-gathered device counters; errors stop every rank alike
+    auto level_end = [&]() -> int {
+        const double tw = now_s();
+        if (int rc = allgather_counters(c, rows.data())) return rc;
+        D.wait_seconds += now_s() - tw;
+        *c->h_ctr = rows[(size_t)me];
         for (int r = 0; r < W; ++r) {
-            const u64 e = rows[(size_t)r].err;
-            if (e & 16u) return fail(c, RMC_E_CAPACITY, "fingerprint set full on rank " + std::to_string(r));
-            if (e & 2u) return fail(c, RMC_E_CAPACITY, "exchange outbox full on rank " + std::to_string(r) +
-                                                       " (raise keys_per_dest)");
-            if (e) return fail(c, RMC_E_CAPACITY, "state store full on rank " + std::to_string(r) +
-                                                  " (raise rmc_config.state_capacity)");
+            const Counters& k = rows[(size_t)r];
+            if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full on rank " + std::to_string(r));
+            if (k.overflow & 2u)
+                return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(r) +
+                                                   " (raise keys_per_dest)");
+            if (k.overflow)
+                return fail(c, RMC_E_CAPACITY, "state store full on rank " + std::to_string(r) +
+                                                   " (raise rmc_config.state_capacity)");
         }
         return 0;
     };
-    {  // Init's violation check (level 1)
-        if (int rc = level_end(0)) return rc;
-        for (int r = 0; r < W && !c->have_target; ++r)
-            if (rows[(size_t)r].viol != ~0ull) {
-                c->res.violated_inv = 1 << (int)(rows[(size_t)r].viol & 15);
-                c->res.violation_depth = 1;
-                c->have_target = 1;
-                c->target_idx = ((u64)r << 48) | (rows[(size_t)r].viol >> 4);
-            }
+    if (int rc = level_end()) return rc;
+    c->level_start.push_back(0);
+    c->level_start.push_back(c->h_ctr->count);
+    u64 total_prev = 0;
+    for (const auto& k : rows) total_prev += k.count;
+    for (int r = 0; r < W && !c->have_target; ++r)  // Init's violation check (level 1)
+        if (rows[(size_t)r].viol != ~0ull) {
+            c->res.violated_inv = 1 << (int)(rows[(size_t)r].viol & 15);
+            c->res.violation_depth = 1;
+            c->have_target = 1;
+            c->target_idx = ((u64)r << 48) | (rows[(size_t)r].viol >> 4);
+        }
+    // the per-level stop vote runs only when some rank passed a progress callback
+    int any_cb = 0;
+    {
+        const int mine = cb ? 1 : 0;
+        std::vector<int> all((size_t)W);
+        if (int rc = allgather(c, &mine, sizeof mine, all.data())) return rc;
+        for (int x : all) any_cb |= x;
     }
-    const u64 kcap = c->B.kcap, scap = c->B.scap;
-    std::vector<u64> M((size_t)W * (W + 1)), soff((size_t)W), scnt((size_t)W), roff((size_t)W), rcnt((size_t)W);
-    std::vector<u64> row((size_t)W + 1);
-    const u64 nl = (u64)c->P.off[10];
-    // Chunk sizing: rho = most keys one chunk sends one owner, per expanded
-    // state.  It varies along a frontier (states received from other ranks are
-    // appended after the local ones, and are of another kind) by up to ~1.6x
-    // within a level (RMC_DIST_DEBUG logs of the bench model), so a chunk is sized
-    // from the worst rho of the previous level and of this level so far, for an
-    // outbox at most 40 % full.  An overflow is an error, never a silent drop.
-    double rho_prev = (double)nl;
+    u64 generated = 1, probes = 0;
+    int depth = 1;
+    // Round sizing: rho = most keys one round sends one owner, per expanded
+    // state, from the previous rounds (it varies along a frontier: states
+    // received from other ranks are appended after the local ones).  A round
+    // aims at an outbox half full; what does not fit is parked, not lost.
+    double rho = 1.0;
+    const u64 row_len = 4 * (u64)W + 1;  // cx: [2W] sent pairs, [1] novf, [2W] received pairs
     while (!c->have_target) {
         const u64 lo = c->level_start[(size_t)depth - 1], hi = c->level_start[(size_t)depth];
         if (c->cfg.max_depth > 0 && depth >= c->cfg.max_depth) {
@@ -206,103 +269,180 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             break;
         }
         if (int rc = reset_counters(c, true)) return rc;
-        u64 cursor = lo;
-        double rho_lvl = 0;
-        for (;;) {  // chunks: every rank takes part until no rank has frontier left
-            const double rho = std::max({0.05, rho_prev, rho_lvl});
-            const u64 chunk = std::max<u64>(1, (u64)((double)kcap / (2.5 * rho)));
-            const u64 a = cursor, b = std::min(hi, a + chunk);
-            HIPCHK(c, hipMemsetAsync(c->B.ocount, 0, 8 * (u64)W, c->st));
-            if (a < b) {
-                HIPCHK(c, hipEventRecord(c->ev0, c->st));
-                HIPCHK(c, launch(c->sh, 3, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));
-                HIPCHK(c, hipEventRecord(c->ev1, c->st));
+        u64 cursor = lo, ovf_known = 0, ovf_done = 0;
+        const u64 frontier = hi - lo;
+        // at least D.split rounds for a large level, so one round's exchange
+        // overlaps the next round's expansion
+        const u64 split_cap = frontier >= (1ull << 21) ? (frontier + D.split - 1) / (u64)D.split : frontier;
+        u64 round_states[2] = {0, 0};  // states expanded by the round held in each set
+        int round_kind[2] = {0, 0};    // 0 empty, 1 expansion, 2 drain
+        // enqueue the expansion (or the drain of parked keys) of round k into set k & 1
+        auto enqueue_A = [&](u64 k) -> int {
+            DistState::Set& S = D.set[k & 1];
+            HIPCHK(c, hipStreamWaitEvent(c->st, S.ev_free, 0));
+            HIPCHK(c, hipMemsetAsync(S.ocount, 0, 8 * (u64)W, c->st));
+            DevBufs Bb = c->B;
+            Bb.key_out = S.key_out;
+            Bb.tick_out = S.tick_out;
+            Bb.ocount = S.ocount;
+            round_states[k & 1] = 0;
+            round_kind[k & 1] = 0;
+            S.timed = 0;
+            if (ovf_done < ovf_known) {
+                const u64 n = std::min(kcap, ovf_known - ovf_done);
+                HIPCHK(c, launch_drain(Bb, ovf_done, n, c->st));
+                ovf_done += n;
+                round_kind[k & 1] = 2;
+            } else if (cursor < hi) {
+                const u64 target = (u64)(D.fill * (double)kcap / std::max(rho, 0.02));
+                const u64 n = std::max<u64>(1, std::min<u64>({hi - cursor, (u64)1 << 24, target, split_cap}));
+                HIPCHK(c, hipEventRecord(S.k0, c->st));
+                HIPCHK(c, launch(c->sh, 3, c->P, c->PT, Bb, cursor, cursor + n, nullptr, nullptr, 0, nullptr, c->st));
+                HIPCHK(c, hipEventRecord(S.k1, c->st));
+                S.timed = 1;
                 c->res.expand_launches += 1;
+                cursor += n;
+                round_states[k & 1] = n;
+                round_kind[k & 1] = 1;
             }
-            HIPCHK(c, hipMemcpyAsync(D.h_cnt, c->B.ocount, 8 * (u64)W, hipMemcpyDeviceToHost, c->st));
-            HIPCHK(c, hipStreamSynchronize(c->st));
-            if (a < b) {
-                float ms = 0.f;
-                HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-                c->res.expand_kernel_seconds += 1e-3 * ms;
+            HIPCHK(c, hipEventRecord(S.ev_exp, c->st));
+            return 0;
+        };
+        std::vector<u64> soff((size_t)W), scnt((size_t)W), roff((size_t)W), rcnt((size_t)W);
+        std::vector<u64> s2((size_t)W), o2((size_t)W), r2((size_t)W), q2((size_t)W);
+        if (int rc = enqueue_A(0)) return rc;
+        for (u64 k = 0;; ++k) {
+            const int b = (int)(k & 1);
+            DistState::Set& S = D.set[b];
+            const bool host_more = cursor < hi || ovf_done < ovf_known;
+            // ---- count row of round k (after its expansion), on xs
+            HIPCHK(c, hipStreamWaitEvent(D.xs, S.ev_exp, 0));
+            HIPCHK(c, hipEventRecord(S.x0, D.xs));
+            {
+                DevBufs Bb = c->B;
+                Bb.ocount = S.ocount;
+                HIPCHK(c, launch_pack_counts(Bb, host_more ? 1ull : 0ull, ovf_done, S.cx, D.xs));
             }
-            const double tx = now_s();
-            u64 mx = 0;
-            for (int d = 0; d < W; ++d) { row[(size_t)d] = D.h_cnt[d]; if (d != me) mx = std::max(mx, D.h_cnt[d]); }
-            row[(size_t)W] = (b < hi ? 1u : 0u) | (mx > kcap ? 2u : 0u);
-            if (D.debug)
-                fprintf(stderr, "[rmc rank %d] level %d chunk [%llu, %llu) of [%llu, %llu): most keys to one owner %llu (cap %llu), rho %.3f\n",
-                        me, depth, (unsigned long long)a, (unsigned long long)b, (unsigned long long)lo,
-                        (unsigned long long)hi, (unsigned long long)mx, (unsigned long long)kcap, rho);
-            if (int rc = allgather(c, row.data(), 8 * ((u64)W + 1), M.data())) return rc;
-            bool more = false;
-            u64 ph2 = 0;  // most keys one rank sent one owner: bounds the phase-2 rounds
-            for (int r = 0; r < W; ++r) {
-                const u64 f = M[(size_t)r * (W + 1) + W];
-                if (f & 2u) return fail(c, RMC_E_CAPACITY, "phase-1 key outbox full on rank " + std::to_string(r) +
-                                                           " (raise keys_per_dest)");
-                more |= (f & 1u) != 0;
-                for (int d = 0; d < W; ++d) if (d != r) ph2 = std::max(ph2, M[(size_t)r * (W + 1) + d]);
+            if (int rc = a2a_u64(c, S.cx, S.cx + 2 * W + 1, 2)) return rc;
+            HIPCHK(c, hipMemcpyAsync(S.h_cx, S.cx, row_len * 8, hipMemcpyDeviceToHost, D.xs));
+            HIPCHK(c, hipEventRecord(D.ev_cnt, D.xs));
+            // the next round's expansion is queued before waiting, so the GPU
+            // expands while the counts travel (not in RMC_DIST_OVERLAP=0 runs)
+            bool next_queued = false;
+            if (D.overlap && host_more) {
+                if (int rc = enqueue_A(k + 1)) return rc;
+                next_queued = true;
             }
-            if (a < b) rho_lvl = std::max(rho_lvl, (double)std::max<u64>(mx, 1) / (double)(b - a));
-            // ---- phase 1: keys to their owners, replies back
-            u64 tot_in = 0;
+            {
+                const double tw = now_s();
+                HIPCHK(c, hipEventSynchronize(D.ev_cnt));
+                D.wait_seconds += now_s() - tw;
+            }
+            const u64* cx = S.h_cx;
+            const u64 novf = cx[2 * W];
+            if (novf > c->B.ovf_cap)
+                return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(me) +
+                                                   " (raise keys_per_dest)");
+            const u64 newly_parked = novf - std::min(novf, ovf_known);
+            D.parked += newly_parked;
+            ovf_known = std::max(ovf_known, novf);
+            bool global_more = false;
+            u64 mx = 0, tot_in = 0;
             for (int p = 0; p < W; ++p) {
+                global_more |= (cx[2 * W + 1 + 2 * p + 1] & 1u) != 0;
+                scnt[(size_t)p] = cx[2 * p] * 8;
                 soff[(size_t)p] = (u64)p * kcap * 8;
-                scnt[(size_t)p] = p == me ? 0 : D.h_cnt[p] * 8;
-                rcnt[(size_t)p] = p == me ? 0 : M[(size_t)p * (W + 1) + me] * 8;
+                rcnt[(size_t)p] = cx[2 * W + 1 + 2 * p] * 8;
                 roff[(size_t)p] = tot_in * 8;
-                tot_in += rcnt[(size_t)p] / 8;
-                if (p != me) D.keys_sent += D.h_cnt[p];
+                tot_in += cx[2 * W + 1 + 2 * p];
+                mx = std::max(mx, cx[2 * p]);
+                D.keys_sent += cx[2 * p];
             }
+            if (S.timed) {
+                c->res.expand_kernel_seconds += 1e-3 * elapsed_ms(S.k0, S.k1);
+                S.timed = 0;
+            }
+            if (D.set[b ^ 1].xtimed) {  // the previous round is complete on xs (stream order)
+                D.xfer_seconds += 1e-3 * elapsed_ms(D.set[b ^ 1].x0, D.set[b ^ 1].x1);
+                D.set[b ^ 1].xtimed = 0;
+            }
+            if (round_kind[b] == 1 && round_states[b])  // keys per state of the fullest owner (parked ones included)
+                rho = std::max(0.5 * rho, (double)(mx + newly_parked) / (double)round_states[b]);
+            if (D.debug)
+                fprintf(stderr, "[rmc rank %d] level %d round %llu kind %d states %llu: most keys to one owner %llu "
+                                "(cap %llu), parked %llu/%llu, in %llu, rho %.3f, more %d\n",
+                        me, depth, (unsigned long long)k, round_kind[b], (unsigned long long)round_states[b],
+                        (unsigned long long)mx, (unsigned long long)kcap, (unsigned long long)ovf_done,
+                        (unsigned long long)ovf_known, (unsigned long long)tot_in, rho, (int)global_more);
             if (tot_in > D.in_cap) return fail(c, RMC_E_CAPACITY, "phase-1 inbox full");
-            if (ph2) {
-                if (int rc = a2a(c, c->B.key_out, soff.data(), scnt.data(), D.key_in, roff.data(), rcnt.data())) return rc;
-                HIPCHK(c, launch_owner_insert(c->B, D.key_in, D.rep_out, tot_in, c->st));
-                // replies: block p of rep_out (keys from p) back to p; from d into rep_in + d * kcap
-                std::vector<u64> s2((size_t)W), o2((size_t)W), r2((size_t)W), q2((size_t)W);
-                for (int p = 0; p < W; ++p) {
-                    s2[(size_t)p] = rcnt[(size_t)p] / 8;
-                    o2[(size_t)p] = roff[(size_t)p] / 8;
-                    r2[(size_t)p] = scnt[(size_t)p] / 8;
-                    q2[(size_t)p] = (u64)p * kcap;
-                }
-                if (int rc = a2a(c, D.rep_out, o2.data(), s2.data(), D.rep_in, q2.data(), r2.data())) return rc;
-                // ---- phase 2: accepted states, in rounds of at most scap per owner
-                for (u64 w0 = 0; w0 < ph2; w0 += scap) {
-                    HIPCHK(c, hipMemsetAsync(c->B.scount, 0, 8 * (u64)W, c->st));
-                    HIPCHK(c, launch(c->sh, 8, c->P, c->PT, c->B, std::min(scap, ph2 - w0), w0,
-                                     reinterpret_cast<const u32*>(D.rep_in), nullptr, 0, nullptr, c->st));
-                    HIPCHK(c, hipMemcpyAsync(D.h_cnt + W, c->B.scount, 8 * (u64)W, hipMemcpyDeviceToHost, c->st));
-                    HIPCHK(c, hipStreamSynchronize(c->st));
-                    std::vector<u64> S2((size_t)W * W);
-                    if (int rc = allgather(c, D.h_cnt + W, 8 * (u64)W, S2.data())) return rc;
-                    u64 tot_st = 0;
-                    const u64 RB = (u64)RW * 4;
-                    for (int p = 0; p < W; ++p) {
-                        soff[(size_t)p] = (u64)p * scap * RB;
-                        scnt[(size_t)p] = p == me ? 0 : D.h_cnt[W + p] * RB;
-                        rcnt[(size_t)p] = p == me ? 0 : S2[(size_t)p * W + me] * RB;
-                        roff[(size_t)p] = tot_st * RB;
-                        tot_st += rcnt[(size_t)p] / RB;
-                        if (p != me) D.states_sent += D.h_cnt[W + p];
-                    }
-                    if (tot_st > (u64)W * scap) return fail(c, RMC_E_CAPACITY, "phase-2 inbox full");
-                    if (int rc = a2a(c, c->B.st_out, soff.data(), scnt.data(), D.st_in, roff.data(), rcnt.data()))
-                        return rc;
-                    HIPCHK(c, launch(c->sh, 9, c->P, c->PT, c->B, tot_st, 0, D.st_in, nullptr, 0, nullptr, c->st));
-                }
+            if (global_more && !next_queued) {
+                if (int rc = enqueue_A(k + 1)) return rc;
+                next_queued = true;
             }
-            D.xfer_seconds += now_s() - tx;
+            // ---- phase 1: keys to their owners, replies back; phase 2 sizes
+            HIPCHK(c, hipMemsetAsync(D.sa, 0, 16 * (u64)W, D.xs));
+            if (int rc = a2a(c, S.key_out, soff.data(), scnt.data(), D.key_in, roff.data(), rcnt.data())) return rc;
+            SrcOff so{};
+            for (int p = 0; p < W; ++p) so.o[p] = roff[(size_t)p] / 8;
+            so.o[W] = tot_in;
+            HIPCHK(c, launch_owner_insert(c->B, D.key_in, D.rep_out, tot_in, so, D.sa + W, D.xs));
+            for (int p = 0; p < W; ++p) {  // block p of rep_out (keys from p) back to p; from d into rep_in + d * kcap
+                s2[(size_t)p] = rcnt[(size_t)p] / 8;
+                o2[(size_t)p] = roff[(size_t)p] / 8;
+                r2[(size_t)p] = scnt[(size_t)p] / 8;
+                q2[(size_t)p] = (u64)p * kcap;
+            }
+            if (int rc = a2a(c, D.rep_out, o2.data(), s2.data(), D.rep_in, q2.data(), r2.data())) return rc;
+            if (mx) {
+                DevBufs Bb = c->B;
+                Bb.key_out = S.key_out;
+                Bb.tick_out = S.tick_out;
+                Bb.ocount = S.ocount;
+                HIPCHK(c, launch(c->sh, 8, c->P, c->PT, Bb, mx, 0, reinterpret_cast<const u32*>(D.rep_in), nullptr, 0,
+                                 nullptr, D.xs));
+            }
+            HIPCHK(c, hipEventRecord(S.ev_free, D.xs));  // the set's keys and tickets are consumed
+            HIPCHK(c, hipMemcpyAsync(D.h_sa, D.sa, 16 * (u64)W, hipMemcpyDeviceToHost, D.xs));
+            HIPCHK(c, hipEventRecord(D.ev_acc, D.xs));
+            {
+                const double tw = now_s();
+                HIPCHK(c, hipEventSynchronize(D.ev_acc));
+                D.wait_seconds += now_s() - tw;
+            }
+            // ---- phase 2: the accepted states
+            u64 tot_st = 0;
+            for (int p = 0; p < W; ++p) {
+                const u64 ns = D.h_sa[p], nr = D.h_sa[W + p];
+                if (p != me && ns > kcap) return fail(c, RMC_E_HIP, "phase 2: more accepted states than keys sent");
+                soff[(size_t)p] = (u64)p * kcap * RB;
+                scnt[(size_t)p] = p == me ? 0 : ns * RB;
+                rcnt[(size_t)p] = p == me ? 0 : nr * RB;
+                roff[(size_t)p] = tot_st * RB;
+                tot_st += rcnt[(size_t)p] / RB;
+                if (p != me) D.states_sent += ns;
+            }
+            if (tot_st > (u64)W * kcap) return fail(c, RMC_E_CAPACITY, "phase-2 inbox full");
+            if (int rc = a2a(c, c->B.st_out, soff.data(), scnt.data(), D.st_in, roff.data(), rcnt.data())) return rc;
+            if (tot_st)
+                HIPCHK(c, launch(c->sh, 9, c->P, c->PT, c->B, tot_st, 0, D.st_in, nullptr, 0, nullptr, D.xs));
+            HIPCHK(c, hipEventRecord(S.x1, D.xs));
+            S.xtimed = 1;
             D.chunks += 1;
-            cursor = b;
-            if (!more) break;
+            if (!global_more) break;
         }
-        if (rho_lvl > 0) rho_prev = rho_lvl;
-        if (int rc = read_counters(c)) return rc;
-        if (int rc = level_end(hi)) return rc;
-        u64 nnew = 0, gen = 0, pr = 0;
-        for (const auto& r : rows) { nnew += r.nnew; gen += r.gen; pr += r.probes; }
+        // expansion of the next level reads what xs stored: the ctx stream waits for it
+        HIPCHK(c, hipEventRecord(D.ev_x, D.xs));
+        HIPCHK(c, hipStreamWaitEvent(c->st, D.ev_x, 0));
+        if (int rc = level_end()) return rc;
+        for (auto& S2 : D.set)  // exchange device time of the level's last round
+            if (S2.xtimed) {
+                D.xfer_seconds += 1e-3 * elapsed_ms(S2.x0, S2.x1);
+                S2.xtimed = 0;
+            }
+        u64 tot = 0, gen = 0, pr = 0;
+        for (const auto& r : rows) { tot += r.count; gen += r.generated; pr += r.probes; }
+        const u64 nnew = tot - total_prev;
+        total_prev = tot;
         generated += gen;
         probes += pr;
         c->level_start.push_back(c->h_ctr->count);
@@ -316,17 +456,16 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             }
         if (!c->have_target && (c->cfg.flags & RMC_FLAG_CHECK_DEADLOCK))
             for (int r = 0; r < W && !c->have_target; ++r)
-                if (rows[(size_t)r].dead != ~0ull) {
+                if (rows[(size_t)r].deadlock != ~0ull) {
                     c->res.deadlock = 1;
                     c->have_target = 1;
-                    c->target_idx = ((u64)r << 48) | rows[(size_t)r].dead;
+                    c->target_idx = ((u64)r << 48) | rows[(size_t)r].deadlock;
                 }
-        {  // progress: the same collectives on every rank, with or without a callback;
-           // all ranks stop together when rank 0's callback asks to
+        if (any_cb) {  // progress: the same collective on every rank; all stop when rank 0's callback asks to
             rmc_level_stats ls{};
             ls.level = nnew ? depth - 1 : depth;
             ls.generated = generated;
-            for (const auto& r : rows) ls.distinct += r.stored;
+            ls.distinct = tot;
             ls.new_states = nnew;
             ls.seconds = now_s() - t0;
             const int stop = (cb && cb(&ls, user)) ? 1 : 0;
@@ -340,21 +479,18 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         if (!nnew) break;
     }
     // ---- global summary
-    u64 mine = c->level_start.back();
-    std::vector<u64> all((size_t)W);
-    if (int rc = allgather(c, &mine, 8, all.data())) return rc;
-    u64 distinct = 0;
-    for (u64 x : all) distinct += x;
     c->res.generated = generated;
-    c->res.distinct = distinct;
+    c->res.distinct = total_prev;
     c->res.depth = depth;
     c->res.probes = probes;
-    c->res.stored_here = mine;
+    c->res.stored_here = c->level_start.back();
     c->res.keys_sent = D.keys_sent;
     c->res.states_sent = D.states_sent;
     c->res.chunks = D.chunks;
     c->res.exchange_seconds = D.xfer_seconds;
-    const double Dd = (double)distinct, G = (double)generated;
+    c->res.exchange_wait_seconds = D.wait_seconds;
+    c->res.parked = D.parked;
+    const double Dd = (double)total_prev, G = (double)generated;
     c->res.collision_probability = Dd * (G - Dd) / 18446744073709551616.0;
     c->res.seconds = now_s() - t0;
     return 0;
@@ -424,7 +560,7 @@ int rmc_rccl_unique_id(uint8_t id[128]) {
 
 int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, const rmc_transport* host,
               uint64_t keys_per_dest, uint64_t sent_cache_slots) {
-    if (!c || world < 1 || world > 64 || rank < 0 || rank >= world) return RMC_E_INVAL;
+    if (!c || world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return RMC_E_INVAL;
     if (!rccl_id && !(host && host->alltoallv && host->allgather))
         return fail(c, RMC_E_INVAL, "rmc_shard needs an RCCL id or a host transport");
     if (c->sh.verify) return fail(c, RMC_E_INVAL, "sharded mode does not support full-state verification");
@@ -437,28 +573,47 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     D.rccl = rccl_id != nullptr;
     if (host) D.host = *host;
     const u64 W = (u64)world;
-    const u64 kcap = keys_per_dest ? keys_per_dest : (1ull << 25);
-    const u64 scap = std::max<u64>(kcap / 4, 1024);
+    // keys one round may send one owner: 2^26 keys over all owners by default
+    // (2^25 at 2 ranks, 2^23 at 8), which bounds the outboxes and inboxes
+    const u64 kcap = keys_per_dest ? keys_per_dest : std::min<u64>(1ull << 25, std::max<u64>(1ull << 20, (1ull << 26) / W));
     u64 slots = 1;
     while (slots < std::max<u64>(sent_cache_slots ? sent_cache_slots : (1ull << 27), 1024)) slots <<= 1;
     const u64 RB = (u64)(c->NW + 2) * 4;
     D.sent_slots = slots;
     D.in_cap = W * kcap;
-    if (hipMalloc(&c->B.sent, slots * 8) != hipSuccess || hipMalloc(&c->B.key_out, W * kcap * 8) != hipSuccess ||
-        hipMalloc(&c->B.tick_out, W * kcap * 8) != hipSuccess || hipMalloc(&c->B.ocount, 8 * W) != hipSuccess ||
-        hipMalloc(&c->B.st_out, W * scap * RB) != hipSuccess || hipMalloc(&c->B.scount, 8 * W) != hipSuccess ||
-        hipMalloc(&D.key_in, W * kcap * 8) != hipSuccess || hipMalloc(&D.rep_out, W * kcap) != hipSuccess ||
-        hipMalloc(&D.rep_in, W * kcap) != hipSuccess || hipMalloc(&D.st_in, W * scap * RB) != hipSuccess ||
-        hipHostMalloc(&D.h_cnt, 16 * W, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&D.ag_dev, 4096 * (W + 1)) != hipSuccess) {
+    bool ok = hipStreamCreateWithFlags(&D.xs, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
+    const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
+    ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
+    for (auto& S : D.set) {
+        ok = ok && hipMalloc(&S.key_out, W * kcap * 8) == hipSuccess && hipMalloc(&S.tick_out, W * kcap * 8) == hipSuccess &&
+             hipMalloc(&S.ocount, 8 * W) == hipSuccess && hipMalloc(&S.cx, 8 * (4 * W + 1)) == hipSuccess &&
+             hipHostMalloc(&S.h_cx, 8 * (4 * W + 1), hipHostMallocDefault) == hipSuccess;
+        for (hipEvent_t* e : {&S.ev_exp, &S.ev_free})
+            ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+        for (hipEvent_t* e : {&S.k0, &S.k1, &S.x0, &S.x1}) ok = ok && hipEventCreate(e) == hipSuccess;
+    }
+    for (hipEvent_t* e : {&D.ev_cnt, &D.ev_acc, &D.ev_c, &D.ev_x})
+        ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipMalloc(&D.key_in, W * kcap * 8) == hipSuccess && hipMalloc(&D.rep_out, W * kcap) == hipSuccess &&
+         hipMalloc(&D.rep_in, W * kcap) == hipSuccess && hipMalloc(&c->B.st_out, W * kcap * RB) == hipSuccess &&
+         hipMalloc(&D.st_in, W * kcap * RB) == hipSuccess && hipMalloc(&D.sa, 16 * W) == hipSuccess &&
+         hipHostMalloc(&D.h_sa, 16 * W, hipHostMallocDefault) == hipSuccess &&
+         hipMalloc(&D.ag_dev, 4096 * (W + 1)) == hipSuccess;
+    if (!ok) {
         free_dist(c);
         return fail(c, RMC_E_NOMEM, "sharded-mode buffers do not fit (lower keys_per_dest / sent_cache_slots)");
     }
     D.ag_cap = 4096;
     D.debug = getenv("RMC_DIST_DEBUG") != nullptr;
+    if (const char* s = getenv("RMC_DIST_SPLIT")) D.split = std::max(1, std::min(64, atoi(s)));
+    if (const char* s = getenv("RMC_DIST_OVERLAP")) D.overlap = atoi(s) != 0;
+    if (const char* s = getenv("RMC_DIST_FILL")) D.fill = std::max(0.01, std::min(64.0, atof(s)));
     c->B.smask = slots - 1;
     c->B.kcap = kcap;
-    c->B.scap = scap;
+    c->B.scap = kcap;
+    c->B.scount = D.sa;
+    c->B.ovf_cap = ovf_cap;
     c->B.rank = (u32)rank;
     c->B.world = (u32)world;
     c->B.ref_tag = (u64)rank << 48;

@@ -21,6 +21,7 @@ struct Counters {
     u64 vchecked;   // fingerprint hits compared state against state
     u64 vcount;     // deferred hits in vbuf (stored twin not yet published)
     u64 nties;      // SYMMETRY: successors with tied signatures deferred to k_ties
+    u64 novf;       // sharded: keys that did not fit their owner's outbox (parked in B.ovf)
 };
 
 struct DevBufs {
@@ -43,8 +44,12 @@ struct DevBufs {
     u64 kcap;                  // keys per destination and chunk
     unsigned long long* ocount;  // [world] keys written per destination
     u32* st_out;               // [world][scap][NW + 2] accepted states for each owner
-    u64 scap;                  // state records per destination and round
+    u64 scap;                  // state records per destination and round (= kcap)
     unsigned long long* scount;  // [world] state records written per destination
+    // keys whose owner's outbox was full: {key, parent index | dest << 48 | lane << 56},
+    // sent in later exchange rounds of the same level (never dropped)
+    u64* ovf;
+    u64 ovf_cap;               // records in ovf
     // full-state verification mode: store index of the state owning each
     // fingerprint-set slot (~0 = not yet published; published between launches
     // by k_publish) and the deferred hits {parent index, slot | lane << 56}
@@ -89,8 +94,20 @@ struct SimCounters {
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
                       int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
 
-// Sharded mode, phase 1 owner side: insert n received keys, reply[t] = new.
-hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, hipStream_t st);
+// Sharded mode, phase 1 owner side: insert n received keys, reply[t] = new;
+// keys [src_off[p], src_off[p + 1]) came from rank p, acc[p] += keys of p that were new.
+constexpr int kMaxWorld = 64;
+struct SrcOff {
+    u64 o[kMaxWorld + 1];
+};
+hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, const SrcOff& so,
+                               unsigned long long* acc, hipStream_t st);
+// Sharded mode: the exchange-count row of one round, out[2p] = keys for rank p
+// (min(ocount[p], kcap), 0 for p = rank), out[2p + 1] = flags (bit 0: this rank
+// has more to send: host_more, or parked keys beyond ovf_done), out[2W] = novf.
+hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st);
+// Sharded mode: move parked keys ovf[a, a + n) into the (emptied) outbox; n <= kcap.
+hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st);
 
 // Fingerprint salt for the kernels of this device (0 = default hash).
 hipError_t set_fp_salt(u64 seed, hipStream_t st);

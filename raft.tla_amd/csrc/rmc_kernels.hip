@@ -478,7 +478,16 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         const int lane = l_lane[e];
         if (dest != B.rank) {  // the key to its owner, the ticket stays here
             if (slot >= B.kcap) {
-                atomicOr(&B.ctr->overflow, 2u);
+                // the owner's outbox is full: park the key with its ticket; a later
+                // exchange round of this level sends it (the sent-cache entry
+                // written at probe time stays right: the key IS sent)
+                const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
+                if (q < B.ovf_cap) {
+                    B.ovf[2 * q] = l_key[e];
+                    B.ovf[2 * q + 1] = (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56);
+                } else {
+                    atomicOr(&B.ctr->overflow, 2u);  // the parking buffer is full too: fatal
+                }
                 continue;
             }
             B.key_out[(u64)dest * B.kcap + slot] = l_key[e];
@@ -884,15 +893,66 @@ __global__ __launch_bounds__(256) void k_expand_dist(
 }
 
 // Sharded mode, phase 1, owner side: insert the keys other ranks sent;
-// reply[t] = 1 if key t was new here (its sender then ships the state).
-__global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64* keys, uint8_t* reply, u64 n) {
+// reply[t] = 1 if key t was new here (its sender then ships the state), and
+// acc[p] counts the new keys of source p — the states p will send in phase 2,
+// so the receive sizes need no second count exchange.  Keys arrive grouped by
+// source, so a wave mostly adds to one counter (one atomic per source present).
+__global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64* keys, uint8_t* reply, u64 n,
+                                                      const SrcOff so, unsigned long long* acc) {
     u64 pr = 0;
+    const int me = (int)__lane_id();
     for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
         const u64 t = t0 + threadIdx.x;
-        if (t < n) reply[t] = (uint8_t)fp_insert(B.table, B.tmask, keys[t], &B.ctr->table_full);
+        u32 src = 0xFFFFFFFFu;
+        if (t < n) {
+            const int isnew = fp_insert(B.table, B.tmask, keys[t], &B.ctr->table_full);
+            reply[t] = (uint8_t)isnew;
+            if (isnew) {
+                u32 p = 0;
+                while (p + 1 < B.world && so.o[p + 1] <= t) ++p;
+                src = p;
+            }
+        }
         pr += (u64)__popcll(__ballot(t < n));
+        u64 pending = __ballot(src != 0xFFFFFFFFu);
+        while (pending) {  // wave-uniform
+            const int l = __ffsll((long long)pending) - 1;
+            const u32 s = (u32)__builtin_amdgcn_readlane((int)src, l);
+            const u64 bal = __ballot(src == s);
+            if (me == l) atomicAdd(&acc[s], (unsigned long long)__popcll(bal));
+            pending &= ~bal;
+        }
     }
-    if (__lane_id() == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+    if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+}
+
+// Sharded mode: the count row of one exchange round (launch_pack_counts).
+__global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64* out) {
+    const u32 p = threadIdx.x;
+    const u64 novf = B.ctr->novf;
+    const u64 flags = host_more | (novf > ovf_done ? 1ull : 0ull);
+    if (p < B.world) {
+        const u64 c = B.ocount[p];
+        out[2 * p] = p == B.rank ? 0ull : (c < B.kcap ? c : B.kcap);
+        out[2 * p + 1] = flags;
+    }
+    if (p == 0) out[2 * B.world] = novf;
+}
+
+// Sharded mode: parked keys ovf[a, a + n) back into the outbox (n <= kcap, so
+// no destination can overflow; ocount was zeroed for this round).
+__global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
+    for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n; t += (u64)gridDim.x * 256ull) {
+        const u64 key = B.ovf[2 * (a + t)], tk = B.ovf[2 * (a + t) + 1];
+        const u32 dest = (u32)((tk >> 48) & 0xFFu);
+        const u64 slot = atomicAdd(&B.ocount[dest], 1ull);
+        if (slot >= B.kcap) {  // cannot happen for n <= kcap; never write past the outbox
+            atomicOr(&B.ctr->overflow, 2u);
+            continue;
+        }
+        B.key_out[(u64)dest * B.kcap + slot] = key;
+        B.tick_out[(u64)dest * B.kcap + slot] = (tk & ((1ull << 48) - 1)) | (tk & (0xFFull << 56));
+    }
 }
 
 // Sharded mode, phase 2, sender side: for every key an owner accepted
@@ -907,7 +967,8 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < total; t += (u64)gridDim.x * 256ull) {
         const u32 d = (u32)(t / per_dest);
         const u64 i = i0 + (t - (u64)d * per_dest);
-        if (d == B.rank || i >= B.ocount[d] || !reply[(u64)d * B.kcap + i]) continue;
+        const u64 sent = B.ocount[d] < B.kcap ? B.ocount[d] : B.kcap;  // beyond kcap: parked, not sent
+        if (d == B.rank || i >= sent || !reply[(u64)d * B.kcap + i]) continue;
         const u64 tick = B.tick_out[(u64)d * B.kcap + i];
         const u64 pidx = tick & ((1ull << 56) - 1);
         const int lane = (int)(tick >> 56);
@@ -1032,11 +1093,25 @@ __global__ __launch_bounds__(256) void k_probe_bench(u64* table, u64 mask, u32 i
     if (acc == 0x5A5A5A5A5A5A5A5Aull) sink[0] = acc;  // keeps the loads live
 }
 
-hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, hipStream_t st) {
+hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, const SrcOff& so,
+                               unsigned long long* acc, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     hipLaunchKernelGGL(k_owner_insert, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, st, B, keys,
-                       reply, n);
+                       reply, n, so, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st) {
+    if (B.world > (u32)kMaxWorld) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, st, B, host_more, ovf_done, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const u64 blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_drain, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st, B, a, n);
     return hipGetLastError();
 }
 

@@ -51,7 +51,8 @@ class Result(C.Structure):
                 ("collisions", C.c_uint64), ("verified", C.c_uint64),
                 ("keys_sent", C.c_uint64), ("states_sent", C.c_uint64), ("chunks", C.c_uint64),
                 ("exchange_seconds", C.c_double), ("stored_here", C.c_uint64),
-                ("spilled", C.c_uint64), ("spills", C.c_uint64), ("spill_seconds", C.c_double)]
+                ("spilled", C.c_uint64), ("spills", C.c_uint64), ("spill_seconds", C.c_double),
+                ("parked", C.c_uint64), ("exchange_wait_seconds", C.c_double)]
 
 
 class LevelStats(C.Structure):

@@ -71,10 +71,12 @@ def main():
         summary = {k: getattr(r, k) for k in fields}
         per_rank = [None] * world
         dist.all_gather_object(per_rank, dict(rank=rank, stored=r.stored_here, keys_sent=r.keys_sent,
-                                              states_sent=r.states_sent, chunks=r.chunks,
-                                              summary=summary, exchange_s=r.exchange_seconds))
+                                              states_sent=r.states_sent, chunks=r.chunks, parked=r.parked,
+                                              summary=summary, exchange_s=r.exchange_seconds,
+                                              wait_s=r.exchange_wait_seconds))
     if rank == 0:
         json.dump(dict(summary, levels=levels, keys_sent=sum(p["keys_sent"] for p in per_rank),
+                       parked=sum(p["parked"] for p in per_rank),
                        states_sent=sum(p["states_sent"] for p in per_rank), per_rank=per_rank,
                        wall_s=wall, transport=info.transport,
                        trace=[[f, i, bytes(v).hex()] for f, i, v in trace],

@@ -138,3 +138,29 @@ def test_sharded_full_bench_model_equals_single_gpu(tmp_path):
     assert (res["distinct"], res["generated"], res["depth"]) == (1_227_465_177, 21_130_972_267, 56)
     assert sum(p["stored"] for p in res["per_rank"]) == 1_227_465_177
     assert res["keys_sent"] > 0 and res["states_sent"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,nproc,overlap", [("small", 2, "1"), ("small_sym", 3, "0"), ("s4_prefix10", 2, "1")])
+def test_sharded_outbox_overflow_is_recovered(case, nproc, overlap, tmp_path):
+    """an owner's key outbox that fills is not fatal.  With
+    4096 keys per owner and round, and rounds sized for 3x that (RMC_DIST_FILL=3),
+    the outboxes overflow on every large level; the parked keys go out
+    in further rounds of the same level and the counts equal the oracle's.
+    overlap "0" runs the rounds without the next expansion queued early
+    (RMC_DIST_OVERLAP=0): same counts."""
+    g = GOLDEN[case]
+    out = tmp_path / "r.json"
+    env_over = dict(os.environ, RMC_DIST_OVERLAP=overlap, RMC_DIST_FILL="3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29680 + nproc),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out", str(out), "--device", "0",
+           "--backend", "gloo", "--keys-per-dest", "4096", "--rerun", "1"]
+    env_over["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env_over, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert (res["distinct"], res["generated"], res["depth"]) == (g["distinct"], g["generated"], g["depth"])
+    assert res["levels"] == g["level_new"]
+    assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
+    assert res["parked"] > 0  # the outboxes did overflow
