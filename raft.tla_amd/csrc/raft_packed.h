@@ -118,6 +118,7 @@ RMC_HD u32 owner_of(u64 key, u32 world) { return (u32)(((key >> 32) * (u64)world
 struct Params {
     int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;
     int off[11];  // family lane offsets (= Lanes<S,K>::off, for host code)
+    int diamond;  // 1: commuting-diamond successors are not probed (RMC_DIAMOND=0 turns it off)
     u64 fp_mask;  // full-state verification mode: fingerprint bits kept (~0 = all; fewer only
                   // to provoke collisions in tests, rmc_set_fp_bits)
 };
@@ -404,7 +405,7 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
 // Returns 1 if the successor is in the model; *h receives its fingerprint.
 template <int S, int K>
 RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d, const Params& P,
-                    u64* h) {
+                    u64* h, int* nmsg_out = nullptr) {
     u64 hh = h0;
     int nmsg = 0;
 #pragma unroll
@@ -437,6 +438,7 @@ RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d
     }
     if (nmsg > P.max_msgs) return 0;
     *h = hh;
+    if (nmsg_out) *nmsg_out = nmsg;
     return 1;
 }
 
@@ -471,7 +473,7 @@ RMC_HD u64 sel64(const u64 (&a)[N], int i) {
 // delta_fp with the parent's mixes precomputed: same result, fewer mixes.
 template <int S, int K>
 RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
-                        const Params& P, u64* h) {
+                        const Params& P, u64* h, int* nmsg_out = nullptr) {
     u64 hh = pm.h0;
     int nmsg = pm.nmsg;
     if (d.srv >= 0) {
@@ -502,6 +504,7 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
     }
     if (nmsg > P.max_msgs) return 0;
     *h = hh;
+    if (nmsg_out) *nmsg_out = nmsg;
     return 1;
 }
 
@@ -649,6 +652,111 @@ RMC_HD void materialise(const u64 (&w)[S], const u32 (&m)[K], const Delta& d, u6
             mo[q + 1] = a > b ? b : a;
         }
     }
+}
+
+// ---- commuting diamonds: successors that need no probe ------------------------------
+// Every stored state t remembers its first discoverer (parent s, lane a:
+// t = a(s)); the footprint word below keeps the messages a acted on and
+// added.  Expanding t, a successor b(t) is not probed when
+//   (1) b precedes a in a fixed, state-independent order of action instances
+//       (family, then the lane for server actions, the message for bag ones);
+//   (2) a and b are independent: different server words (a lane reads and
+//       writes at most one: Restart..AppendEntries their server i, Receive
+//       the message's mdest, Duplicate/Drop none) and disjoint messages;
+//   (3) b(s) satisfies the CONSTRAINT (only |DOMAIN messages| can differ from
+//       b(t), by a's net change of the domain).
+// Then b is enabled at s with the same effect and a(b(s)) = b(a(s)) = b(t):
+// b(t) is generated from b(s), a state of the same or an earlier level, in
+// the same or an earlier pass — and if a is skipped there too, the lane it
+// relies on is later still in the order, so the chain ends.  Skipped
+// successors still count as generated (TLC counts them); distinct counts,
+// levels and depth are unchanged (tests/native/diamond_model.cpp checks it
+// on whole BFS runs).  Not under SYMMETRY (canonical representatives break
+// the instance order).
+constexpr u64 FOOT_VALID = 1ull << 63, FOOT_ACT = 1ull << 62, FOOT_ADD = 1ull << 61, FOOT_CONSUMED = 1ull << 60;
+
+// Family of a lane from the runtime offsets (wave-uniform lanes: scalar compares).
+RMC_HD int lane_family(const Params& P, int lane) {
+    int f = 0;
+#pragma unroll
+    for (int k = 1; k <= 9; ++k) f += lane >= P.off[k] ? 1 : 0;
+    return f;
+}
+RMC_HD int family_off(const Params& P, int f) {
+    int o = 0;
+#pragma unroll
+    for (int k = 0; k <= 9; ++k) o = f == k ? P.off[k] : o;
+    return o;
+}
+
+// The footprint of t = lane(parent (w, m)) with delta d.
+template <int S, int K>
+RMC_HD u64 make_foot(const u32 (&m)[K], int lane, const Delta& d, const Params& P) {
+    u64 f = FOOT_VALID;
+    if (lane >= P.off[7]) {
+        const int q = lane - (lane < P.off[8] ? P.off[7] : lane < P.off[9] ? P.off[8] : P.off[9]);
+        f |= FOOT_ACT | (u64)(selm<K>(m, q) & MSG_MASK);
+        if (d.rm >= 0) f |= FOOT_CONSUMED;
+    }
+    if (d.has_add) f |= FOOT_ADD | ((u64)(d.add & MSG_MASK) << 30);
+    return f;
+}
+
+template <int S>
+RMC_HD int lane_server(const Params& P, int lane, int fam, u32 msg) {
+    const int t = lane - family_off(P, fam);
+    return (fam == 0 || fam == 1 || fam == 3 || fam == 5) ? t
+         : (fam == 2 || fam == 6) ? t / S
+         : fam == 4 ? t / VMAX
+         : fam == 7 ? (int)m_dst(msg) : -1;
+}
+
+template <int K>
+RMC_HD int count_of(const u32 (&m)[K], u32 msg) {
+    u32 c = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) c |= (m[q] && (m[q] & MSG_MASK) == msg) ? m_cnt(m[q]) : 0u;
+    return (int)c;
+}
+
+// Per expanded state: a's side of the test (lane a = act, its footprint).
+struct Diamond {
+    u64 ord;   // a's instance order key; 0 = no skipping from this state
+    u32 k0, k1;  // a's messages (sentinels when absent; never equal to a 30-bit message)
+    int srv;   // a's server word, -1 none
+    int dom;   // max |DOMAIN messages| of b(t) so that b(s) is in the model
+};
+template <int S, int K>
+RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diamond& dm) {
+    dm.ord = 0;
+    dm.k0 = 0xFFFFFFFFu;
+    dm.k1 = 0xFFFFFFFEu;
+    dm.srv = -1;
+    dm.dom = 0;
+    if (a == 255 || !(foot & FOOT_VALID)) return;
+    const int fa = lane_family(P, a);
+    const u32 mact = (u32)(foot & MSG_MASK), madd = (u32)((foot >> 30) & MSG_MASK);
+    dm.ord = ((u64)fa << 40) | (fa < 7 ? (u64)a : (u64)mact) | (1ull << 48);
+    if (foot & FOOT_ACT) dm.k0 = mact;
+    if (foot & FOOT_ADD) dm.k1 = madd;
+    dm.srv = lane_server<S>(P, a, fa, mact);
+    int delta = 0;
+    if ((foot & FOOT_ADD) && count_of<K>(m, madd) == 1) delta += 1;       // a created the key
+    if ((foot & FOOT_CONSUMED) && count_of<K>(m, mact) == 0) delta -= 1;  // a removed its last copy
+    dm.dom = P.max_msgs + delta;
+}
+// b's side: lane b with delta db on t (m = t's bag), nmsg_b = |DOMAIN| of b(t).
+template <int S, int K>
+RMC_HD bool diamond_skip(const u32 (&m)[K], int b, const Delta& db, int nmsg_b, const Diamond& dm, const Params& P) {
+    const int fb = lane_family(P, b);
+    const u32 mb = fb >= 7 ? (selm<K>(m, b - family_off(P, fb)) & MSG_MASK) : 0xFFFFFFFDu;
+    const u64 ob = ((u64)fb << 40) | (fb < 7 ? (u64)b : (u64)mb) | (1ull << 48);
+    if (!(ob < dm.ord)) return false;  // dm.ord = 0: never
+    const int sb = lane_server<S>(P, b, fb, mb);
+    if (sb >= 0 && sb == dm.srv) return false;
+    const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
+    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
+    return nmsg_b <= dm.dom;
 }
 
 // ---- invariants (fused into the insert of a new state) -----------------------------

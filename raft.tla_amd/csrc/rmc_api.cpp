@@ -67,6 +67,10 @@ void fill_params(rmc_ctx* c) {
     P.inv_mask = (int)g.invariants;
     P.symmetry = c->sh.sym ? 1 : 0;
     P.fp_mask = ~0ull;
+    {  // commuting-diamond probe elimination (not under SYMMETRY; RMC_DIAMOND=0 turns it off)
+        const char* e = getenv("RMC_DIAMOND");
+        P.diamond = (!c->sh.sym && !(e && e[0] == '0')) ? 1 : 0;
+    }
     const int S = c->sh.S, K = c->sh.K;
     const int sizes[10] = {S, S, S * S, S, S * VMAX, S, S * S, K, K, K};  // = Lanes<S,K>
     P.off[0] = 0;
@@ -289,6 +293,7 @@ void spill_rebase(rmc_ctx* c, u64 base) {
     c->B.store = (u32*)((uintptr_t)X.store - (uintptr_t)base * nw * 4);
     c->B.parent = (u64*)((uintptr_t)X.parent - (uintptr_t)base * 8);
     c->B.act = (uint8_t*)((uintptr_t)X.act - (uintptr_t)base);
+    c->B.foot = (u64*)((uintptr_t)X.foot - (uintptr_t)base * 8);
     c->B.cap = base + X.win;
 }
 
@@ -359,6 +364,7 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
                                  hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.parent + off, X.parent + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.act + off, X.act + n + off, k, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipMemcpyAsync(X.foot + off, X.foot + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
     }
     HIPCHK(c, hipStreamSynchronize(c->st));
     spill_rebase(c, a);
@@ -441,7 +447,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     }
 
     // ---- capacity: state store + parents + lanes + fingerprint set (load <= 0.5)
-    const u64 per_state = (u64)c->NW * 4 + 8 + 1;
+    const u64 per_state = (u64)c->NW * 4 + 8 + 1 + 8;  // state, parent, lane, footprint
     const bool spill = (cfg->flags & RMC_FLAG_SPILL) != 0;
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -467,6 +473,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     c->B.tmask = slots - 1;
     if (hipMalloc(&c->B.store, win * (u64)c->NW * 4) != hipSuccess ||
         hipMalloc(&c->B.parent, win * 8) != hipSuccess || hipMalloc(&c->B.act, win) != hipSuccess ||
+        hipMalloc(&c->B.foot, win * 8) != hipSuccess ||
         hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
         hipMalloc(&c->d_staged, (size_t)c->NW * 4 * 64) != hipSuccess) {
         c->err = "device allocation failed (capacity " + std::to_string(win) + " states)";
@@ -478,6 +485,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     c->spill.store = c->B.store;
     c->spill.parent = c->B.parent;
     c->spill.act = c->B.act;
+    c->spill.foot = c->B.foot;
     if (spill && spill_reserve(c)) return bail(RMC_E_NOMEM);
     if (hipHostMalloc(&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
         c->err = "pinned allocation failed";
@@ -513,6 +521,7 @@ void rmc_destroy(rmc_ctx* c) {
     (void)hipFree(c->spill.store ? c->spill.store : c->B.store);
     (void)hipFree(c->spill.parent ? c->spill.parent : c->B.parent);
     (void)hipFree(c->spill.act ? c->spill.act : c->B.act);
+    (void)hipFree(c->spill.foot ? c->spill.foot : c->B.foot);
     (void)hipFree(c->B.table);
     (void)hipFree(c->B.ctr);
     (void)hipFree(c->d_staged);
@@ -864,6 +873,10 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     };
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
+    // footprints are not checkpointed: the recovered frontier is expanded without
+    // diamond skipping (FOOT_VALID clear), the levels after it with
+    HIPCHK(c, hipMemsetAsync(c->spill.on ? c->spill.foot : c->B.foot, 0,
+                             (c->spill.on ? c->spill.win : c->B.cap) * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
     if (s) get(c->spill.h_parent, s * 8);

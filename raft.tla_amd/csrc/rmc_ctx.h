@@ -75,6 +75,7 @@ struct SpillState {
     rmc::u32* store = nullptr;  // the real device allocations
     rmc::u64* parent = nullptr;
     uint8_t* act = nullptr;
+    rmc::u64* foot = nullptr;
     rmc::u64* h_parent = nullptr;  // host, [total_cap], reserved address space,
     uint8_t* h_act = nullptr;      // pages touched as levels spill
     size_t h_bytes = 0;

@@ -189,7 +189,7 @@ void free_dist(rmc_ctx* c) {
 int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     DistState& D = c->dist;
     const int W = D.world, me = D.rank;
-    const u64 RB = (u64)(c->NW + 2) * 4;  // state record: packed state + global parent ref
+    const u64 RB = (u64)(c->NW + 4) * 4;  // state record: packed state, global parent ref, footprint
     const u64 kcap = c->B.kcap;
     const double t0 = now_s();
     c->res = rmc_result{};
@@ -578,7 +578,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     const u64 kcap = keys_per_dest ? keys_per_dest : std::min<u64>(1ull << 25, std::max<u64>(1ull << 20, (1ull << 26) / W));
     u64 slots = 1;
     while (slots < std::max<u64>(sent_cache_slots ? sent_cache_slots : (1ull << 27), 1024)) slots <<= 1;
-    const u64 RB = (u64)(c->NW + 2) * 4;
+    const u64 RB = (u64)(c->NW + 4) * 4;
     D.sent_slots = slots;
     D.in_cap = W * kcap;
     bool ok = hipStreamCreateWithFlags(&D.xs, hipStreamNonBlocking) == hipSuccess;

@@ -28,6 +28,7 @@ struct DevBufs {
     u32* store;      // packed states, (2S + K) words each; levels are contiguous ranges
     u64* parent;     // parent index per state (~0 for initial states)
     uint8_t* act;    // lane that produced the state (255 for initial states)
+    u64* foot;       // messages the producing lane acted on / added (make_foot; 0 = unknown)
     u64* table;      // fingerprint set, power-of-two slots, 0 = empty
     u64 tmask;       // slots - 1
     u64 cap;         // state store capacity
@@ -43,7 +44,7 @@ struct DevBufs {
     u64* tick_out;             // [world][kcap] local tickets: parent index | lane << 56
     u64 kcap;                  // keys per destination and chunk
     unsigned long long* ocount;  // [world] keys written per destination
-    u32* st_out;               // [world][scap][NW + 2] accepted states for each owner
+    u32* st_out;               // [world][scap][NW + 4] accepted states for each owner (+ ref, footprint)
     u64 scap;                  // state records per destination and round (= kcap)
     unsigned long long* scount;  // [world] state records written per destination
     // keys whose owner's outbox was full: {key, parent index | dest << 48 | lane << 56},

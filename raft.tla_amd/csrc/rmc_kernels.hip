@@ -130,6 +130,7 @@ __device__ __forceinline__ void commit_new(int is_new, const u64 (&w)[S], const 
     store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
     B.parent[ni] = parent_idx;
     B.act[ni] = (uint8_t)lane;
+    B.foot[ni] = 0;  // initial states and deferred SYMMETRY ties: no diamond skipping from them
     const int v = check_invariants<S, K>(wo, mo, P);
     if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
 }
@@ -176,6 +177,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
         B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
+        B.foot[ni] = make_foot<S, K>(m, lane, d, P);
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
@@ -242,6 +244,7 @@ __device__ __forceinline__ void flush_new_sorted(const Params& P, const DevBufs&
         store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
         B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
+        B.foot[ni] = make_foot<S, K>(m, lane, d, P);
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
@@ -509,6 +512,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
         B.parent[slot] = B.ref_tag | (lo + rel);
         B.act[slot] = (uint8_t)lane;
+        B.foot[slot] = make_foot<S, K>(m, lane, d, P);
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
     }
@@ -521,9 +525,12 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // DIST: sharded mode — successors owned by another rank are looked up in the
 // local sent-cache instead of the set and, if not sent before, shipped
 // through the outbox (flush_dist).
+// DIA: commuting-diamond successors are not probed (raft_packed.h "commuting
+// diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool SORT = false, bool WSORT = false, bool FSORT = true>
+          bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
+    static_assert(!DIA || (!SYM && !VERIFY), "diamond skipping: not under SYMMETRY or verification");
     constexpr int NW = 2 * S + K;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
     // SORT: class-sorted flushes + the wave walks only lane_superset's lanes
@@ -639,6 +646,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         }
         SymParent<S, K> spar;  // SYMMETRY, incremental keys: the parent's frame
         if constexpr (SYMINC) sym_parent<S, K>(w, m, sbase, spar);
+        Diamond dm;  // DIA: how this state was discovered (lane + footprint), once per state
+        if constexpr (DIA) {
+            const bool on = live && P.diamond;
+            diamond_of<S, K>(m, on ? (int)B.act[lo + rel] : 255, on ? B.foot[lo + rel] : 0ull, P, dm);
+        }
         u32 g = 0;
         // SORT: the lanes some state of this wave can enable (wave-uniform, scalar)
         u64 wm = 0;
@@ -686,8 +698,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                             }
                         }
                     } else if (en) {
-                        if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h);
-                        else in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
+                        int nmb = 0;
+                        if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr);
+                        else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
+                        if constexpr (DIA)
+                            if (in_model && h != h0 && diamond_skip<S, K>(m, lane, d, nmb, dm, P)) in_model = 0;
                         if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
                     }
                     if (in_model && (SYM || h != h0)) {
@@ -864,7 +879,7 @@ template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -887,7 +902,7 @@ template <int S, int K, int BATCH, bool WS>
 __global__ __launch_bounds__(256) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, false, false, true, true, false>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, false, false, true, true, false, true>(P, PT, B, lo, hi);
     else
         expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
@@ -962,7 +977,7 @@ __global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, const DevBufs B, const uint8_t* reply,
                                                             u64 per_dest, u64 i0) {
-    constexpr int NW = 2 * S + K, RW = NW + 2;
+    constexpr int NW = 2 * S + K, RW = NW + 4;  // state, parent ref, footprint
     const u64 total = per_dest * B.world;  // window [i0, i0 + per_dest) of every destination's keys
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < total; t += (u64)gridDim.x * 256ull) {
         const u32 d = (u32)(t / per_dest);
@@ -990,6 +1005,9 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
         const u64 ref = B.ref_tag | ((u64)lane << 40) | pidx;
         r[NW] = (u32)ref;
         r[NW + 1] = (u32)(ref >> 32);
+        const u64 ft = make_foot<S, K>(m, lane, dl, P);
+        r[NW + 2] = (u32)ft;
+        r[NW + 3] = (u32)(ft >> 32);
     }
 }
 
@@ -998,7 +1016,7 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
 // wave, parent ref and lane from the record, fused invariants.
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevBufs B, const u32* inbox, u64 n) {
-    constexpr int NW = 2 * S + K, RW = NW + 2;
+    constexpr int NW = 2 * S + K, RW = NW + 4;  // state, parent ref, footprint
     const int me = (int)__lane_id();
     const u64 lt = (1ull << me) - 1ull;
     for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
@@ -1024,6 +1042,7 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
         const u64 ref = (u64)r[NW] | ((u64)r[NW + 1] << 32);
         B.parent[ni] = ref & ~(0xFFull << 40);
         B.act[ni] = (uint8_t)(ref >> 40);
+        B.foot[ni] = (u64)r[NW + 2] | ((u64)r[NW + 3] << 32);
         const int v = check_invariants<S, K>(w, m, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }

@@ -6,6 +6,7 @@
 // state graph", "Error: Invariant ... is violated", "State N:") keep working.
 // It is the host side above the C ABI (include/rmc.h); Java users bind the
 // same symbols through Panama.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -14,6 +15,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../../include/rmc.h"
 
@@ -289,65 +292,101 @@ int main(int argc, char** argv) {
     rc = rmc_create(&c, &ctx);
     if (rc) { printf("Error: rmc_create failed (%d)\n", rc); return 1; }
     // -gpus N: one ctx per GPU (devices device..device+N-1), each a rank of the
-    // sharded search on librmc's RCCL communicator; ranks 1..N-1 run on helper
-    // threads and take part in every collective (the BFS and the trace walk)
-    std::vector<std::thread> helpers;
+    // sharded search on librmc's RCCL communicator, each driven by its own
+    // thread through every collective (the BFS and the trace walk).  All
+    // contexts are created before any communicator exists, and a rank that
+    // fails later ends the process (stdout flushed, exit code 1) instead of
+    // leaving the other ranks blocked in a collective.
+    std::vector<rmc_state_view> tr_st;
+    std::vector<int32_t> tr_fam, tr_inst;
+    rmc_result r{};
     if (gpus > 1) {
         if (verify || !ckpt.empty() || !recover.empty()) {
             printf("Error: -verify, -checkpoint and -recover are single-GPU options\n");
+            rmc_destroy(ctx);
             return 1;
+        }
+        std::vector<rmc_ctx*> ctxs((size_t)gpus, nullptr);
+        ctxs[0] = ctx;
+        for (int k = 1; k < gpus; ++k) {
+            rmc_config cr = c;
+            cr.device = device + k;
+            if (rmc_create(&cr, &ctxs[(size_t)k])) {
+                printf("Error: rank %d: rmc_create on device %d failed\n", k, cr.device);
+                for (rmc_ctx* x : ctxs) rmc_destroy(x);
+                return 1;
+            }
         }
         uint8_t id[128];
         if (rmc_rccl_unique_id(id)) { printf("Error: rmc_rccl_unique_id failed\n"); return 1; }
-        for (int r = 1; r < gpus; ++r) {
-            helpers.emplace_back([=]() {
-                rmc_config cr = c;
-                cr.device = device + r;
-                rmc_ctx* h = nullptr;
-                if (rmc_create(&cr, &h)) { fprintf(stderr, "rank %d: rmc_create failed\n", r); return; }
-                if (rmc_shard(h, r, gpus, id, nullptr, 0, 0)) { fprintf(stderr, "rank %d: %s\n", r, rmc_last_error(h)); return; }
-                if (rmc_run_bfs(h, nullptr, nullptr)) { fprintf(stderr, "rank %d: %s\n", r, rmc_last_error(h)); return; }
+        printf("Sharded over %d GPUs (librmc two-phase exchange over RCCL).\n", gpus);
+        printf("Computing initial states...\n");
+        fflush(stdout);
+        std::atomic<int> done{0}, failed{-1};
+        std::vector<std::string> errs((size_t)gpus);
+        std::vector<std::thread> ranks;
+        for (int k = 0; k < gpus; ++k) {
+            ranks.emplace_back([&, k]() {
+                rmc_ctx* h = ctxs[(size_t)k];
+                auto bad = [&](const char* what) {
+                    errs[(size_t)k] = std::string(what) + ": " + rmc_last_error(h);
+                    int none = -1;
+                    failed.compare_exchange_strong(none, k);
+                };
+                if (rmc_shard(h, k, gpus, id, nullptr, 0, 0)) { bad("rmc_shard"); return; }
+                if (rmc_run_bfs(h, k == 0 ? progress : nullptr, nullptr)) { bad("rmc_run_bfs"); return; }
                 rmc_result rr;
                 rmc_get_result(h, &rr);
-                if (rr.violated_inv || rr.deadlock) {  // the trace walk is collective: same calls as rank 0
+                if (rr.violated_inv || rr.deadlock) {  // the trace walk is collective: every rank calls it
                     size_t n = 0;
-                    rmc_trace(h, nullptr, nullptr, nullptr, 0, &n);
+                    if (rmc_trace(h, nullptr, nullptr, nullptr, 0, &n)) { bad("rmc_trace"); return; }
                     std::vector<rmc_state_view> st(n);
                     std::vector<int32_t> f(n), in(n);
-                    rmc_trace(h, st.data(), f.data(), in.data(), n, &n);
+                    if (rmc_trace(h, st.data(), f.data(), in.data(), n, &n)) { bad("rmc_trace"); return; }
+                    if (k == 0) { tr_st.swap(st); tr_fam.swap(f); tr_inst.swap(in); }
                 }
-                rmc_destroy(h);
+                done.fetch_add(1);
             });
         }
-        rc = rmc_shard(ctx, 0, gpus, id, nullptr, 0, 0);
-        if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); return 1; }
-        printf("Sharded over %d GPUs (librmc two-phase exchange over RCCL).\n", gpus);
-    }
-    if (!recover.empty()) {
-        rc = rmc_recover(ctx, recover.c_str());
-        if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
-        printf("Recovering from checkpoint %s...\n", recover.c_str());
+        while (done.load() < gpus && failed.load() < 0) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        if (failed.load() >= 0) {
+            printf("Error: rank %d: %s\n", failed.load(), errs[(size_t)failed.load()].c_str());
+            fflush(stdout);
+            fflush(stderr);
+            _exit(1);  // the other ranks may be blocked in a collective of the failed one
+        }
+        for (auto& t : ranks) t.join();
+        rmc_get_result(ctx, &r);
+        for (int k = 1; k < gpus; ++k) rmc_destroy(ctxs[(size_t)k]);
     } else {
-        printf("Computing initial states...\n");
+        if (!recover.empty()) {
+            rc = rmc_recover(ctx, recover.c_str());
+            if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
+            printf("Recovering from checkpoint %s...\n", recover.c_str());
+        } else {
+            printf("Computing initial states...\n");
+        }
+        rc = rmc_run_bfs(ctx, progress, nullptr);
+        if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
+        rmc_get_result(ctx, &r);
+        if (r.violated_inv || r.deadlock) {
+            size_t len = 0;
+            rmc_trace(ctx, nullptr, nullptr, nullptr, 0, &len);
+            tr_st.resize(len);
+            tr_fam.resize(len);
+            tr_inst.resize(len);
+            rmc_trace(ctx, tr_st.data(), tr_fam.data(), tr_inst.data(), len, &len);
+        }
     }
-    rc = rmc_run_bfs(ctx, progress, nullptr);
-    if (rc) { printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 1; }
-    rmc_result r;
-    rmc_get_result(ctx, &r);
     int exitcode = 0;
     if (r.violated_inv || r.deadlock) {
         if (r.violated_inv) printf("Error: Invariant %s is violated.\n", inv_name(r.violated_inv));
         else printf("Error: Deadlock reached.\n");
         printf("Error: The behavior up to this point is:\n");
-        size_t len = 0;
-        rmc_trace(ctx, nullptr, nullptr, nullptr, 0, &len);
-        std::vector<rmc_state_view> st(len);
-        std::vector<int32_t> fam(len), inst(len);
-        rmc_trace(ctx, st.data(), fam.data(), inst.data(), len, &len);
-        for (size_t k = 0; k < len; ++k) {
-            if (fam[k] < 0 || k == 0) printf("State %zu: <Initial predicate>\n", k + 1);
-            else printf("State %zu: %s\n", k + 1, step_header(fam[k], inst[k], st[k - 1]).c_str());
-            print_state(st[k]);
+        for (size_t k = 0; k < tr_st.size(); ++k) {
+            if (tr_fam[k] < 0 || k == 0) printf("State %zu: <Initial predicate>\n", k + 1);
+            else printf("State %zu: %s\n", k + 1, step_header(tr_fam[k], tr_inst[k], tr_st[k - 1]).c_str());
+            print_state(tr_st[k]);
             printf("\n");
         }
         exitcode = 12;
@@ -366,6 +405,11 @@ int main(int argc, char** argv) {
     if (r.spills)
         printf("Spilled %llu expanded states to host memory in %llu spills (%.2fs).\n",
                (unsigned long long)r.spilled, (unsigned long long)r.spills, r.spill_seconds);
+    if (gpus > 1)
+        printf("Exchange (rank 0): %llu rounds, %llu keys and %llu states sent, %llu keys parked, "
+               "%.1fms of exchange on the device, %.1fms waited on the host.\n",
+               (unsigned long long)r.chunks, (unsigned long long)r.keys_sent, (unsigned long long)r.states_sent,
+               (unsigned long long)r.parked, r.exchange_seconds * 1e3, r.exchange_wait_seconds * 1e3);
     if (!ckpt.empty() && r.left_on_queue > 0 && !r.violated_inv && !r.deadlock) {
         if (rmc_checkpoint(ctx, ckpt.c_str())) printf("Error: %s\n", rmc_last_error(ctx));
         else printf("Checkpoint written to %s (%llu states on the queue).\n", ckpt.c_str(),
@@ -375,7 +419,6 @@ int main(int argc, char** argv) {
         printf("Finished in %.0fms (%.0f distinct states/s)\n", r.seconds * 1e3, r.distinct / (r.seconds > 0 ? r.seconds : 1));
     else
         printf("Finished in %.0fms after recovery (counts include the checkpointed levels)\n", r.seconds * 1e3);
-    for (auto& t : helpers) t.join();
     rmc_destroy(ctx);
     return exitcode;
 }

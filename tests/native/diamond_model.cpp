@@ -1,0 +1,238 @@
+// Host model of commuting-diamond probe elimination.
+//
+// A BFS on the packed encoding (raft_packed.h, the kernels' own lane code),
+// recording for every stored state t its first discoverer: parent s and lane
+// a, t = a(s).  When t is expanded, a successor b(t) need not be probed when
+//   (1) b precedes a in a fixed, state-independent order of action instances
+//       (family, then the lane index for server actions, the message for bag
+//       actions);
+//   (2) a and b are independent: they read/write different server words
+//       (a lane touches at most one: Restart..AppendEntries their server i,
+//       Receive the message's mdest, Duplicate/Drop none) and touch disjoint
+//       messages (the message acted on, the message added);
+//   (3) b(s) satisfies the CONSTRAINT (only |DOMAIN messages| can differ from
+//       b(t): by a's net change of the bag's domain).
+// Then b is enabled at s with the same effect, a is enabled at b(s), and
+// a(b(s)) = b(a(s)) = b(t): the state is generated from b(s), a state of the
+// same or an earlier level, in the same or an earlier pass.  Successors whose
+// probe is skipped still count as generated (TLC counts them).  Mode "check"
+// runs the BFS twice, without and with skipping, and requires identical
+// per-level counts; mode "count" reports the skippable fraction of probes.
+// Build: g++ -O2 -std=c++17 -I raft.tla_amd/csrc diamond_model.cpp
+// Run:   ./a.out S V MaxTerm MaxLogLen MaxMsgs MaxDup max_levels
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "raft_packed.h"
+
+using namespace rmc;
+
+namespace {
+
+struct Foot {  // what the kernels would store per state: the discovering lane's messages
+    u32 m_act;   // message acted on (Receive / Duplicate / Drop), 0 otherwise
+    u32 m_add;   // message added, 0 when none
+    uint8_t consumed, has_add, has_act;
+};
+
+template <int S, int K>
+struct Model {
+    Params P{};
+    int nl = Lanes<S, K>::N;
+    std::vector<u64> W;      // S words per state
+    std::vector<u32> M;      // K slots per state
+    std::vector<uint8_t> act;
+    std::vector<Foot> foot;
+    std::vector<u64> hfoot;  // the kernels' footprint word (make_foot)
+    std::vector<u64> table;
+    u64 mask = 0;
+
+    int family(int lane) const {
+        int f = 0;
+        while (f < 9 && lane >= P.off[f + 1]) ++f;
+        return f;
+    }
+    bool insert(u64 key) {
+        key = key ? key : 1;
+        for (u64 s = key & mask;; s = (s + 1) & mask) {
+            if (table[s] == key) return false;
+            if (!table[s]) { table[s] = key; return true; }
+        }
+    }
+    // the server word a lane reads/writes (-1: none) and the message it acts on
+    int lane_server(int lane, u32 msg) const {
+        const int f = family(lane);
+        const int t = lane - P.off[f];
+        switch (f) {
+            case 0: case 1: case 3: case 5: return t;
+            case 2: case 6: return t / S;
+            case 4: return t / VMAX;
+            case 7: return (int)m_dst(msg);
+            default: return -1;
+        }
+    }
+    u64 order_key(int lane, u32 msg) const {
+        const int f = family(lane);
+        return ((u64)f << 40) | (f < 7 ? (u64)lane : (u64)(msg & MSG_MASK));
+    }
+    static int cnt_of(const u32 (&m)[K], u32 msg) {
+        for (int q = 0; q < K; ++q)
+            if (m[q] && (m[q] & MSG_MASK) == msg) return (int)m_cnt(m[q]);
+        return 0;
+    }
+    // |DOMAIN messages| of the successor of delta d on (w, m)
+    static int dom_after(const u32 (&m)[K], const Delta& d) {
+        int n = 0;
+        for (int q = 0; q < K; ++q) n += m[q] ? 1 : 0;
+        if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) n -= 1;
+        if (d.has_add && !cnt_of(m, d.add)) n += 1;
+        return n;
+    }
+    bool skippable(u64 t, const u32 (&m)[K], int lane_b, const Delta& db) const {
+        const int a = act[t];
+        if (a == 255) return false;
+        const Foot& fa = foot[t];
+        const int fb = family(lane_b);
+        const u32 mb = fb >= 7 ? (selm<K>(m, lane_b - P.off[fb]) & MSG_MASK) : 0u;
+        // (1) order
+        if (!(order_key(lane_b, mb) < order_key(a, fa.m_act))) return false;
+        // (2) independence: server words
+        const int sa = lane_server(a, fa.m_act), sb = lane_server(lane_b, mb);
+        if (sa >= 0 && sb >= 0 && sa == sb) return false;
+        // (2) independence: messages
+        u32 ka[2], kb[2];
+        int na = 0, nb = 0;
+        if (fa.has_act) ka[na++] = fa.m_act;
+        if (fa.has_add) ka[na++] = fa.m_add;
+        if (fb >= 7) kb[nb++] = mb;
+        if (db.has_add) kb[nb++] = db.add;
+        for (int x = 0; x < na; ++x)
+            for (int y = 0; y < nb; ++y)
+                if (ka[x] == kb[y]) return false;
+        // (3) b(s) in the model: |DOMAIN| differs from b(t)'s by a's net domain change
+        int delta_a = 0;
+        if (fa.has_add && cnt_of(m, fa.m_add) == 1) delta_a += 1;   // a created the key
+        if (fa.consumed && cnt_of(m, fa.m_act) == 0) delta_a -= 1;  // a removed its last copy
+        if (dom_after(m, db) - delta_a > P.max_msgs) return false;
+        return true;
+    }
+
+    struct Out { std::vector<u64> level_new; u64 generated = 0, probes = 0, skipped = 0, mismatch = 0; };
+
+    Out bfs(int max_levels, bool skip, u64 cap) {
+        Out o;
+        W.clear(); M.clear(); act.clear(); foot.clear(); hfoot.clear();
+        u64 slots = 1;
+        while (slots < 2 * cap) slots <<= 1;
+        table.assign(slots, 0);
+        mask = slots - 1;
+        u64 w0[S];
+        u32 m0[K];
+        for (int i = 0; i < S; ++i) w0[i] = 1ull | ((u64)NILV << VF_SH);
+        for (int q = 0; q < K; ++q) m0[q] = 0;
+        insert(state_fp<S, K>(w0, m0));
+        W.insert(W.end(), w0, w0 + S);
+        M.insert(M.end(), m0, m0 + K);
+        act.push_back(255);
+        foot.push_back(Foot{});
+        hfoot.push_back(0);
+        o.generated = 1;
+        o.level_new.push_back(1);
+        u64 lo = 0, hi = 1;
+        for (int lv = 1; (max_levels == 0 || lv < max_levels) && lo < hi; ++lv) {
+            for (u64 t = lo; t < hi; ++t) {
+                u64 w[S];
+                u32 m[K];
+                for (int i = 0; i < S; ++i) w[i] = W[t * S + i];
+                for (int q = 0; q < K; ++q) m[q] = M[t * K + q];
+                const u64 h0 = state_fp<S, K>(w, m);
+                for (int lane = 0; lane < nl; ++lane) {
+                    Delta d;
+                    lane_delta<S, K>(w, m, lane, P, d);
+                    if (!d.en) continue;
+                    ++o.generated;
+                    u64 h = 0;
+                    if (!delta_fp<S, K>(w, m, h0, d, P, &h)) continue;
+                    if (h == h0) continue;  // stutter
+                    const bool sk = skippable(t, m, lane, d);
+                    {  // the kernels' implementation (raft_packed.h) must decide the same
+                        Diamond dm;
+                        diamond_of<S, K>(m, act[t], hfoot[t], P, dm);
+                        int nmb = 0;
+                        u64 h2 = 0;
+                        delta_fp<S, K>(w, m, h0, d, P, &h2, &nmb);
+                        if (diamond_skip<S, K>(m, lane, d, nmb, dm, P) != sk) ++o.mismatch;
+                    }
+                    if (sk) {
+                        ++o.skipped;
+                        if (skip) continue;
+                    }
+                    ++o.probes;
+                    if (!insert(h)) continue;
+                    u64 wo[S];
+                    u32 mo[K];
+                    materialise<S, K>(w, m, d, wo, mo);
+                    W.insert(W.end(), wo, wo + S);
+                    M.insert(M.end(), mo, mo + K);
+                    act.push_back((uint8_t)lane);
+                    Foot f{};
+                    const int fam = family(lane);
+                    if (fam >= 7) {
+                        f.has_act = 1;
+                        f.m_act = selm<K>(m, lane - P.off[fam]) & MSG_MASK;
+                        f.consumed = d.rm >= 0;
+                    }
+                    if (d.has_add) { f.has_add = 1; f.m_add = d.add; }
+                    foot.push_back(f);
+                    hfoot.push_back(make_foot<S, K>(m, lane, d, P));
+                }
+            }
+            lo = hi;
+            hi = act.size();
+            if (hi > lo) o.level_new.push_back(hi - lo);
+            if (act.size() > cap) { fprintf(stderr, "capacity\n"); exit(2); }
+        }
+        return o;
+    }
+};
+
+template <int S, int K>
+int run(int V, int mt, int ml, int mm, int md, int levels, u64 cap) {
+    Model<S, K> X;
+    X.P.V = V; X.P.max_term = mt; X.P.max_log = ml; X.P.max_msgs = mm; X.P.max_dup = md; X.P.diamond = 1;
+    for (int f = 0; f <= 10; ++f) X.P.off[f] = Lanes<S, K>::off(f);
+    auto a = X.bfs(levels, false, cap);
+    auto b = X.bfs(levels, true, cap);
+    u64 da = 0, db = 0;
+    for (u64 x : a.level_new) da += x;
+    for (u64 x : b.level_new) db += x;
+    printf("{\"S\": %d, \"V\": %d, \"max_term\": %d, \"max_log\": %d, \"max_msgs\": %d, \"max_dup\": %d, "
+           "\"levels\": %zu, \"distinct\": %llu, \"generated\": %llu, \"probes\": %llu, \"skippable\": %llu, "
+           "\"skippable_frac\": %.4f, \"with_skip\": {\"distinct\": %llu, \"generated\": %llu, \"probes\": %llu, "
+           "\"levels\": %zu}, \"same_levels\": %s, \"kernel_rule_mismatches\": %llu}\n",
+           S, V, mt, ml, mm, md, a.level_new.size(), (unsigned long long)da, (unsigned long long)a.generated,
+           (unsigned long long)a.probes, (unsigned long long)a.skipped, (double)a.skipped / (double)a.probes,
+           (unsigned long long)db, (unsigned long long)b.generated, (unsigned long long)b.probes,
+           b.level_new.size(), a.level_new == b.level_new && a.generated == b.generated ? "true" : "false",
+           (unsigned long long)(a.mismatch + b.mismatch));
+    return a.level_new == b.level_new && a.generated == b.generated && !a.mismatch && !b.mismatch ? 0 : 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 8) {
+        fprintf(stderr, "usage: %s S V MaxTerm MaxLogLen MaxMsgs MaxDup max_levels [capacity]\n", argv[0]);
+        return 2;
+    }
+    const int S = atoi(argv[1]), V = atoi(argv[2]), mt = atoi(argv[3]), ml = atoi(argv[4]), mm = atoi(argv[5]),
+              md = atoi(argv[6]), lv = atoi(argv[7]);
+    const u64 cap = argc > 8 ? strtoull(argv[8], nullptr, 10) : (1ull << 26);
+    const bool k8 = mm > 4;
+    if (S == 2) return k8 ? run<2, 8>(V, mt, ml, mm, md, lv, cap) : run<2, 4>(V, mt, ml, mm, md, lv, cap);
+    if (S == 3) return k8 ? run<3, 8>(V, mt, ml, mm, md, lv, cap) : run<3, 4>(V, mt, ml, mm, md, lv, cap);
+    if (S == 4) return k8 ? run<4, 8>(V, mt, ml, mm, md, lv, cap) : run<4, 4>(V, mt, ml, mm, md, lv, cap);
+    return k8 ? run<5, 8>(V, mt, ml, mm, md, lv, cap) : run<5, 4>(V, mt, ml, mm, md, lv, cap);
+}
