@@ -674,6 +674,8 @@ RMC_HD void materialise(const u64 (&w)[S], const u32 (&m)[K], const Delta& d, u6
 // on whole BFS runs).  Not under SYMMETRY (canonical representatives break
 // the instance order).
 constexpr u64 FOOT_VALID = 1ull << 63, FOOT_ACT = 1ull << 62, FOOT_ADD = 1ull << 61, FOOT_CONSUMED = 1ull << 60;
+// sharded verification records only: the owner had seen this key (compare, do not store)
+constexpr u64 FOOT_SEEN = 1ull << 59;
 
 // Family of a lane from the runtime offsets (wave-uniform lanes: scalar compares).
 RMC_HD int lane_family(const Params& P, int lane) {

@@ -198,7 +198,9 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     D.keys_sent = D.states_sent = D.chunks = D.parked = 0;
     D.xfer_seconds = D.wait_seconds = 0;
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
-    HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
+    if (c->B.sent) HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
+    const bool verify = c->sh.verify;
+    if (verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
     if (int rc = reset_counters(c, false)) return rc;
     // ---- Init (raft.tla:125-129): stored by its owner only
@@ -221,6 +223,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         for (int r = 0; r < W; ++r) {
             const Counters& k = rows[(size_t)r];
             if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full on rank " + std::to_string(r));
+            if (k.overflow & 4u) return fail(c, RMC_E_CAPACITY, "verification buffer full on rank " + std::to_string(r));
+            if (k.overflow & 8u)
+                return fail(c, RMC_E_HIP, "verification: a fingerprint without a published state on rank " +
+                                              std::to_string(r));
             if (k.overflow & 2u)
                 return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(r) +
                                                    " (raise keys_per_dest)");
@@ -233,6 +239,8 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (int rc = level_end()) return rc;
     c->level_start.push_back(0);
     c->level_start.push_back(c->h_ctr->count);
+    if (verify && c->h_ctr->count)  // slot -> store index of the initial state(s)
+        HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
     u64 total_prev = 0;
     for (const auto& k : rows) total_prev += k.count;
     for (int r = 0; r < W && !c->have_target; ++r)  // Init's violation check (level 1)
@@ -257,6 +265,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     // received from other ranks are appended after the local ones).  A round
     // aims at an outbox half full; what does not fit is parked, not lost.
     double rho = 1.0;
+    u64 vpub = c->h_ctr->count;  // verification: states [0, vpub) are published (slot -> index)
     const u64 row_len = 4 * (u64)W + 1;  // cx: [2W] sent pairs, [1] novf, [2W] received pairs
     while (!c->have_target) {
         const u64 lo = c->level_start[(size_t)depth - 1], hi = c->level_start[(size_t)depth];
@@ -304,6 +313,17 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 cursor += n;
                 round_states[k & 1] = n;
                 round_kind[k & 1] = 1;
+            }
+            if (verify) {  // publish this round's local states, then check the hits deferred to them
+                if (int rc = read_counters(c)) return rc;
+                const u64 c1 = c->h_ctr->count;
+                if (c1 > vpub)
+                    HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, vpub, c1, nullptr, nullptr, 0, nullptr, c->st));
+                vpub = c1;
+                if (c->h_ctr->vcount) {
+                    HIPCHK(c, launch(c->sh, 6, c->P, c->PT, c->B, c->h_ctr->vcount, 0, nullptr, nullptr, 0, nullptr, c->st));
+                    HIPCHK(c, hipMemsetAsync(&c->B.ctr->vcount, 0, 8, c->st));
+                }
             }
             HIPCHK(c, hipEventRecord(S.ev_exp, c->st));
             return 0;
@@ -412,7 +432,8 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             // ---- phase 2: the accepted states
             u64 tot_st = 0;
             for (int p = 0; p < W; ++p) {
-                const u64 ns = D.h_sa[p], nr = D.h_sa[W + p];
+                // verification ships every key's state (the seen ones to be compared)
+                const u64 ns = D.h_sa[p], nr = verify ? cx[2 * W + 1 + 2 * p] : D.h_sa[W + p];
                 if (p != me && ns > kcap) return fail(c, RMC_E_HIP, "phase 2: more accepted states than keys sent");
                 soff[(size_t)p] = (u64)p * kcap * RB;
                 scnt[(size_t)p] = p == me ? 0 : ns * RB;
@@ -425,6 +446,16 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             if (int rc = a2a(c, c->B.st_out, soff.data(), scnt.data(), D.st_in, roff.data(), rcnt.data())) return rc;
             if (tot_st)
                 HIPCHK(c, launch(c->sh, 9, c->P, c->PT, c->B, tot_st, 0, D.st_in, nullptr, 0, nullptr, D.xs));
+            if (verify && tot_st) {  // publish the received new states, then compare the seen ones
+                HIPCHK(c, hipStreamSynchronize(D.xs));
+                if (int rc = read_counters(c)) return rc;
+                const u64 c2 = c->h_ctr->count;
+                if (c2 > vpub)
+                    HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, vpub, c2, nullptr, nullptr, 0, nullptr, D.xs));
+                vpub = c2;
+                HIPCHK(c, launch(c->sh, 11, c->P, c->PT, c->B, tot_st, 0, D.st_in, nullptr, 0, nullptr, D.xs));
+                HIPCHK(c, hipStreamSynchronize(D.xs));
+            }
             HIPCHK(c, hipEventRecord(S.x1, D.xs));
             S.xtimed = 1;
             D.chunks += 1;
@@ -440,7 +471,11 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 S2.xtimed = 0;
             }
         u64 tot = 0, gen = 0, pr = 0;
-        for (const auto& r : rows) { tot += r.count; gen += r.generated; pr += r.probes; }
+        for (const auto& r : rows) {
+            tot += r.count; gen += r.generated; pr += r.probes;
+            c->res.collisions += r.collisions;
+            c->res.verified += r.vchecked;
+        }
         const u64 nnew = tot - total_prev;
         total_prev = tot;
         generated += gen;
@@ -563,7 +598,6 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     if (!c || world < 1 || world > kMaxWorld || rank < 0 || rank >= world) return RMC_E_INVAL;
     if (!rccl_id && !(host && host->alltoallv && host->allgather))
         return fail(c, RMC_E_INVAL, "rmc_shard needs an RCCL id or a host transport");
-    if (c->sh.verify) return fail(c, RMC_E_INVAL, "sharded mode does not support full-state verification");
     if (c->spill.on) return fail(c, RMC_E_INVAL, "sharded mode does not support RMC_FLAG_SPILL");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     free_dist(c);
@@ -582,7 +616,8 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     D.sent_slots = slots;
     D.in_cap = W * kcap;
     bool ok = hipStreamCreateWithFlags(&D.xs, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
+    // full-state verification ships every remote successor: no sent-cache
+    if (!c->sh.verify) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
     const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
     ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
     for (auto& S : D.set) {
@@ -608,6 +643,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     D.debug = getenv("RMC_DIST_DEBUG") != nullptr;
     if (const char* s = getenv("RMC_DIST_SPLIT")) D.split = std::max(1, std::min(64, atoi(s)));
     if (const char* s = getenv("RMC_DIST_OVERLAP")) D.overlap = atoi(s) != 0;
+    if (c->sh.verify) D.overlap = 0;  // rounds in order: each publishes its states before the next compares
     if (const char* s = getenv("RMC_DIST_FILL")) D.fill = std::max(0.01, std::min(64.0, atof(s)));
     c->B.smask = slots - 1;
     c->B.kcap = kcap;

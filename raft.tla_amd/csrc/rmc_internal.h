@@ -83,6 +83,7 @@ struct Shape {
 //        5 = k_publish over store[a, b) (verification: slot -> store index);
 //        6 = k_verify of `a` deferred hits in B.vbuf;
 //        7 = k_rehash of the stored states [a, b) (recovery).
+//       11 = k_compare_remote of `a` received state records `in` (sharded verification).
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 

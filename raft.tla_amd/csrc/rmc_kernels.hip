@@ -735,7 +735,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 key[b] = s_key[b][threadIdx.x];
                 if constexpr (DIST) {
                     const bool remote = key[b] && s_own[b][threadIdx.x] != B.rank;
-                    cur[b] = !key[b] ? 0ull : remote ? B.sent[(key[b] >> 8) & B.smask] : B.table[key[b] & B.tmask];
+                    // no sent-cache in verification mode (B.sent null): every remote successor is shipped
+                    cur[b] = !key[b] ? 0ull
+                           : remote ? (B.sent ? B.sent[(key[b] >> 8) & B.smask] : 0ull)
+                                    : B.table[key[b] & B.tmask];
                 } else {
                     cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
                 }
@@ -757,7 +760,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 }
                 if constexpr (DIST) {
                     if (s_own[b][threadIdx.x] != B.rank) {  // not sent before (lossy cache): ship it
-                        B.sent[(key[b] >> 8) & B.smask] = key[b];
+                        if (B.sent) B.sent[(key[b] >> 8) & B.smask] = key[b];
                         newbits |= 1u << b;
                         continue;
                     }
@@ -974,6 +977,8 @@ __global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
 // (reply[d * kcap + i] = 1), re-derive the successor from its ticket and put
 // the record {state, global parent ref | lane << 40} into owner d's state
 // outbox.  Grid over (destination, key index).
+// Full-state verification (B.sidx set): every key is shipped, the ones the
+// owner had seen flagged FOOT_SEEN, so the owner compares them with its state.
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, const DevBufs B, const uint8_t* reply,
                                                             u64 per_dest, u64 i0) {
@@ -983,7 +988,9 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
         const u32 d = (u32)(t / per_dest);
         const u64 i = i0 + (t - (u64)d * per_dest);
         const u64 sent = B.ocount[d] < B.kcap ? B.ocount[d] : B.kcap;  // beyond kcap: parked, not sent
-        if (d == B.rank || i >= sent || !reply[(u64)d * B.kcap + i]) continue;
+        if (d == B.rank || i >= sent) continue;
+        const bool seen = !reply[(u64)d * B.kcap + i];
+        if (seen && !B.sidx) continue;
         const u64 tick = B.tick_out[(u64)d * B.kcap + i];
         const u64 pidx = tick & ((1ull << 56) - 1);
         const int lane = (int)(tick >> 56);
@@ -1005,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
         const u64 ref = B.ref_tag | ((u64)lane << 40) | pidx;
         r[NW] = (u32)ref;
         r[NW + 1] = (u32)(ref >> 32);
-        const u64 ft = make_foot<S, K>(m, lane, dl, P);
+        const u64 ft = make_foot<S, K>(m, lane, dl, P) | (seen ? FOOT_SEEN : 0ull);
         r[NW + 2] = (u32)ft;
         r[NW + 3] = (u32)(ft >> 32);
     }
@@ -1021,7 +1028,8 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
     const u64 lt = (1ull << me) - 1ull;
     for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
         const u64 t = t0 + threadIdx.x;
-        const bool live = t < n;
+        // verification mode also receives the states the owner had seen (compared by k_compare_remote)
+        const bool live = t < n && !(inbox[t * (u64)RW + NW + 3] & (u32)(FOOT_SEEN >> 32));
         const u64 bal = __ballot(live);
         if (!bal) continue;
         const int leader = __ffsll((long long)bal) - 1;
@@ -1046,6 +1054,40 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
         const int v = check_invariants<S, K>(w, m, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
+}
+
+// Sharded full-state verification, owner side: every received record the
+// owner had already seen (FOOT_SEEN) is compared with the stored state that
+// owns its fingerprint's slot (published by k_publish before this runs); a
+// difference is a fingerprint collision.
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_compare_remote(const Params P, const PermTable PT, const DevBufs B,
+                                                        const u32* inbox, u64 n) {
+    constexpr int NW = 2 * S + K, RW = NW + 4;
+    u64 vchk = 0, vcol = 0;
+    for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n; t += (u64)gridDim.x * 256ull) {
+        const u32* r = inbox + t * (u64)RW;
+        if (!(r[NW + 3] & (u32)(FOOT_SEEN >> 32))) continue;
+        PackedState<S, K> o;
+        load_state<S, K>(r, o.w, o.m);
+        const u64 key = verify_key<S, K, SYM>(o.w, o.m, P, PT);
+        u64 s = key & B.tmask, k = 0;
+        while (B.table[s] != key && k <= B.tmask) { s = (s + 1) & B.tmask; ++k; }
+        const u64 ix = k > B.tmask ? ~0ull : B.sidx[s];
+        if (ix == ~0ull) {
+            atomicOr(&B.ctr->overflow, 8u);  // a seen key without a published owner
+            continue;
+        }
+        ++vchk;
+        bool same;
+        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)NW, PT);
+        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW);
+        vcol += same ? 0u : 1u;
+    }
+    vchk = wave_sum64(vchk);
+    vcol = wave_sum64(vcol);
+    if (__lane_id() == 0 && vchk) atomicAdd((unsigned long long*)&B.ctr->vchecked, (unsigned long long)vchk);
+    if (__lane_id() == 0 && vcol) atomicAdd((unsigned long long*)&B.ctr->collisions, (unsigned long long)vcol);
 }
 
 // SYMMETRY, single GPU: the successors k_expand_sym deferred because their
@@ -1425,6 +1467,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3((unsigned)g), dim3(256), 0, st,
                                P, PT, B, a, b);
         }
+    } else if (which == 3 && verify) {  // sharded full-state verification: every lane, hits compared
+        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                           b);
+    } else if (which == 11) {
+        hipLaunchKernelGGL((k_compare_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
     } else if (which == 3) {
         if constexpr (SYM)
             hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--capacity", type=int, default=0)
     ap.add_argument("--rerun", type=int, default=1)
     ap.add_argument("--sent-cache", type=int, default=1 << 22, help="sent-cache slots per rank")
+    ap.add_argument("--verify", action="store_true", help="full-state verification (RMC_FLAG_VERIFY_STATES)")
+    ap.add_argument("--fp-bits", type=int, default=64, help="verification test hook: fingerprint bits kept")
     args = ap.parse_args()
     dev = args.device if args.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "nccl":
@@ -48,14 +50,19 @@ def main():
                               max_dup=p["max_dup"], bug_quorum=bool(p["bug_quorum"]),
                               invariants=p["invariants"], device=dev, symmetry=bool(p["symmetry"]),
                               max_depth=p["max_depth"],
-                              state_capacity=args.capacity or max(1 << 20, g["distinct"]))
+                              state_capacity=args.capacity or max(1 << 20, g["distinct"]),
+                              verify_states=args.verify)
     else:
         cfg = rmc.config_from_files(args.cfg, builtin_raft=True)
         cfg.device = dev
         cfg.state_capacity = args.capacity or (1 << 26)
+        if args.verify:
+            cfg.flags |= rmc.FLAG_VERIFY_STATES
     with rmc.Checker(cfg) as ck:
         info = rdist.shard(ck, transport=args.transport, keys_per_dest=args.keys_per_dest,
                            sent_cache_slots=args.sent_cache)
+        if args.fp_bits < 64:
+            ck.set_fp_bits(args.fp_bits)
         t0 = time.time()
         r = ck.run()  # collective: the global result on every rank
         wall = time.time() - t0
@@ -67,7 +74,8 @@ def main():
             dist.all_gather_object(allt, mine)
             assert all(t == mine for t in allt), "ranks disagree on the trace"
         reruns = [ck.run() for _ in range(args.rerun)]
-        fields = ("distinct", "generated", "depth", "left_on_queue", "violated_inv", "violation_depth")
+        fields = ("distinct", "generated", "depth", "left_on_queue", "violated_inv", "violation_depth",
+                  "collisions", "verified")
         summary = {k: getattr(r, k) for k in fields}
         per_rank = [None] * world
         dist.all_gather_object(per_rank, dict(rank=rank, stored=r.stored_here, keys_sent=r.keys_sent,

@@ -164,3 +164,44 @@ def test_sharded_outbox_overflow_is_recovered(case, nproc, overlap, tmp_path):
     assert res["levels"] == g["level_new"]
     assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
     assert res["parked"] > 0  # the outboxes did overflow
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,nproc", [("small", 2), ("small", 4), ("small_sym", 3)])
+def test_sharded_verification(case, nproc, tmp_path):
+    """Full-state verification on a sharded search: every
+    fingerprint hit, local or at the owner of a remote successor, is compared
+    state by state.  Full fingerprints: 0 collisions and the oracle's counts.
+    Fingerprints cut to 16 bits: the collisions are found and reported."""
+    g = GOLDEN[case]
+    out = tmp_path / "r.json"
+    base = [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--device", "0", "--backend", "gloo",
+            "--verify", "--rerun", "0"]
+    r = _torchrun(nproc, base + ["--out", str(out)], 29700 + nproc)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert (res["distinct"], res["generated"], res["depth"]) == (g["distinct"], g["generated"], g["depth"])
+    assert res["collisions"] == 0 and res["verified"] > 0
+    assert sum(p["stored"] for p in res["per_rank"]) == g["distinct"]
+    out16 = tmp_path / "r16.json"
+    r = _torchrun(nproc, base + ["--out", str(out16), "--fp-bits", "16"], 29710 + nproc)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res16 = json.load(open(out16))
+    assert res16["collisions"] > 0 and res16["verified"] > 0
+    assert res16["distinct"] < g["distinct"]  # the colliding states were (reported as) dropped
+
+
+@pytest.mark.gpu
+def test_sharded_verification_full_bench_model(tmp_path):
+    """The 1.23 G-state bench model verified state by state on 2 ranks: the
+    single-GPU counts and 0 collisions (SURVEY.md §8d config 3's "full-state
+    verification runs at least once", sharded)."""
+    out = tmp_path / "r.json"
+    r = _torchrun(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--cfg",
+                      os.path.join(ROOT, "specs", "MCraftBench.cfg"), "--out", str(out), "--device", "0",
+                      "--backend", "gloo", "--capacity", "800000000", "--keys-per-dest", str(1 << 24),
+                      "--rerun", "0", "--verify"], 29720, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert (res["distinct"], res["generated"], res["depth"]) == (1_227_465_177, 21_130_972_267, 56)
+    assert res["collisions"] == 0 and res["verified"] > 1_000_000_000
