@@ -508,6 +508,50 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
     return 1;
 }
 
+// delta_fp_pre split in two, so a lane can decide to skip its probe before it
+// hashes: the CONSTRAINT and |DOMAIN messages| of the successor ...
+template <int S, int K>
+RMC_HD int delta_bounds_pre(const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d, const Params& P,
+                            int* nmsg_out) {
+    int nmsg = pm.nmsg;
+    if (d.srv >= 0) {
+        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
+        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
+    }
+    if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
+    if (d.has_add) {
+        u32 cnt = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) cnt |= (m[q] && (m[q] & MSG_MASK) == d.add) ? m_cnt(m[q]) : 0u;
+        if ((int)cnt + 1 > P.max_dup) return 0;
+        nmsg += cnt ? 0 : 1;
+    }
+    *nmsg_out = nmsg;
+    return nmsg <= P.max_msgs;
+}
+// ... and the fingerprint of a successor known to be in the model (same value as delta_fp_pre).
+template <int S, int K>
+RMC_HD u64 delta_hash_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d) {
+    u64 hh = pm.h0;
+    if (d.srv >= 0) {
+        const u64 wo = selw<S>(w, d.srv);
+        if (d.w_new != wo) hh += hS(d.w_new, (u32)d.srv) - sel64<S>(pm.hw, d.srv);
+    }
+    if (d.rm >= 0) {
+        const u32 sl = selm<K>(m, d.rm);
+        hh -= sel64<K>(pm.hm, d.rm);
+        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
+    }
+    if (d.has_add) {
+        int found = -1;
+#pragma unroll
+        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+        if (found >= 0) hh += hM(selm<K>(m, found) + CNT_ONE) - sel64<K>(pm.hm, found);
+        else hh += hM(d.add | CNT_ONE);
+    }
+    return hh;
+}
+
 // ---- wave homogeneity (the single-GPU expansion kernel) ------------------------------
 // A wave walks every action lane that ANY of its 64 states enables, so states
 // of one kind (same roles, same number of messages) should sit together.

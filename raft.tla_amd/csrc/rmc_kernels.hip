@@ -528,9 +528,12 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // DIA: commuting-diamond successors are not probed (raft_packed.h "commuting
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false>
+          bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!DIA || (!SYM && !VERIFY), "diamond skipping: not under SYMMETRY or verification");
+    // EARLY: the stutter / CONSTRAINT / diamond decisions come before the hash,
+    // so a lane that does not probe never hashes (needs the parent's mixes)
+    static_assert(!EARLY || (DIA && PRE), "EARLY needs DIA and PRE");
     constexpr int NW = 2 * S + K;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
     // SORT: class-sorted flushes + the wave walks only lane_superset's lanes
@@ -699,10 +702,17 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         }
                     } else if (en) {
                         int nmb = 0;
-                        if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr);
-                        else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
-                        if constexpr (DIA)
-                            if (in_model && h != h0 && diamond_skip<S, K>(m, lane, d, nmb, dm, P)) in_model = 0;
+                        if constexpr (EARLY) {
+                            const bool stutter = d.rm < 0 && !d.has_add && (d.srv < 0 || d.w_new == selw<S>(w, d.srv));
+                            in_model = !stutter && delta_bounds_pre<S, K>(m, pmx, d, P, &nmb) &&
+                                       !diamond_skip<S, K>(m, lane, d, nmb, dm, P);
+                            h = in_model ? delta_hash_pre<S, K>(w, m, pmx, d) : h0;
+                        } else {
+                            if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr);
+                            else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
+                            if constexpr (DIA)
+                                if (in_model && h != h0 && diamond_skip<S, K>(m, lane, d, nmb, dm, P)) in_model = 0;
+                        }
                         if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
                     }
                     if (in_model && (SYM || h != h0)) {
@@ -878,11 +888,11 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
-template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true>
+template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -901,15 +911,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K
 
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
 // WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
+// 4 waves/SIMD like k_expand_sort (uncapped it takes 131 VGPRs: 3 waves).
 template <int S, int K, int BATCH, bool WS>
-__global__ __launch_bounds__(256) void k_expand_dist(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 4 : 1))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, false, false, true, true, false, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, true, true>(P, PT, B, lo, hi);
     else
         expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
 
+#ifndef RMC_SHAPE_S  // non-template kernels: in the common object only
 // Sharded mode, phase 1, owner side: insert the keys other ranks sent;
 // reply[t] = 1 if key t was new here (its sender then ships the state), and
 // acc[p] counts the new keys of source p — the states p will send in phase 2,
@@ -972,6 +984,8 @@ __global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
         B.tick_out[(u64)dest * B.kcap + slot] = (tk & ((1ull << 48) - 1)) | (tk & (0xFFull << 56));
     }
 }
+
+#endif  // !RMC_SHAPE_S
 
 // Sharded mode, phase 2, sender side: for every key an owner accepted
 // (reply[d * kcap + i] = 1), re-derive the successor from its ticket and put
@@ -1154,6 +1168,7 @@ __global__ __launch_bounds__(256) void k_probe_bench(u64* table, u64 mask, u32 i
     if (acc == 0x5A5A5A5A5A5A5A5Aull) sink[0] = acc;  // keeps the loads live
 }
 
+#ifndef RMC_SHAPE_S
 hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, const SrcOff& so,
                                unsigned long long* acc, hipStream_t st) {
     if (n == 0) return hipSuccess;
@@ -1181,6 +1196,8 @@ hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int 
                        iters, mode, sink);
     return hipGetLastError();
 }
+
+#endif  // !RMC_SHAPE_S
 
 // Insert n staged initial states (packed) into the set and the store.
 template <int S, int K, bool SYM>
@@ -1359,23 +1376,7 @@ static hipError_t launch_sim_t(const Params& P, const u32* inits, u64 n_init, u6
     return hipGetLastError();
 }
 
-hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
-                      int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
-#define RMC_SCASE(SS, KK) \
-    if (sh.S == SS && sh.K == KK)   \
-        return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, st);
-    RMC_SCASE(2, 4) RMC_SCASE(2, 8) RMC_SCASE(3, 4) RMC_SCASE(3, 8) RMC_SCASE(4, 4) RMC_SCASE(4, 8) RMC_SCASE(5, 4)
-    RMC_SCASE(5, 8)
-#undef RMC_SCASE
-    return hipErrorInvalidValue;
-}
-
 // ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
-hipError_t set_fp_salt(u64 seed, hipStream_t st) {
-    const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
-    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &salt, sizeof salt, 0, hipMemcpyHostToDevice, st);
-}
-
 // Blocks of the grid-stride kernels (RMC_EXPAND_GRID for A/B runs; default 2048).
 static u64 expand_grid() {
     static u64 v = [] {
@@ -1387,7 +1388,9 @@ static u64 expand_grid() {
 }
 
 // Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
-// profiles/r02/ab/): 6 (default) = the lane-superset walk over class-sorted
+// profiles/r02/ab/, profiles/r03/): 7 (default) = 6 with the stutter,
+// CONSTRAINT and commuting-diamond decisions taken before the lane hashes;
+// 6 = the lane-superset walk over class-sorted
 // windows of up to 2048 states (k_expand_sort, 4 waves/SIMD; 317 vs 343 ms per
 // MCraftBench BFS against 1; shapes with > 64 lanes run 1), 1 = every lane of
 // every state, the parent's per-component mixes precomputed (k_expand, 95
@@ -1398,7 +1401,7 @@ static u64 expand_grid() {
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 6;
+        return e ? atoi(e) : 7;
     }();
     return v;
 }
@@ -1460,6 +1463,9 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                B, a, b);
         } else if (expand_variant() == 4 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 0>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+        } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+                               PT, B, a, b);
         } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
@@ -1512,15 +1518,68 @@ static hipError_t launch_sk(bool sym, bool verify, int which, const Params& P, c
     return launch_t<S, K, false>(which, verify, P, PT, B, a, b, in, out, cap, count, st);
 }
 
+// ---- objects: one per shape (RMC_SHAPE_S / RMC_SHAPE_K, the template
+// instantiations, built in parallel) + the common object (dispatch, the
+// shape-free kernels).  The fingerprint salt is a __constant__ of each object.
+#define RMC_SHAPES(X) X(2, 4) X(2, 8) X(3, 4) X(3, 8) X(4, 4) X(4, 8) X(5, 4) X(5, 8)
+#define RMC_SHAPE_DECLS(SS, KK)                                                                                 \
+    hipError_t launch_shape_##SS##_##KK(const Shape& sh, int which, const Params& P, const PermTable& PT,       \
+                                        const DevBufs& B, u64 a, u64 b, const u32* in, u32* out, u64 cap,       \
+                                        unsigned long long* count, hipStream_t st);                             \
+    hipError_t launch_sim_shape_##SS##_##KK(const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, \
+                                            u64 seed, int mode, SimCounters* out, i64 rec_beh, u32* rec,        \
+                                            hipStream_t st);                                                    \
+    hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, hipStream_t st);
+RMC_SHAPES(RMC_SHAPE_DECLS)
+
+#ifdef RMC_SHAPE_S
+#define RMC_DEFINE_SHAPE(SS, KK)                                                                                \
+    hipError_t launch_shape_##SS##_##KK(const Shape& sh, int which, const Params& P, const PermTable& PT,       \
+                                        const DevBufs& B, u64 a, u64 b, const u32* in, u32* out, u64 cap,       \
+                                        unsigned long long* count, hipStream_t st) {                            \
+        return launch_sk<SS, KK>(sh.sym, sh.verify, which, P, PT, B, a, b, in, out, cap, count, st);           \
+    }                                                                                                           \
+    hipError_t launch_sim_shape_##SS##_##KK(const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, \
+                                            u64 seed, int mode, SimCounters* out, i64 rec_beh, u32* rec,        \
+                                            hipStream_t st) {                                                   \
+        return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, st);        \
+    }                                                                                                           \
+    hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, hipStream_t st) {                                        \
+        static u64 h_salt;                                                                                      \
+        h_salt = salt;                                                                                          \
+        return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &h_salt, sizeof h_salt, 0, hipMemcpyHostToDevice, st); \
+    }
+#define RMC_DEFINE_SHAPE_(SS, KK) RMC_DEFINE_SHAPE(SS, KK)
+RMC_DEFINE_SHAPE_(RMC_SHAPE_S, RMC_SHAPE_K)
+#else
+hipError_t set_fp_salt(u64 seed, hipStream_t st) {
+    const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
+    hipError_t e = hipSuccess;
+#define RMC_SET_SALT(SS, KK) \
+    if ((e = set_fp_salt_shape_##SS##_##KK(salt, st)) != hipSuccess) return e;
+    RMC_SHAPES(RMC_SET_SALT)
+#undef RMC_SET_SALT
+    return hipStreamSynchronize(st);  // the staged host copies are static per object
+}
+
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-#define RMC_CASE(SS, KK)                                                                                      \
-    if (sh.S == SS && sh.K == KK)                                                                             \
-        return launch_sk<SS, KK>(sh.sym, sh.verify, which, P, PT, B, a, b, in, out, cap, count, st);
-    RMC_CASE(2, 4) RMC_CASE(2, 8) RMC_CASE(3, 4) RMC_CASE(3, 8) RMC_CASE(4, 4) RMC_CASE(4, 8) RMC_CASE(5, 4)
-    RMC_CASE(5, 8)
+#define RMC_CASE(SS, KK) \
+    if (sh.S == SS && sh.K == KK) return launch_shape_##SS##_##KK(sh, which, P, PT, B, a, b, in, out, cap, count, st);
+    RMC_SHAPES(RMC_CASE)
 #undef RMC_CASE
     return hipErrorInvalidValue;
 }
+
+hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
+                      int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st) {
+#define RMC_SCASE(SS, KK) \
+    if (sh.S == SS && sh.K == KK)   \
+        return launch_sim_shape_##SS##_##KK(P, inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, st);
+    RMC_SHAPES(RMC_SCASE)
+#undef RMC_SCASE
+    return hipErrorInvalidValue;
+}
+#endif  // RMC_SHAPE_S
 
 }  // namespace rmc

@@ -66,7 +66,7 @@ def main():
     json.dump(rec, open(os.path.join(out, f"pmc_traffic_{stem}.json"), "w"), indent=1)
     print(json.dumps(rec, indent=1))
     extra = {}
-    for pas in ("insts", "stall", "tcc"):
+    for pas in ("insts", "stall", "tcc", "lds"):
         d = os.path.join(src, pas)
         if not os.path.isdir(d):
             continue
