@@ -62,6 +62,18 @@ extern "C" {
                                            /* sizes the fingerprint set (all states),   */
                                            /* device_window the resident states.  Single */
                                            /* GPU; not with RMC_FLAG_VERIFY_STATES       */
+/* A model without a CONSTRAINT on some field (MCraft.cfg as shipped) runs only
+ * under a depth bound (max_depth > 0, TLC -depth).  The front-end then gives
+ * each unbounded field the packed capacity (RMC_MAX_TERM, RMC_MAX_LOG,
+ * RMC_MAX_MSGS, RMC_MAX_DUP) and sets its bit here; the search stops with
+ * RMC_E_CAPACITY, naming the field, the first time a successor needs more
+ * than the capacity (it is never silently filtered as out of the model). */
+#define RMC_FLAG_UNBOUNDED_TERM (1u << 5)  /* no CONSTRAINT on currentTerm[i]            */
+#define RMC_FLAG_UNBOUNDED_LOG (1u << 6)   /* no CONSTRAINT on Len(log[i])               */
+#define RMC_FLAG_UNBOUNDED_MSGS (1u << 7)  /* no CONSTRAINT on Cardinality(DOMAIN messages) */
+#define RMC_FLAG_UNBOUNDED_DUP (1u << 8)   /* no CONSTRAINT on messages[m]               */
+#define RMC_UNBOUNDED_ANY (RMC_FLAG_UNBOUNDED_TERM | RMC_FLAG_UNBOUNDED_LOG | RMC_FLAG_UNBOUNDED_MSGS | \
+                           RMC_FLAG_UNBOUNDED_DUP)
 
 /* rmc_config.invariants — the INVARIANT names the engine knows (fused checks). */
 #define RMC_INV_TYPEOK (1u << 0)           /* raft.tla:482-492                          */
@@ -362,10 +374,17 @@ int rmc_probe_bench(int device, uint64_t table_bytes, uint64_t accesses, int mod
  *    be Smokeraft's sampler (k and SmokeNat are read as its parameters); a
  *    CONSTRAINT that only reads TLCGet/TLCSet is a run budget, replaced by
  *    sim->behaviours; bounds the cfg does not give are the packed capacity.
+ *  - an unconstrained field is refused unless options has
+ *    RMC_FRONT_DEPTH_BOUNDED (see RMC_FLAG_UNBOUNDED_TERM).
  * On success `info` receives the provenance notes (which raft.tla was
  * verified, which overrides were recognised), on failure the error. */
 #define RMC_FRONT_BUILTIN_RAFT (1u << 0)
 #define RMC_FRONT_SIMULATE (1u << 1)
+/* RMC_FRONT_DEPTH_BOUNDED: the caller bounds the depth (TLC -depth), so a model
+ * whose CONSTRAINT leaves fields unbounded — or that has none, as MCraft.cfg
+ * as shipped (MCraft.cfg:1-39) — is accepted with the RMC_FLAG_UNBOUNDED_*
+ * bits set (rmc_create then requires max_depth > 0). */
+#define RMC_FRONT_DEPTH_BOUNDED (1u << 2)
 int rmc_model_from_files(const char* cfg_path, const char* tla_path, const char* raft_path,
                          uint32_t options, rmc_config* cfg, rmc_sim_config* sim,
                          char* info, size_t info_cap);

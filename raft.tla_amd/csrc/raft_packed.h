@@ -119,6 +119,8 @@ struct Params {
     int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;
     int off[11];  // family lane offsets (= Lanes<S,K>::off, for host code)
     int diamond;  // 1: commuting-diamond successors are not probed (RMC_DIAMOND=0 turns it off)
+    int unbounded;  // fields no CONSTRAINT bounds (1 term, 2 log, 4 msgs, 8 dup): their bound is the packed
+                    // capacity, and a successor beyond it is an error (capacity_exceeded), not filtered
     u64 fp_mask;  // full-state verification mode: fingerprint bits kept (~0 = all; fewer only
                   // to provoke collisions in tests, rmc_set_fp_bits)
 };
@@ -649,6 +651,31 @@ RMC_HD int delta_in_model(const u32 (&m)[K], const Delta& d, const Params& P) {
         }
     }
     return nmsg <= P.max_msgs;
+}
+
+// The unbounded fields (Params.unbounded) a delta takes past the packed
+// capacity: 0 = none (the successor is in the model or filtered by a real
+// CONSTRAINT), else the field bits.
+template <int S, int K>
+RMC_HD int capacity_exceeded(const u32 (&m)[K], const Delta& d, const Params& P) {
+    int bad = 0;
+    if (d.srv >= 0) {  // from an in-model parent (term <= 14) bit 63 only marks a 4th log entry
+        if ((P.unbounded & 1) && (d.w_new >> 63) == 0 && (int)w_ct(d.w_new) > P.max_term) bad |= 1;
+        if ((P.unbounded & 2) && ((d.w_new >> 63) != 0 || (int)w_len(d.w_new) > P.max_log)) bad |= 2;
+    }
+    int nmsg = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
+    if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
+    if (d.has_add) {
+        u32 cnt = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) cnt |= (m[q] && (m[q] & MSG_MASK) == d.add) ? m_cnt(m[q]) : 0u;
+        if ((P.unbounded & 8) && (int)cnt + 1 > P.max_dup) bad |= 8;
+        nmsg += cnt ? 0 : 1;
+    }
+    if ((P.unbounded & 4) && nmsg > P.max_msgs) bad |= 4;
+    return bad;
 }
 
 template <int S, int K>

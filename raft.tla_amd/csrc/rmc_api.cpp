@@ -46,7 +46,9 @@ int validate(const rmc_config* c, std::string* why) {
     if (c->invariants & ~1023u) return bad("unknown invariant bit");
     if ((c->flags & RMC_FLAG_SPILL) && (c->flags & RMC_FLAG_VERIFY_STATES))
         return bad("RMC_FLAG_SPILL does not combine with RMC_FLAG_VERIFY_STATES");
-    if (c->flags & ~31u) return bad("unknown flag bit");
+    if (c->flags & ~511u) return bad("unknown flag bit");
+    if ((c->flags & RMC_UNBOUNDED_ANY) && c->max_depth <= 0)
+        return bad("a model with unbounded fields (RMC_FLAG_UNBOUNDED_*) needs max_depth > 0 (TLC -depth)");
     return 0;
 }
 
@@ -67,6 +69,7 @@ void fill_params(rmc_ctx* c) {
     P.inv_mask = (int)g.invariants;
     P.symmetry = c->sh.sym ? 1 : 0;
     P.fp_mask = ~0ull;
+    P.unbounded = (int)((g.flags >> 5) & 15u);  // RMC_FLAG_UNBOUNDED_TERM .. _DUP
     {  // commuting-diamond probe elimination (not under SYMMETRY; RMC_DIAMOND=0 turns it off)
         const char* e = getenv("RMC_DIAMOND");
         P.diamond = (!c->sh.sym && !(e && e[0] == '0')) ? 1 : 0;
@@ -272,6 +275,19 @@ int reset_counters(rmc_ctx* c, bool keep_count) {
     *c->h_ctr = h;
     HIPCHK(c, hipMemcpyAsync(c->B.ctr, c->h_ctr, sizeof(Counters), hipMemcpyHostToDevice, c->st));
     return 0;
+}
+
+std::string capacity_message(const rmc_ctx* c, u32 overflow, int depth) {
+    const u32 f = (overflow >> 8) & 15u;
+    if (!f) return "";
+    std::string what;
+    if (f & 1) what += std::string(what.empty() ? "" : ", ") + "currentTerm > " + std::to_string(c->cfg.max_term);
+    if (f & 2) what += std::string(what.empty() ? "" : ", ") + "Len(log) > " + std::to_string(c->cfg.max_log_len);
+    if (f & 4) what += std::string(what.empty() ? "" : ", ") + "Cardinality(DOMAIN messages) > " +
+                       std::to_string(c->cfg.max_msgs);
+    if (f & 8) what += std::string(what.empty() ? "" : ", ") + "messages[m] > " + std::to_string(c->cfg.max_dup);
+    return "a successor of a level-" + std::to_string(depth) + " state needs " + what +
+           ": beyond the packed capacity of a field no CONSTRAINT bounds (lower the depth bound or add a CONSTRAINT)";
 }
 
 int read_counters(rmc_ctx* c) {
@@ -665,6 +681,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         c->res.expand_kernel_seconds += 1e-3 * ms;
         const Counters& k = *c->h_ctr;
         if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full");
+        if (k.overflow >> 8) return fail(c, RMC_E_CAPACITY, capacity_message(c, k.overflow, depth));
         if (k.overflow & 4u) return fail(c, RMC_E_CAPACITY, "verification buffer full");
         if (k.overflow & 16u) return fail(c, RMC_E_CAPACITY, "symmetry tie buffer full");
         if (k.overflow & 8u) return fail(c, RMC_E_HIP, "verification: a stored state has no fingerprint slot");

@@ -126,6 +126,9 @@ void decode_state(const rmc_ctx* c, const rmc::u32* in, rmc_state_view* v);
 void init_view(const rmc_config& g, rmc_state_view* v);
 int reset_counters(rmc_ctx* c, bool keep_count);
 int read_counters(rmc_ctx* c);
+// RMC_E_CAPACITY message for an unbounded field a successor took past the
+// packed capacity (Counters.overflow bits 8-11), "" if none
+std::string capacity_message(const rmc_ctx* c, rmc::u32 overflow, int depth);
 // sharded mode (rmc_dist.cpp)
 int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user);
 int trace_sharded(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* instances, size_t cap,

@@ -214,6 +214,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
     }
     std::vector<Counters> rows((size_t)W);
+    int lvl_now = 1;  // the level being expanded (error messages)
     // level end: the all-gathered device counters; errors stop every rank alike
     auto level_end = [&]() -> int {
         const double tw = now_s();
@@ -223,6 +224,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         for (int r = 0; r < W; ++r) {
             const Counters& k = rows[(size_t)r];
             if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full on rank " + std::to_string(r));
+            if (k.overflow >> 8) return fail(c, RMC_E_CAPACITY, capacity_message(c, k.overflow, lvl_now));
             if (k.overflow & 4u) return fail(c, RMC_E_CAPACITY, "verification buffer full on rank " + std::to_string(r));
             if (k.overflow & 8u)
                 return fail(c, RMC_E_HIP, "verification: a fingerprint without a published state on rank " +
@@ -278,6 +280,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             break;
         }
         if (int rc = reset_counters(c, true)) return rc;
+        lvl_now = depth;
         u64 cursor = lo, ovf_known = 0, ovf_done = 0;
         const u64 frontier = hi - lo;
         // at least D.split rounds for a large level, so one round's exchange

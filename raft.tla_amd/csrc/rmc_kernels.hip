@@ -715,6 +715,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         }
                         if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
                     }
+                    if (P.unbounded && en && !in_model)  // a depth-bounded unconstrained model outgrew the encoding
+                        if (const int f = capacity_exceeded<S, K>(m, d, P)) atomicOr(&B.ctr->overflow, (u32)f << 8);
                     if (in_model && (SYM || h != h0)) {
                         key = h;
                         if constexpr (VERIFY) key &= P.fp_mask;

@@ -267,6 +267,8 @@ int main(int argc, char** argv) {
     if (simulate) return run_simulation(cfg, tla, raft, fopts, device, depth, num, seed);
     rmc_config c;
     char info[2048];
+    // -depth N: a model that leaves fields unbounded (MCraft.cfg as shipped) runs level by level
+    if (depth > 0) fopts |= RMC_FRONT_DEPTH_BOUNDED;
     int rc = rmc_model_from_files(cfg.c_str(), tla.c_str(), raft.empty() ? nullptr : raft.c_str(), fopts, &c, nullptr,
                                   info, sizeof info);
     if (rc) { printf("Error: %s\n", info); return 1; }

@@ -26,7 +26,8 @@ INV_NAMES = {INV_TYPEOK: "TypeOK", INV_ONE_LEADER: "OneLeaderPerTerm",
              INV_LEADER_VOTES: "LeaderVotesQuorum", INV_CAND_TERM: "CandidateTermNotInLog",
              INV_VOTES_GRANTED: "VotesGrantedInv", INV_QUORUM_LOG: "QuorumLogInv",
              INV_MORE_UP_TO_DATE: "MoreUpToDateCorrect", INV_LEADER_COMPLETE: "LeaderCompleteness"}
-FRONT_BUILTIN_RAFT, FRONT_SIMULATE = 1, 2
+FRONT_BUILTIN_RAFT, FRONT_SIMULATE, FRONT_DEPTH_BOUNDED = 1, 2, 4
+FLAG_UNBOUNDED_TERM, FLAG_UNBOUNDED_LOG, FLAG_UNBOUNDED_MSGS, FLAG_UNBOUNDED_DUP = 32, 64, 128, 256
 FAMILIES = ("Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
             "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
             "DropMessage")
@@ -207,14 +208,18 @@ def make_config(n_servers=3, n_values=2, max_term=2, max_log_len=1, max_msgs=2, 
                   invariants, device, max_depth, state_capacity, 0, device_window)
 
 
-def model_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False, simulate=False):
+def model_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False, simulate=False,
+                     depth_bounded=False):
     """rmc_model_from_files: (Config, SimConfig or None, provenance notes).
     Raises RmcError naming the construct when the model is not the compiled-in
-    raft.tla (with its recognised bug variant, bounds and invariants)."""
+    raft.tla (with its recognised bug variant, bounds and invariants).
+    depth_bounded: the caller sets max_depth (TLC -depth), so fields without a
+    CONSTRAINT are accepted at the packed capacity (RMC_FLAG_UNBOUNDED_*)."""
     lib = native()
     cfg, sc = Config(), SimConfig()
     info = C.create_string_buffer(4096)
-    opts = (FRONT_BUILTIN_RAFT if builtin_raft else 0) | (FRONT_SIMULATE if simulate else 0)
+    opts = (FRONT_BUILTIN_RAFT if builtin_raft else 0) | (FRONT_SIMULATE if simulate else 0) | \
+        (FRONT_DEPTH_BOUNDED if depth_bounded else 0)
     rc = lib.rmc_model_from_files(cfg_path.encode(), tla_path.encode() if tla_path else None,
                                   raft_path.encode() if raft_path else None, opts, C.byref(cfg),
                                   C.byref(sc) if simulate else None, info, 4096)

@@ -255,6 +255,12 @@ def test_reference_models_in_place():
     is a simulation model whose SmokeInit is recognised (k = 2)."""
     with pytest.raises(rmc.RmcError, match="infinite"):
         load("/root/reference/MCraft.cfg")
+    # under a depth bound (TLC -depth) it is accepted at the packed capacity
+    c, _, info = load("/root/reference/MCraft.cfg", depth_bounded=True)
+    unb = rmc.FLAG_UNBOUNDED_TERM | rmc.FLAG_UNBOUNDED_LOG | rmc.FLAG_UNBOUNDED_MSGS | rmc.FLAG_UNBOUNDED_DUP
+    assert (c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (3, 2, 14, 3, 8, 3)
+    assert (c.flags & unb) == unb and c.invariants == rmc.INV_TYPEOK
+    assert "/root/reference/raft.tla verified" in info and "depth bound" in info
     c, sc, info = load("/root/reference/Smokeraft.cfg", simulate=True)
     assert (c.n_servers, c.n_values, sc.smoke_k, sc.smoke_nat) == (3, 2, 2, 2)
     assert "/root/reference/raft.tla verified" in info and "Smokeraft.tla" in info
@@ -292,3 +298,23 @@ def test_front_fixtures_are_current():
     import make_front_fixtures
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "front_models.json")))
     assert make_front_fixtures.build() == want
+
+
+def test_unconstrained_model_needs_a_depth_bound():
+    """MCraft.cfg's layout without a CONSTRAINT (tests/golden/models/MCunbounded):
+    refused as infinite, accepted with RMC_FRONT_DEPTH_BOUNDED; unbounded fields
+    get the packed capacity and their RMC_FLAG_UNBOUNDED_* bit, and rmc_create
+    refuses such a config without max_depth (checked before any GPU call)."""
+    cfgp = os.path.join(MODELS, "MCunbounded.cfg")
+    with pytest.raises(rmc.RmcError, match="infinite"):
+        load(cfgp, builtin_raft=True)
+    c, _, info = load(cfgp, builtin_raft=True, depth_bounded=True)
+    unb = rmc.FLAG_UNBOUNDED_TERM | rmc.FLAG_UNBOUNDED_LOG | rmc.FLAG_UNBOUNDED_MSGS | rmc.FLAG_UNBOUNDED_DUP
+    assert (c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (14, 3, 8, 3) and (c.flags & unb) == unb
+    assert "depth bound" in info
+    # a bounded model is unaffected by the option
+    c2, _, _ = load(os.path.join(SPECS, "MCraftBounded.cfg"), builtin_raft=True, depth_bounded=True)
+    assert (c2.flags & unb) == 0 and (c2.max_term, c2.max_msgs) == (2, 2)
+    c.max_depth = 0
+    ctx = rmc.C.c_void_p()
+    assert rmc.native().rmc_create(rmc.C.byref(c), rmc.C.byref(ctx)) == -22  # RMC_E_INVAL: no depth bound

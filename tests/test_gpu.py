@@ -17,6 +17,7 @@ from tests.convert import check_trace, from_view, random_state, random_state_edg
 pytestmark = pytest.mark.gpu
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_levels.json")))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def cfg_from(p, capacity=1 << 25):
@@ -494,3 +495,40 @@ def test_diamond_skipping_cuts_probes_not_states(monkeypatch):
         assert res[flag][:3] == (g["distinct"], g["generated"], g["depth"]), flag
         assert [1] + res[flag][4] == g["level_new"], flag
     assert res["1"][3] <= 0.8 * res["0"][3], (res["1"][3], res["0"][3])
+
+
+@pytest.mark.gpu
+def test_unconstrained_model_under_a_depth_bound():
+    """MCraft.cfg as shipped has no CONSTRAINT; under -depth
+    it runs level by level.  Fixture in its layout:
+    depth 3 gives the survey's KAT (1 + 3 + 18 = 22 distinct, 1 + 6 + 27 = 34
+    generated); depths 4-5 equal the C oracle with every bound at the packed
+    capacity; depth 6 needs a 4th copy of a message (Duplicate), beyond the
+    capacity: RMC_E_CAPACITY naming messages[m], not a silent filter.  The CLI
+    prints TLC's lines for the depth-3 run."""
+    import subprocess
+    from tests import oracle_c
+    cfgp = os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg")
+    base, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, depth_bounded=True)
+    for depth in (3, 4, 5):
+        c = rmc.Config.from_buffer_copy(base)
+        c.max_depth = depth
+        c.state_capacity = 1 << 22
+        with rmc.Checker(c) as ck:
+            r = ck.run()
+        ref, _, _ = oracle_c.bfs(3, 2, 14, 3, 8, 3, threads=4, max_levels=depth, capacity=1 << 22)
+        assert (r.distinct, r.generated, r.depth) == (ref.distinct, ref.generated, ref.depth), depth
+        if depth == 3:
+            assert (r.distinct, r.generated, r.left_on_queue) == (22, 34, 18)
+    c = rmc.Config.from_buffer_copy(base)
+    c.max_depth = 6
+    c.state_capacity = 1 << 22
+    with rmc.Checker(c) as ck:
+        with pytest.raises(rmc.RmcError, match=r"messages\[m\] > 3") as e:
+            ck.run()
+    assert e.value.code == -28
+    exe = os.path.join(ROOT, "raft.tla_amd", "bin", "rmc-tlc")
+    out = subprocess.run([exe, "-depth", "3", "-builtin-raft", "-config", cfgp,
+                          os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.tla")],
+                         capture_output=True, text=True, timeout=120)
+    assert "34 states generated, 22 distinct states found, 18 states left on queue." in out.stdout, out.stdout
