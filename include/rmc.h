@@ -246,7 +246,9 @@ int rmc_trace(rmc_ctx* ctx, rmc_state_view* states, int32_t* families, int32_t* 
  * same model (constants, bounds, flags, seed; capacity >= the checkpoint's
  * states), load them and rebuild the fingerprint set from the states; the next
  * rmc_run_bfs continues from the first unexpanded level, with cumulative
- * counts.  Single-GPU contexts. */
+ * counts.  A sharded ctx (rmc_shard) writes and reads its own part,
+ * <path>.rank<r>; every rank of the same world calls them, and the recovered
+ * ctxs must be sharded the same way (rank, world) before rmc_recover. */
 int rmc_checkpoint(rmc_ctx* ctx, const char* path);
 int rmc_recover(rmc_ctx* ctx, const char* path);
 
@@ -328,8 +330,9 @@ int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, r
  * recv_bytes[s] from rank s (back to back in `recv`); allgather gathers
  * `bytes` from every rank into recv (rank order).  They return 0 on success.
  * keys_per_dest bounds the keys one round sends to one owner (0 = auto);
- * sent_cache_slots sizes the sent-cache (0 = auto).  Checkpoints and
- * full-state verification are single-GPU only. */
+ * sent_cache_slots sizes the sent-cache (0 = auto).  Full-state verification
+ * (RMC_FLAG_VERIFY_STATES) ships every remote successor and compares the ones
+ * the owner had seen; checkpoints are per rank; RMC_FLAG_SPILL is single-GPU. */
 typedef struct rmc_transport {
     void* user;
     int (*alltoallv)(void* user, const void* send, const uint64_t* send_bytes, void* recv,

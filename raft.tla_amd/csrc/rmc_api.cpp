@@ -277,6 +277,13 @@ int reset_counters(rmc_ctx* c, bool keep_count) {
     return 0;
 }
 
+// The checkpoint file of this ctx's part: <path> on one GPU, <path>.rank<r>
+// for rank r of a sharded search.
+std::string shard_path(const rmc_ctx* c, const char* path) {
+    if (!c->dist.on || c->dist.world <= 1) return path;
+    return std::string(path) + ".rank" + std::to_string(c->dist.rank);
+}
+
 std::string capacity_message(const rmc_ctx* c, u32 overflow, int depth) {
     const u32 f = (overflow >> 8) & 15u;
     if (!f) return "";
@@ -761,7 +768,8 @@ struct CkptHeader {
     uint32_t version, nw;
     rmc_config cfg;
     uint64_t count, nlevels;
-    int32_t depth, pad;
+    int32_t depth;
+    int32_t shard;   // sharded checkpoint: rank | world << 16 (0: single GPU)
     rmc_result res;
     uint64_t first;  // states are written from this index on (0: all; else the frontier)
     uint64_t slots;  // fingerprint-set slots dumped after the states (first > 0), else 0
@@ -802,15 +810,18 @@ int move_file(rmc_ctx* c, FILE* f, void* dev, u64 n, bool to_file) {
 // exist — the fingerprint set itself (TLC checkpoints its FPSet too).
 int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
-    if (c->dist.on) return fail(c, RMC_E_INVAL, "checkpoint: single-GPU runs only");
     if (c->level_start.size() < 2 || c->have_target)
         return fail(c, RMC_E_STATE, "checkpoint: needs a BFS stopped at a level boundary without a violation");
     if (c->res.left_on_queue == 0) return fail(c, RMC_E_STATE, "checkpoint: the search is complete");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->st));
-    FILE* f = fopen(path, "wb");
-    if (!f) return fail(c, RMC_E_IO, std::string("checkpoint: cannot create ") + path);
+    // a sharded search: every rank writes its own part, <path>.rank<r> (collective
+    // only in the sense that every rank calls it; the global counts ride in res)
+    const std::string file = shard_path(c, path);
+    FILE* f = fopen(file.c_str(), "wb");
+    if (!f) return fail(c, RMC_E_IO, "checkpoint: cannot create " + file);
     CkptHeader h{};
+    h.shard = c->dist.on ? (c->dist.rank | (c->dist.world << 16)) : 0;
     memcpy(h.magic, kCkptMagic, 8);
     h.version = 2;  // 2: rmc_config with device_window, spilled checkpoints
     h.nw = (uint32_t)c->NW;
@@ -840,15 +851,18 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
 
 int rmc_recover(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
-    if (c->dist.on) return fail(c, RMC_E_INVAL, "recover: single-GPU runs only");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    FILE* f = fopen(path, "rb");
-    if (!f) return fail(c, RMC_E_IO, std::string("recover: cannot open ") + path);
+    const std::string file = shard_path(c, path);
+    FILE* f = fopen(file.c_str(), "rb");
+    if (!f) return fail(c, RMC_E_IO, "recover: cannot open " + file);
     CkptHeader h{};
     int rc = 0;
     std::vector<u64> ls;
     if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 2)
         rc = fail(c, RMC_E_IO, "recover: not an rmc checkpoint");
+    else if (h.shard != (c->dist.on ? (c->dist.rank | (c->dist.world << 16)) : 0))
+        rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another shard layout (rank / world), or of a "
+                                  "single-GPU run recovered on a sharded ctx or the reverse");
     else if (h.nw != (uint32_t)c->NW || !same_model(h.cfg, c->cfg))
         rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another model (constants, bounds, flags or seed)");
     else if (h.first && (!c->spill.on || h.slots != c->table_slots))

@@ -192,19 +192,25 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     const u64 RB = (u64)(c->NW + 4) * 4;  // state record: packed state, global parent ref, footprint
     const u64 kcap = c->B.kcap;
     const double t0 = now_s();
+    // rmc_recover restored this rank's levels, parents and set (every rank of
+    // the checkpoint's world, each from its own part)
+    const bool resume = c->resume != 0;
+    c->resume = 0;
+    const rmc_result saved = c->res;
     c->res = rmc_result{};
-    c->level_start.clear();
+    if (!resume) c->level_start.clear();
     c->have_target = 0;
     D.keys_sent = D.states_sent = D.chunks = D.parked = 0;
     D.xfer_seconds = D.wait_seconds = 0;
-    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
+    if (!resume) HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->B.sent) HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
     const bool verify = c->sh.verify;
-    if (verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
+    if (verify && !resume) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
-    if (int rc = reset_counters(c, false)) return rc;
+    if (resume) c->h_ctr->count = c->level_start.back();
+    if (int rc = reset_counters(c, resume)) return rc;
     // ---- Init (raft.tla:125-129): stored by its owner only
-    {
+    if (!resume) {
         rmc_state_view iv;
         init_view(c->cfg, &iv);
         std::vector<u32> packed((size_t)c->NW);
@@ -239,13 +245,18 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         return 0;
     };
     if (int rc = level_end()) return rc;
-    c->level_start.push_back(0);
-    c->level_start.push_back(c->h_ctr->count);
-    if (verify && c->h_ctr->count)  // slot -> store index of the initial state(s)
+    if (!resume) {
+        c->level_start.push_back(0);
+        c->level_start.push_back(c->h_ctr->count);
+    }
+    if (verify && !resume && c->h_ctr->count)  // slot -> store index of the initial state(s)
         HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
     u64 total_prev = 0;
     for (const auto& k : rows) total_prev += k.count;
-    for (int r = 0; r < W && !c->have_target; ++r)  // Init's violation check (level 1)
+    if (resume && total_prev != saved.distinct)
+        return fail(c, RMC_E_IO, "recover: the ranks' parts hold " + std::to_string(total_prev) +
+                                     " states, the checkpoint " + std::to_string(saved.distinct));
+    for (int r = 0; r < W && !c->have_target && !resume; ++r)  // Init's violation check (level 1)
         if (rows[(size_t)r].viol != ~0ull) {
             c->res.violated_inv = 1 << (int)(rows[(size_t)r].viol & 15);
             c->res.violation_depth = 1;
@@ -260,8 +271,8 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         if (int rc = allgather(c, &mine, sizeof mine, all.data())) return rc;
         for (int x : all) any_cb |= x;
     }
-    u64 generated = 1, probes = 0;
-    int depth = 1;
+    u64 generated = resume ? saved.generated : 1, probes = resume ? saved.probes : 0;
+    int depth = resume ? c->resume_depth : 1;
     // Round sizing: rho = most keys one round sends one owner, per expanded
     // state, from the previous rounds (it varies along a frontier: states
     // received from other ranks are appended after the local ones).  A round

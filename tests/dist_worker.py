@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--sent-cache", type=int, default=1 << 22, help="sent-cache slots per rank")
     ap.add_argument("--verify", action="store_true", help="full-state verification (RMC_FLAG_VERIFY_STATES)")
     ap.add_argument("--fp-bits", type=int, default=64, help="verification test hook: fingerprint bits kept")
+    ap.add_argument("--max-depth", type=int, default=-1, help="override the case's depth bound")
+    ap.add_argument("--checkpoint", help="after the run, write each rank's part (rmc_checkpoint)")
+    ap.add_argument("--recover", help="before the run, load each rank's part (rmc_recover)")
     args = ap.parse_args()
     dev = args.device if args.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "nccl":
@@ -58,11 +61,15 @@ def main():
         cfg.state_capacity = args.capacity or (1 << 26)
         if args.verify:
             cfg.flags |= rmc.FLAG_VERIFY_STATES
+    if args.max_depth >= 0:
+        cfg.max_depth = args.max_depth
     with rmc.Checker(cfg) as ck:
         info = rdist.shard(ck, transport=args.transport, keys_per_dest=args.keys_per_dest,
                            sent_cache_slots=args.sent_cache)
         if args.fp_bits < 64:
             ck.set_fp_bits(args.fp_bits)
+        if args.recover:
+            ck.recover(args.recover)
         t0 = time.time()
         r = ck.run()  # collective: the global result on every rank
         wall = time.time() - t0
@@ -73,6 +80,8 @@ def main():
             allt = [None] * world
             dist.all_gather_object(allt, mine)
             assert all(t == mine for t in allt), "ranks disagree on the trace"
+        if args.checkpoint:
+            ck.checkpoint(args.checkpoint)
         reruns = [ck.run() for _ in range(args.rerun)]
         fields = ("distinct", "generated", "depth", "left_on_queue", "violated_inv", "violation_depth",
                   "collisions", "verified")

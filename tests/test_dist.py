@@ -205,3 +205,28 @@ def test_sharded_verification_full_bench_model(tmp_path):
     res = json.load(open(out))
     assert (res["distinct"], res["generated"], res["depth"]) == (1_227_465_177, 21_130_972_267, 56)
     assert res["collisions"] == 0 and res["verified"] > 1_000_000_000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,nproc,stop", [("small", 2, 20), ("small_sym", 3, 25)])
+def test_sharded_checkpoint_and_recover(case, nproc, stop, tmp_path):
+    """TLC -checkpoint / -recover on a sharded search: N ranks stop at depth
+    `stop`, each writes its part (<path>.rank<r>); N new rank processes recover
+    their parts (fingerprint sets rebuilt from the states) and finish with the
+    oracle's counts."""
+    g = GOLDEN[case]
+    ck = tmp_path / "ckpt"
+    out1, out2 = tmp_path / "r1.json", tmp_path / "r2.json"
+    base = [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--device", "0", "--backend", "gloo",
+            "--rerun", "0"]
+    r = _torchrun(nproc, base + ["--out", str(out1), "--max-depth", str(stop), "--checkpoint", str(ck)], 29730 + nproc)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    first = json.load(open(out1))
+    assert first["depth"] == stop and first["left_on_queue"] > 0
+    assert first["levels"] == g["level_new"][:stop]
+    assert all(os.path.exists(f"{ck}.rank{k}") for k in range(nproc))
+    r = _torchrun(nproc, base + ["--out", str(out2), "--max-depth", "0", "--recover", str(ck)], 29740 + nproc)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out2))
+    assert (res["distinct"], res["generated"], res["depth"]) == (g["distinct"], g["generated"], g["depth"])
+    assert sum(p["stored"] for p in res["per_rank"]) == g["distinct"]
