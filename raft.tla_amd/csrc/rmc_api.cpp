@@ -516,8 +516,16 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     }
     memset(c->h_ctr, 0, sizeof(Counters));
     if (c->sh.sym) {  // successors with tied signatures, canonicalised by k_ties after each launch
-        c->B.tie_cap = 1ull << 25;
-        if (hipMalloc(&c->B.ties, c->B.tie_cap * 8) != hipSuccess) {
+        // a lane defers at most one tied successor, so launches of at most
+        // tie_cap / lanes states cannot overflow it (run_bfs sizes them so);
+        // 2 GB of HBM, halved until it fits
+        c->B.tie_cap = 1ull << 28;
+        while (hipMalloc(&c->B.ties, c->B.tie_cap * 8) != hipSuccess) {
+            c->B.ties = nullptr;
+            c->B.tie_cap >>= 1;
+            if (c->B.tie_cap < (1ull << 20)) break;
+        }
+        if (!c->B.ties) {
             c->err = "device allocation failed (symmetry tie buffer)";
             return bail(RMC_E_NOMEM);
         }
@@ -631,9 +639,11 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, hipEventRecord(c->ev0, c->st));
         // verification mode: smaller launches, each followed by publishing its
         // new states (k_publish) and checking its deferred hits (k_verify)
-        // SYMMETRY: at most 2^24 states per launch, so the tied successors it
-        // defers (~1 % of lanes) fit the tie buffer
-        const u64 chunk = c->sh.verify ? (1ull << 20) : c->sh.sym ? (1ull << 24) : CHUNK;
+        // SYMMETRY: every lane of a launch could defer a tied successor, so a
+        // launch holds at most tie_cap / lanes states (5.6 M for S = 3, K = 4):
+        // the tie buffer cannot overflow whatever the model's tie rate
+        const u64 sym_chunk = c->sh.sym ? std::max<u64>(1, std::min<u64>(CHUNK, c->B.tie_cap / (u64)c->P.off[10])) : CHUNK;
+        const u64 chunk = c->sh.verify ? (1ull << 20) : c->sh.sym ? sym_chunk : CHUNK;
         for (u64 a = lo, b = 0; a < hi; a = b) {
             b = std::min(hi, a + chunk);
             if (c->spill.on) {

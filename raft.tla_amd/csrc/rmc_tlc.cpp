@@ -290,6 +290,10 @@ int main(int argc, char** argv) {
            c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,
            (c.flags & RMC_FLAG_SYMMETRY) ? ", SYMMETRY Permutations(Server)" : "",
            (c.flags & RMC_FLAG_BUG_QUORUM) ? ", BecomeLeader quorum guard weakened" : "");
+    if (c.invariants & (RMC_INV_VOTES_GRANTED | RMC_INV_QUORUM_LOG | RMC_INV_MORE_UP_TO_DATE | RMC_INV_LEADER_COMPLETE))
+        printf("Note: Committed(i) is read as the first min(commitIndex[i], Len(log[i])) entries; raft.tla:896's "
+               "SubSeq(log[i], 1, commitIndex[i]) is out of range when commitIndex[i] > Len(log[i]), which TLC "
+               "would report as an evaluation error (specs/MCraftBounded.tla).\n");
     rmc_ctx* ctx = nullptr;
     rc = rmc_create(&c, &ctx);
     if (rc) { printf("Error: rmc_create failed (%d)\n", rc); return 1; }
@@ -303,11 +307,8 @@ int main(int argc, char** argv) {
     std::vector<int32_t> tr_fam, tr_inst;
     rmc_result r{};
     if (gpus > 1) {
-        if (verify || !ckpt.empty() || !recover.empty()) {
-            printf("Error: -verify, -checkpoint and -recover are single-GPU options\n");
-            rmc_destroy(ctx);
-            return 1;
-        }
+        // -verify, -checkpoint and -recover work per rank: every rank compares
+        // its own hits and writes / reads its own part, <F>.rank<r>
         std::vector<rmc_ctx*> ctxs((size_t)gpus, nullptr);
         ctxs[0] = ctx;
         for (int k = 1; k < gpus; ++k) {
@@ -322,7 +323,8 @@ int main(int argc, char** argv) {
         uint8_t id[128];
         if (rmc_rccl_unique_id(id)) { printf("Error: rmc_rccl_unique_id failed\n"); return 1; }
         printf("Sharded over %d GPUs (librmc two-phase exchange over RCCL).\n", gpus);
-        printf("Computing initial states...\n");
+        if (!recover.empty()) printf("Recovering from checkpoint %s.rank0..%d...\n", recover.c_str(), gpus - 1);
+        else printf("Computing initial states...\n");
         fflush(stdout);
         std::atomic<int> done{0}, failed{-1};
         std::vector<std::string> errs((size_t)gpus);
@@ -336,9 +338,12 @@ int main(int argc, char** argv) {
                     failed.compare_exchange_strong(none, k);
                 };
                 if (rmc_shard(h, k, gpus, id, nullptr, 0, 0)) { bad("rmc_shard"); return; }
+                if (!recover.empty() && rmc_recover(h, recover.c_str())) { bad("rmc_recover"); return; }
                 if (rmc_run_bfs(h, k == 0 ? progress : nullptr, nullptr)) { bad("rmc_run_bfs"); return; }
                 rmc_result rr;
                 rmc_get_result(h, &rr);
+                if (!ckpt.empty() && rr.left_on_queue > 0 && !rr.violated_inv && !rr.deadlock &&
+                    rmc_checkpoint(h, ckpt.c_str())) { bad("rmc_checkpoint"); return; }
                 if (rr.violated_inv || rr.deadlock) {  // the trace walk is collective: every rank calls it
                     size_t n = 0;
                     if (rmc_trace(h, nullptr, nullptr, nullptr, 0, &n)) { bad("rmc_trace"); return; }
@@ -413,7 +418,9 @@ int main(int argc, char** argv) {
                (unsigned long long)r.chunks, (unsigned long long)r.keys_sent, (unsigned long long)r.states_sent,
                (unsigned long long)r.parked, r.exchange_seconds * 1e3, r.exchange_wait_seconds * 1e3);
     if (!ckpt.empty() && r.left_on_queue > 0 && !r.violated_inv && !r.deadlock) {
-        if (rmc_checkpoint(ctx, ckpt.c_str())) printf("Error: %s\n", rmc_last_error(ctx));
+        if (gpus > 1) printf("Checkpoint written to %s.rank0..%d (%llu states on the queue).\n", ckpt.c_str(), gpus - 1,
+                             (unsigned long long)r.left_on_queue);
+        else if (rmc_checkpoint(ctx, ckpt.c_str())) printf("Error: %s\n", rmc_last_error(ctx));
         else printf("Checkpoint written to %s (%llu states on the queue).\n", ckpt.c_str(),
                     (unsigned long long)r.left_on_queue);
     }

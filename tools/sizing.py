@@ -3,7 +3,11 @@ until a time budget) and print one JSON line per model with distinct/generated/
 depth/time.  Used to calibrate config 3 (5 servers, >= 1e9 distinct states,
 BASELINE.json configs[2]).
 
-    python tools/sizing.py S:V:MaxTerm:MaxLogLen:MaxMsgs:MaxDup[:verify][:dDEPTH] ... [--budget SECONDS]
+    python tools/sizing.py S:V:MaxTerm:MaxLogLen:MaxMsgs:MaxDup[:verify][:spill][:dDEPTH] ... [--budget SECONDS]
+
+`spill`: expanded levels move to host memory when the device store fills
+(RMC_FLAG_SPILL), so a model larger than HBM still runs to its fixpoint while
+its fingerprints fit.
 """
 import json
 import os
@@ -31,9 +35,11 @@ def main():
         f = sp.split(":")
         s, v, t, l, mm, dd = (int(x) for x in f[:6])
         verify = "verify" in f[6:]
+        spill = "spill" in f[6:]
         depth = max([int(x[1:]) for x in f[6:] if x.startswith("d")] or [0])
         cfg = rmc.make_config(n_servers=s, n_values=v, max_term=t, max_log_len=l, max_msgs=mm, max_dup=dd,
-                              check_deadlock=False, verify_states=verify, max_depth=depth)
+                              check_deadlock=False, verify_states=verify, max_depth=depth,
+                              spill=spill)
         t0 = time.time()
         rec = {"model": sp}
         try:
@@ -48,6 +54,7 @@ def main():
                            kernel_seconds=r.expand_kernel_seconds, probes=r.probes,
                            complete=r.left_on_queue == 0,
                            verified=r.verified, collisions=r.collisions,
+                           spilled=getattr(r, "spilled", 0), spills=getattr(r, "spills", 0),
                            rate=r.distinct / r.seconds if r.seconds else None)
         except rmc.RmcError as e:
             rec["error"] = str(e)
