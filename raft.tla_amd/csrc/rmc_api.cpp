@@ -517,9 +517,10 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     memset(c->h_ctr, 0, sizeof(Counters));
     if (c->sh.sym) {  // successors with tied signatures, canonicalised by k_ties after each launch
         // a lane defers at most one tied successor, so launches of at most
-        // tie_cap / lanes states cannot overflow it (run_bfs sizes them so);
-        // 2 GB of HBM, halved until it fits
-        c->B.tie_cap = 1ull << 28;
+        // tie_cap / lanes states cannot overflow it (run_bfs sizes them so):
+        // room for full 2^24-state launches (6.4 GB for S = 3, K = 4; smaller
+        // launches cost ~6 % on the MCraftBench bounds), halved until it fits
+        c->B.tie_cap = (u64)c->P.off[10] << 24;
         while (hipMalloc(&c->B.ties, c->B.tie_cap * 8) != hipSuccess) {
             c->B.ties = nullptr;
             c->B.tie_cap >>= 1;

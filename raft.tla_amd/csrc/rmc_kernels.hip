@@ -914,11 +914,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
 // WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
 // 4 waves/SIMD like k_expand_sort (uncapped it takes 131 VGPRs: 3 waves).
-template <int S, int K, int BATCH, bool WS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? 4 : 1))) void k_expand_dist(
+template <int S, int K, int BATCH, bool WS, int WPE = 4, bool DIA = true, bool EARLY = true>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? WPE : 1))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, true, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, DIA, DIA && EARLY>(P, PT, B, lo, hi);
     else
         expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
@@ -1379,20 +1379,27 @@ static hipError_t launch_sim_t(const Params& P, const u32* inits, u64 n_init, u6
 }
 
 // ---- host launchers (template dispatch on S, K, symmetry) ------------------------------
-// Blocks of the grid-stride kernels (RMC_EXPAND_GRID for A/B runs; default 2048).
+// Blocks of the expansion kernels (RMC_EXPAND_GRID for A/B runs; default
+// 1024 = the resident blocks at 4 waves/SIMD: 4 per CU x 256 CUs, so a launch
+// is one block round and every window sorts more tiles; 309.7 vs 315.6 ms per
+// MCraftBench BFS against 2048, profiles/r03/ab/).  The other grid-stride
+// kernels run 2048 blocks.
 static u64 expand_grid() {
     static u64 v = [] {
         const char* e = getenv("RMC_EXPAND_GRID");
         const long long x = e ? atoll(e) : 0;
-        return x >= 64 && x <= (1 << 20) ? (u64)x : (u64)2048;
+        return x >= 64 && x <= (1 << 20) ? (u64)x : (u64)1024;
     }();
     return v;
 }
 
 // Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
-// profiles/r02/ab/, profiles/r03/): 7 (default) = 6 with the stutter,
-// CONSTRAINT and commuting-diamond decisions taken before the lane hashes;
-// 6 = the lane-superset walk over class-sorted
+// profiles/r02/ab/, profiles/r03/ab/): 6 (default) = commuting-diamond
+// skipping (7.18 G instead of 10.41 G probes per MCraftBench BFS: 315 vs
+// 337-340 ms) on the lane-superset walk over class-sorted windows;
+// 7 = 6 with the stutter, CONSTRAINT and commuting-diamond decisions taken
+// before the lane hashes (317-322 ms: the split costs more than the hashes
+// it saves); without the diamond, 6 is the round-2 kernel: the lane-superset walk over class-sorted
 // windows of up to 2048 states (k_expand_sort, 4 waves/SIMD; 317 vs 343 ms per
 // MCraftBench BFS against 1; shapes with > 64 lanes run 1), 1 = every lane of
 // every state, the parent's per-component mixes precomputed (k_expand, 95
@@ -1403,7 +1410,7 @@ static u64 expand_grid() {
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 7;
+        return e ? atoi(e) : 6;
     }();
     return v;
 }
@@ -1443,8 +1450,9 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs
-    const u64 grid = expand_grid();
+    // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs;
+    // the expansion kernels (4 waves/SIMD) one round of resident blocks
+    const u64 grid = (which == 0 || which == 3) ? expand_grid() : (u64)2048;
     const u64 g = blocks < grid ? blocks : grid;
     if (which == 0) {
         if constexpr (SYM) {
@@ -1483,13 +1491,34 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     } else if (which == 3) {
         if constexpr (SYM)
             hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-        else
-            if (dist_variant() == 1)
+        else {
+            bool ab = false;
+            if constexpr (S == 3 && K == 4) {  // A/B variants, bench shape only: 2 = 3 waves/SIMD (no
+                ab = true;  // spills), 3 = 6 probes in flight, 4 = no diamond skipping, 5 = diamonds, not EARLY
+                if (dist_variant() == 2)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 3>), dim3((unsigned)g), dim3(256), 0, st, P,
+                                       PT, B, a, b);
+                else if (dist_variant() == 3)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, 6, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                                       b);
+                else if (dist_variant() == 4)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>), dim3((unsigned)g), dim3(256), 0,
+                                       st, P, PT, B, a, b);
+                else if (dist_variant() == 5)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false>), dim3((unsigned)g), dim3(256),
+                                       0, st, P, PT, B, a, b);
+                else
+                    ab = false;
+            }
+            if (ab) {
+            } else if (dist_variant() == 1) {
                 hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
                                    b);
-            else
+            } else {
                 hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
                                    b);
+            }
+        }
     } else if (which == 8) {  // a = keys per destination block (max); out = replies
         hipLaunchKernelGGL((k_materialize_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B,
                            reinterpret_cast<const uint8_t*>(in), a, b);
