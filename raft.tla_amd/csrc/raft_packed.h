@@ -475,14 +475,17 @@ RMC_HD u64 sel64(const u64 (&a)[N], int i) {
 // delta_fp with the parent's mixes precomputed: same result, fewer mixes.
 template <int S, int K>
 RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
-                        const Params& P, u64* h, int* nmsg_out = nullptr) {
+                        const Params& P, u64* h, int* nmsg_out = nullptr, u64* hw_new = nullptr) {
     u64 hh = pm.h0;
     int nmsg = pm.nmsg;
     if (d.srv >= 0) {
         if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
         if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
         const u64 wo = selw<S>(w, d.srv);
-        if (d.w_new != wo) hh += hS(d.w_new, (u32)d.srv) - sel64<S>(pm.hw, d.srv);
+        const u64 ho = sel64<S>(pm.hw, d.srv);
+        const u64 hn = d.w_new != wo ? hS(d.w_new, (u32)d.srv) : ho;
+        hh += hn - ho;
+        if (hw_new) *hw_new = hn;  // the new word's mix (the sharded owner reuses it)
     }
     if (d.rm >= 0) {
         const u32 sl = selm<K>(m, d.rm);
@@ -533,11 +536,15 @@ RMC_HD int delta_bounds_pre(const u32 (&m)[K], const ParentMix<S, K>& pm, const 
 }
 // ... and the fingerprint of a successor known to be in the model (same value as delta_fp_pre).
 template <int S, int K>
-RMC_HD u64 delta_hash_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d) {
+RMC_HD u64 delta_hash_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
+                          u64* hw_new = nullptr) {
     u64 hh = pm.h0;
     if (d.srv >= 0) {
         const u64 wo = selw<S>(w, d.srv);
-        if (d.w_new != wo) hh += hS(d.w_new, (u32)d.srv) - sel64<S>(pm.hw, d.srv);
+        const u64 ho = sel64<S>(pm.hw, d.srv);
+        const u64 hn = d.w_new != wo ? hS(d.w_new, (u32)d.srv) : ho;
+        hh += hn - ho;
+        if (hw_new) *hw_new = hn;
     }
     if (d.rm >= 0) {
         const u32 sl = selm<K>(m, d.rm);

@@ -407,24 +407,29 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable 
 // server 0's word — a successor that does not touch server 0 (bag-only
 // actions, actions of the other servers) stays on its parent's rank, so far
 // fewer successors cross GPUs; balance relies on server 0's many word values.
-// Mode 2: by the words of servers 0 and 1 (more distinct values: better
-// balance, successors of two servers cross).
-constexpr u64 OWN_C0 = 0x6a09e667f3bcc909ull, OWN_C1 = 0xbb67ae8584caa73bull;
-__device__ __forceinline__ u64 own_h0(u64 w0, const DevBufs& B) { return B.owner_mode ? mix64(w0 ^ OWN_C0) : 0ull; }
-__device__ __forceinline__ u64 own_h1(u64 w1, const DevBufs& B) { return B.owner_mode == 2 ? mix64(w1 ^ OWN_C1) : 0ull; }
+// Mode 2 (default): by the words of servers 0 and 1 (more distinct values:
+// better balance, successors of two servers cross).  The word hash is the
+// fingerprint's own component mix hS(w, i): the expansion kernel has the
+// parent's mixes and the new word's mix at hand, so routing a successor costs
+// no extra mix64 (and no extra registers) in its lane loop.
 __device__ __forceinline__ u32 owner_state(u64 key, u64 w0, u64 w1, const DevBufs& B) {
     if (B.owner_mode == 0) return owner_of(key, B.world);
-    return owner_of(own_h0(w0, B) + own_h1(w1, B), B.world);
+    return owner_of(hS(w0, 0u) + (B.owner_mode == 2 ? hS(w1, 1u) : 0ull), B.world);
 }
-// Owner of a successor: a lane that leaves servers 0 and 1 alone (mode 2; mode 1:
-// server 0) keeps its parent's owner — this rank, since a state is stored by
-// its owner — so only the other lanes mix their words.
-template <int S>
-__device__ __forceinline__ u32 owner_succ(u64 key, const Delta& d, const u64 (&w)[S], const DevBufs& B) {
+// Owner of a successor from the parent's word mixes (pm.hw) and the new word's
+// mix hn (delta_fp_pre / delta_hash_pre): a lane that leaves servers 0 and 1
+// alone (mode 2; mode 1: server 0) keeps its parent's owner — this rank, since
+// a state is stored by its owner.
+template <int S, int K>
+__device__ __forceinline__ u32 owner_succ(u64 key, const Delta& d, const ParentMix<S, K>& pm, u64 hn,
+                                          const DevBufs& B) {
     if (B.world == 1) return 0;
     if (B.owner_mode == 0) return owner_of(key, B.world);
-    if (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2))
-        return owner_state(key, d.srv == 0 ? d.w_new : w[0], d.srv == 1 ? d.w_new : w[1], B);
+    if (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2)) {
+        const u64 a = d.srv == 0 ? hn : pm.hw[0];
+        const u64 b = B.owner_mode == 2 ? (d.srv == 1 ? hn : pm.hw[1]) : 0ull;
+        return owner_of(a + b, B.world);
+    }
     return B.rank;
 }
 
@@ -519,6 +524,163 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
     wave_sync_lds();
 }
 
+// Sharded mode with send markers (MARK): the local fingerprint set doubles
+// as the record of keys already sent — a successor owned elsewhere is
+// CAS-inserted into it like a local one, so the probe loop is the single-GPU
+// loop and a remote key is shipped at most once per rank (a lossless
+// sent-cache).  The list carries only (rel | owner << 24, lane); here each
+// listed successor is re-derived: owned ones are stored as in flush_new,
+// the others get their key back from the materialised successor (the
+// fingerprint is order-free: it equals the incremental probe key) and go to
+// the owner's outbox with a ticket.  One reservation atomic per destination.
+template <int S, int K>
+__device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                           const uint8_t* l_lane, u32 n) {
+    constexpr int NW = 2 * S + K;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    const u64 lt = (1ull << me) - 1ull;
+    u64 mine = 0;  // lane dd: entries for destination dd, then its next slot
+    for (u32 e0 = 0; e0 < n; e0 += 64) {
+        const u32 e = e0 + (u32)me;
+        const u32 dest = e < n ? (l_rel[e] >> 24) : 0xFFu;
+        for (u32 dd = 0; dd < B.world; ++dd) {
+            const u64 bal = __ballot(dest == dd);
+            if ((u32)me == dd) mine += (u64)__popcll(bal);
+        }
+    }
+    if ((u32)me < B.world && mine) {
+        unsigned long long* ctr = (u32)me == B.rank ? (unsigned long long*)&B.ctr->count : &B.ocount[me];
+        mine = atomicAdd(ctr, (unsigned long long)mine);
+    }
+    for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
+        const u32 e = e0 + (u32)me;
+        const bool valid = e < n;
+        const u32 rd = valid ? l_rel[e] : 0xFF000000u;
+        const u32 dest = rd >> 24;
+        u64 slot = ~0ull;
+        for (u32 dd = 0; dd < B.world; ++dd) {
+            const u64 bal = __ballot(dest == dd);
+            if (!bal) continue;
+            const u64 base = bcast64(mine, (int)dd);
+            if (dest == dd) slot = base + (u64)__popcll(bal & lt);
+            if ((u32)me == dd) mine += (u64)__popcll(bal);
+        }
+        if (!valid) continue;
+        const u64 rel = rd & 0xFFFFFFu;
+        const int lane = l_lane[e];
+        if (dest == B.rank && slot >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, d, wo, mo);
+        if (dest != B.rank) {  // the key to its owner, the ticket stays here
+            const u64 key = fp_of_materialised<S, K>(wo, mo, P);
+            if (slot >= B.kcap) {  // outbox full: parked, sent by a later round of this level
+                const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
+                if (q < B.ovf_cap) {
+                    B.ovf[2 * q] = key;
+                    B.ovf[2 * q + 1] = (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56);
+                } else {
+                    atomicOr(&B.ctr->overflow, 2u);
+                }
+                continue;
+            }
+            B.key_out[(u64)dest * B.kcap + slot] = key;
+            B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
+            continue;
+        }
+        store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
+        B.parent[slot] = B.ref_tag | (lo + rel);
+        B.act[slot] = (uint8_t)lane;
+        B.foot[slot] = make_foot<S, K>(m, lane, d, P);
+        const int v = check_invariants<S, K>(wo, mo, P);
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
+    }
+    wave_sync_lds();
+}
+
+// flush_mark with the owner decided here (FOWN): the probe loop is then the
+// single-GPU loop exactly (no owner per probe).  Each 64-entry round
+// re-derives its successors, routes them by their words (owner_state) and
+// reserves slots with one atomic per destination present in the round.
+template <int S, int K>
+__device__ __forceinline__ void flush_mark_own(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                               const uint8_t* l_lane, u32 n) {
+    constexpr int NW = 2 * S + K;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    const u64 lt = (1ull << me) - 1ull;
+    for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
+        const u32 e = e0 + (u32)me;
+        const bool valid = e < n;
+        const u64 rel = valid ? (u64)(l_rel[e] & 0xFFFFFFu) : 0ull;
+        const int lane = valid ? (int)l_lane[e] : 0;
+        u64 w[S];
+        u32 m[K];
+        Delta d;
+        u64 wo[S];
+        u32 mo[K];
+        u32 dest = 0xFFu;
+        if (valid) {
+            load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+            lane_delta<S, K>(w, m, lane, P, d);
+            materialise<S, K>(w, m, d, wo, mo);
+            dest = (B.owner_mode == 0) ? owner_of(fp_of_materialised<S, K>(wo, mo, P), B.world)
+                 : (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2)) ? owner_state(0ull, wo[0], wo[1], B)
+                 : B.rank;
+        }
+        u64 slot = ~0ull;
+        for (u32 dd = 0; dd < B.world; ++dd) {  // one reservation atomic per destination present
+            const u64 bal = __ballot(dest == dd);
+            if (!bal) continue;
+            const int leader = __ffsll((long long)bal) - 1;
+            u64 base = 0;
+            if (me == leader) {
+                unsigned long long* ctr = dd == B.rank ? (unsigned long long*)&B.ctr->count : &B.ocount[dd];
+                base = atomicAdd(ctr, (unsigned long long)__popcll(bal));
+            }
+            base = bcast64(base, leader);
+            if (dest == dd) slot = base + (u64)__popcll(bal & lt);
+        }
+        if (!valid) continue;
+        if (dest != B.rank) {  // the key to its owner, the ticket stays here
+            const u64 key = fp_of_materialised<S, K>(wo, mo, P);
+            if (slot >= B.kcap) {  // outbox full: parked, sent by a later round of this level
+                const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
+                if (q < B.ovf_cap) {
+                    B.ovf[2 * q] = key;
+                    B.ovf[2 * q + 1] = (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56);
+                } else {
+                    atomicOr(&B.ctr->overflow, 2u);
+                }
+                continue;
+            }
+            B.key_out[(u64)dest * B.kcap + slot] = key;
+            B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
+            continue;
+        }
+        if (slot >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
+        store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
+        B.parent[slot] = B.ref_tag | (lo + rel);
+        B.act[slot] = (uint8_t)lane;
+        B.foot[slot] = make_foot<S, K>(m, lane, d, P);
+        const int v = check_invariants<S, K>(wo, mo, P);
+        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
+    }
+    wave_sync_lds();
+}
+
 // Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
 // processed BATCH at a time so BATCH fingerprint probes per thread are in
 // flight together (the kernel is bound by probe latency, not bandwidth).
@@ -528,8 +690,13 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // DIA: commuting-diamond successors are not probed (raft_packed.h "commuting
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false>
+          bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
+          bool MARK = false, bool FOWN = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
+    static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
+    static_assert(!FOWN || MARK, "owner decided in the flush: with send markers only");
+    constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
+    constexpr bool OWNP = DIST && !FOWN;   // the owner of every probe, decided in the lane loop
     static_assert(!DIA || (!SYM && !VERIFY), "diamond skipping: not under SYMMETRY or verification");
     // EARLY: the stutter / CONSTRAINT / diamond decisions come before the hash,
     // so a lane that does not probe never hashes (needs the parent's mixes)
@@ -551,21 +718,21 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
-    constexpr int LCAP = DIST ? 256 : WCAP;
+    constexpr int LCAP = SENTC ? 256 : WCAP;
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
-    __shared__ uint8_t s_dest[DIST ? 4 : 1][DIST ? LCAP : 1];
-    __shared__ u64 s_lkey[DIST ? 4 : 1][DIST ? LCAP : 1];  // sharded: the key of each listed successor
+    __shared__ uint8_t s_dest[SENTC ? 4 : 1][SENTC ? LCAP : 1];
+    __shared__ u64 s_lkey[SENTC ? 4 : 1][SENTC ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
-    __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
+    __shared__ uint8_t s_own[OWNP ? BATCH : 1][OWNP ? 256 : 1];  // owner rank per probe
     __shared__ u32 s_bins[SORT && FSORT ? 4 : 1][SORT && FSORT ? 128 : 1];  // FSORT: 256 16-bit class counters
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
     const u64 lt_mask = (1ull << me) - 1ull;
     u32* l_rel = s_rel[wv];
     uint8_t* l_lane = s_lane[wv];
-    uint8_t* l_dest = s_dest[DIST ? wv : 0];
-    u64* l_key = s_lkey[DIST ? wv : 0];
+    uint8_t* l_dest = s_dest[SENTC ? wv : 0];
+    u64* l_key = s_lkey[SENTC ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u64 gen = 0;
     u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
@@ -684,6 +851,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     const int en = d.en && live;
                     g += (u32)en;
                     u64 h = 0;
+                    u64 hwn = 0;  // DIST: the mix of the changed server word (owner routing)
                     int in_model = 0;
                     if constexpr (SYM) {
                         // a stutter (successor = parent: no bag change, no word change) is never probed
@@ -706,9 +874,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                             const bool stutter = d.rm < 0 && !d.has_add && (d.srv < 0 || d.w_new == selw<S>(w, d.srv));
                             in_model = !stutter && delta_bounds_pre<S, K>(m, pmx, d, P, &nmb) &&
                                        !diamond_skip<S, K>(m, lane, d, nmb, dm, P);
-                            h = in_model ? delta_hash_pre<S, K>(w, m, pmx, d) : h0;
+                            h = in_model ? delta_hash_pre<S, K>(w, m, pmx, d, DIST ? &hwn : nullptr) : h0;
                         } else {
-                            if constexpr (PRE) in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr);
+                            if constexpr (PRE)
+                                in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr,
+                                                              DIST ? &hwn : nullptr);
                             else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
                             if constexpr (DIA)
                                 if (in_model && h != h0 && diamond_skip<S, K>(m, lane, d, nmb, dm, P)) in_model = 0;
@@ -721,7 +891,16 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         key = h;
                         if constexpr (VERIFY) key &= P.fp_mask;
                         key = key ? key : 1ull;
-                        if constexpr (DIST) s_own[b][threadIdx.x] = (uint8_t)owner_succ<S>(key, d, w, B);
+                        if constexpr (OWNP) {
+                            if constexpr (PRE) s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(key, d, pmx, hwn, B);
+                            else  // no parent mixes: the successor's words 0 and 1 when it changes one
+                                s_own[b][threadIdx.x] = (uint8_t)(
+                                    B.world == 1 ? 0u
+                                    : B.owner_mode == 0 ? owner_of(key, B.world)
+                                    : (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2))
+                                        ? owner_state(key, d.srv == 0 ? d.w_new : w[0], d.srv == 1 ? d.w_new : w[1], B)
+                                        : B.rank);
+                        }
                     }
                 }
                 s_key[b][threadIdx.x] = key;
@@ -745,7 +924,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
                 key[b] = s_key[b][threadIdx.x];
-                if constexpr (DIST) {
+                if constexpr (SENTC) {
                     const bool remote = key[b] && s_own[b][threadIdx.x] != B.rank;
                     // no sent-cache in verification mode (B.sent null): every remote successor is shipped
                     cur[b] = !key[b] ? 0ull
@@ -770,7 +949,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     }
                     continue;
                 }
-                if constexpr (DIST) {
+                if constexpr (SENTC) {
                     if (s_own[b][threadIdx.x] != B.rank) {  // not sent before (lossy cache): ship it
                         if (B.sent) B.sent[(key[b] >> 8) & B.smask] = key[b];
                         newbits |= 1u << b;
@@ -842,16 +1021,20 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 if (bal) {
                     if (is_new) {
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
-                        l_rel[pos] = (SORT && FSORT) ? (u32)rel | ((u32)(cp >> (8 * b)) << 24) : (u32)rel;
+                        l_rel[pos] = (SORT && FSORT) ? (u32)rel | ((u32)(cp >> (8 * b)) << 24)
+                                   : (MARK && !FOWN) ? (u32)rel | ((u32)s_own[OWNP ? b : 0][OWNP ? threadIdx.x : 0] << 24)
+                                   : (u32)rel;
                         l_lane[pos] = (uint8_t)(SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b);
-                        if constexpr (DIST) {
+                        if constexpr (SENTC) {
                             l_dest[pos] = s_own[b][threadIdx.x];
                             l_key[pos] = key[b];
                         }
                     }
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
-                        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
+                        if constexpr (FOWN) flush_mark_own<S, K>(P, B, lo, l_rel, l_lane, n);
+                        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+                        else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
                         else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
@@ -864,7 +1047,9 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     }
     if (n) {
-        if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
+        if constexpr (FOWN) flush_mark_own<S, K>(P, B, lo, l_rel, l_lane, n);
+        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+        else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
         else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
@@ -914,11 +1099,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
 // WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
 // 4 waves/SIMD like k_expand_sort (uncapped it takes 131 VGPRs: 3 waves).
-template <int S, int K, int BATCH, bool WS, int WPE = 4, bool DIA = true, bool EARLY = true>
+template <int S, int K, int BATCH, bool WS, int WPE = 4, bool DIA = true, bool EARLY = true, bool MARK = false,
+          bool FOWN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? WPE : 1))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, DIA, DIA && EARLY>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, DIA, DIA && EARLY, MARK, FOWN>(
+            P, PT, B, lo, hi);
     else
         expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
 }
@@ -1452,7 +1639,8 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs;
     // the expansion kernels (4 waves/SIMD) one round of resident blocks
-    const u64 grid = (which == 0 || which == 3) ? expand_grid() : (u64)2048;
+    // (SYMMETRY keeps 2048: 79.7 vs 81.5 ms on the MCraftBench bounds)
+    const u64 grid = ((which == 0 && !SYM) || which == 3) ? expand_grid() : (u64)2048;
     const u64 g = blocks < grid ? blocks : grid;
     if (which == 0) {
         if constexpr (SYM) {
@@ -1494,7 +1682,9 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         else {
             bool ab = false;
             if constexpr (S == 3 && K == 4) {  // A/B variants, bench shape only: 2 = 3 waves/SIMD (no
-                ab = true;  // spills), 3 = 6 probes in flight, 4 = no diamond skipping, 5 = diamonds, not EARLY
+                ab = true;  // spills), 3 = 6 probes in flight, 4 = no diamond skipping, 5 = diamonds, not EARLY,
+                            // 6 = 5 with send markers in the local set (flush_mark), 7 = 6 without diamonds,
+                            // 8 = 6 with the owner decided in the flush (flush_mark_own), 9 = 8 without diamonds
                 if (dist_variant() == 2)
                     hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 3>), dim3((unsigned)g), dim3(256), 0, st, P,
                                        PT, B, a, b);
@@ -1507,6 +1697,18 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                 else if (dist_variant() == 5)
                     hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false>), dim3((unsigned)g), dim3(256),
                                        0, st, P, PT, B, a, b);
+                else if (dist_variant() == 6)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>), dim3((unsigned)g),
+                                       dim3(256), 0, st, P, PT, B, a, b);
+                else if (dist_variant() == 7)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>), dim3((unsigned)g),
+                                       dim3(256), 0, st, P, PT, B, a, b);
+                else if (dist_variant() == 8)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true, true>), dim3((unsigned)g),
+                                       dim3(256), 0, st, P, PT, B, a, b);
+                else if (dist_variant() == 9)
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true, true>), dim3((unsigned)g),
+                                       dim3(256), 0, st, P, PT, B, a, b);
                 else
                     ab = false;
             }

@@ -16,4 +16,4 @@ run single "" && run d1 --force-dist RMC_DIST_VARIANT=1 && run d5 --force-dist R
   && run single2 "" && run d1b --force-dist RMC_DIST_VARIANT=1 || exit $?
 timeout -k 10 200 python -u tools/sym_bench.py default 300000000 > gpurun_out/r03h_sym.jsonl 2> gpurun_out/r03h_sym.err || exit $?
 RMC_EXPAND_GRID=2048 timeout -k 10 200 python -u tools/sym_bench.py default 300000000 > gpurun_out/r03h_sym2048.jsonl 2> gpurun_out/r03h_sym2048.err || exit $?
-bash tools/gpu/r03g.sh
+# (PC sampling is not available on this pool)
