@@ -631,7 +631,8 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     D.in_cap = W * kcap;
     bool ok = hipStreamCreateWithFlags(&D.xs, hipStreamNonBlocking) == hipSuccess;
     // full-state verification ships every remote successor: no sent-cache
-    if (!c->sh.verify) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
+    // (the default kernel keeps send markers in the fingerprint set instead)
+    if (!c->sh.verify && (c->sh.sym || dist_uses_sent_cache())) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
     const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
     ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
     for (auto& S : D.set) {
@@ -652,6 +653,19 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     if (!ok) {
         free_dist(c);
         return fail(c, RMC_E_NOMEM, "sharded-mode buffers do not fit (lower keys_per_dest / sent_cache_slots)");
+    }
+    // send markers share the fingerprint set with this rank's states: twice the
+    // slots keeps the load of linear probing near the single-GPU one (when
+    // HBM allows; otherwise the set stays as rmc_create sized it)
+    if (world > 1 && !c->sh.verify && !c->sh.sym && !dist_uses_sent_cache() && !D.table_grown) {
+        u64* t2 = nullptr;
+        if (hipMalloc(&t2, c->table_slots * 16) == hipSuccess) {
+            (void)hipFree(c->B.table);
+            c->B.table = t2;
+            c->table_slots *= 2;
+            c->B.tmask = c->table_slots - 1;
+            D.table_grown = 1;
+        }
     }
     D.ag_cap = 4096;
     D.debug = getenv("RMC_DIST_DEBUG") != nullptr;

@@ -111,6 +111,10 @@ hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64
 // Sharded mode: move parked keys ovf[a, a + n) into the (emptied) outbox; n <= kcap.
 hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st);
 
+// Sharded expansion: does the selected kernel (RMC_DIST_VARIANT) use the lossy
+// sent-cache B.sent, or send markers in the fingerprint set?
+bool dist_uses_sent_cache();
+
 // Fingerprint salt for the kernels of this device (0 = default hash).
 hipError_t set_fp_salt(u64 seed, hipStream_t st);
 

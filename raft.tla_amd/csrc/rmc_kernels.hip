@@ -607,80 +607,6 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
     wave_sync_lds();
 }
 
-// flush_mark with the owner decided here (FOWN): the probe loop is then the
-// single-GPU loop exactly (no owner per probe).  Each 64-entry round
-// re-derives its successors, routes them by their words (owner_state) and
-// reserves slots with one atomic per destination present in the round.
-template <int S, int K>
-__device__ __forceinline__ void flush_mark_own(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
-                                               const uint8_t* l_lane, u32 n) {
-    constexpr int NW = 2 * S + K;
-    wave_sync_lds();
-    const int me = (int)__lane_id();
-    const u64 lt = (1ull << me) - 1ull;
-    for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
-        const u32 e = e0 + (u32)me;
-        const bool valid = e < n;
-        const u64 rel = valid ? (u64)(l_rel[e] & 0xFFFFFFu) : 0ull;
-        const int lane = valid ? (int)l_lane[e] : 0;
-        u64 w[S];
-        u32 m[K];
-        Delta d;
-        u64 wo[S];
-        u32 mo[K];
-        u32 dest = 0xFFu;
-        if (valid) {
-            load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
-            lane_delta<S, K>(w, m, lane, P, d);
-            materialise<S, K>(w, m, d, wo, mo);
-            dest = (B.owner_mode == 0) ? owner_of(fp_of_materialised<S, K>(wo, mo, P), B.world)
-                 : (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2)) ? owner_state(0ull, wo[0], wo[1], B)
-                 : B.rank;
-        }
-        u64 slot = ~0ull;
-        for (u32 dd = 0; dd < B.world; ++dd) {  // one reservation atomic per destination present
-            const u64 bal = __ballot(dest == dd);
-            if (!bal) continue;
-            const int leader = __ffsll((long long)bal) - 1;
-            u64 base = 0;
-            if (me == leader) {
-                unsigned long long* ctr = dd == B.rank ? (unsigned long long*)&B.ctr->count : &B.ocount[dd];
-                base = atomicAdd(ctr, (unsigned long long)__popcll(bal));
-            }
-            base = bcast64(base, leader);
-            if (dest == dd) slot = base + (u64)__popcll(bal & lt);
-        }
-        if (!valid) continue;
-        if (dest != B.rank) {  // the key to its owner, the ticket stays here
-            const u64 key = fp_of_materialised<S, K>(wo, mo, P);
-            if (slot >= B.kcap) {  // outbox full: parked, sent by a later round of this level
-                const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
-                if (q < B.ovf_cap) {
-                    B.ovf[2 * q] = key;
-                    B.ovf[2 * q + 1] = (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56);
-                } else {
-                    atomicOr(&B.ctr->overflow, 2u);
-                }
-                continue;
-            }
-            B.key_out[(u64)dest * B.kcap + slot] = key;
-            B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
-            continue;
-        }
-        if (slot >= B.cap) {
-            atomicOr(&B.ctr->overflow, 1u);
-            continue;
-        }
-        store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
-        B.parent[slot] = B.ref_tag | (lo + rel);
-        B.act[slot] = (uint8_t)lane;
-        B.foot[slot] = make_foot<S, K>(m, lane, d, P);
-        const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
-    }
-    wave_sync_lds();
-}
-
 // Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
 // processed BATCH at a time so BATCH fingerprint probes per thread are in
 // flight together (the kernel is bound by probe latency, not bandwidth).
@@ -691,12 +617,10 @@ __device__ __forceinline__ void flush_mark_own(const Params& P, const DevBufs& B
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
           bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
-          bool MARK = false, bool FOWN = false>
+          bool MARK = false, int WTILES = 8>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
-    static_assert(!FOWN || MARK, "owner decided in the flush: with send markers only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
-    constexpr bool OWNP = DIST && !FOWN;   // the owner of every probe, decided in the lane loop
     static_assert(!DIA || (!SYM && !VERIFY), "diamond skipping: not under SYMMETRY or verification");
     // EARLY: the stutter / CONSTRAINT / diamond decisions come before the hash,
     // so a lane that does not probe never hashes (needs the parent's mixes)
@@ -711,7 +635,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     static_assert(!SORT || BATCH * 7 <= 64, "SORT packs a batch's lanes 7 bits each into one u64");
     static_assert(!(SORT && FSORT && (SYM || DIST)), "class-sorted flushes are built for the plain kernel only");
     static_assert(!WSORT || SORT, "WSORT needs SORT");
-    constexpr int WT = WSORT ? 8 : 1;  // tiles per window
+    constexpr int WT = WSORT ? WTILES : 1;  // tiles per window
     __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
     __shared__ uint8_t s_wcls[WSORT ? 256 * WT : 1];  // WSORT: class of each window position
     __shared__ u32 s_wbin[WSORT ? 64 : 1];            // WSORT: class counters / cursors
@@ -724,7 +648,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     __shared__ uint8_t s_dest[SENTC ? 4 : 1][SENTC ? LCAP : 1];
     __shared__ u64 s_lkey[SENTC ? 4 : 1][SENTC ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
-    __shared__ uint8_t s_own[OWNP ? BATCH : 1][OWNP ? 256 : 1];  // owner rank per probe
+    __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
     __shared__ u32 s_bins[SORT && FSORT ? 4 : 1][SORT && FSORT ? 128 : 1];  // FSORT: 256 16-bit class counters
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
@@ -891,7 +815,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         key = h;
                         if constexpr (VERIFY) key &= P.fp_mask;
                         key = key ? key : 1ull;
-                        if constexpr (OWNP) {
+                        if constexpr (DIST) {
                             if constexpr (PRE) s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(key, d, pmx, hwn, B);
                             else  // no parent mixes: the successor's words 0 and 1 when it changes one
                                 s_own[b][threadIdx.x] = (uint8_t)(
@@ -1022,8 +946,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     if (is_new) {
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
                         l_rel[pos] = (SORT && FSORT) ? (u32)rel | ((u32)(cp >> (8 * b)) << 24)
-                                   : (MARK && !FOWN) ? (u32)rel | ((u32)s_own[OWNP ? b : 0][OWNP ? threadIdx.x : 0] << 24)
-                                   : (u32)rel;
+                                   : MARK ? (u32)rel | ((u32)s_own[DIST ? b : 0][threadIdx.x] << 24) : (u32)rel;
                         l_lane[pos] = (uint8_t)(SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b);
                         if constexpr (SENTC) {
                             l_dest[pos] = s_own[b][threadIdx.x];
@@ -1032,8 +955,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     }
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
-                        if constexpr (FOWN) flush_mark_own<S, K>(P, B, lo, l_rel, l_lane, n);
-                        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+                        if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
                         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
                         else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
@@ -1047,8 +969,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     }
     if (n) {
-        if constexpr (FOWN) flush_mark_own<S, K>(P, B, lo, l_rel, l_lane, n);
-        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+        if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
         else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
@@ -1075,11 +996,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
-template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false>
+template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT>(P, PT, B, lo,
+                                                                                                       hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1099,15 +1021,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K
 // The sharded expansion (owner routing, sent-cache, per-wave key lists).
 // WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
 // 4 waves/SIMD like k_expand_sort (uncapped it takes 131 VGPRs: 3 waves).
-template <int S, int K, int BATCH, bool WS, int WPE = 4, bool DIA = true, bool EARLY = true, bool MARK = false,
-          bool FOWN = false>
+template <int S, int K, int BATCH, bool WS, int WPE = 4, bool DIA = true, bool EARLY = true, bool MARK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? WPE : 1))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, DIA, DIA && EARLY, MARK, FOWN>(
-            P, PT, B, lo, hi);
-    else
-        expand_body<S, K, false, BATCH, true, false>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, DIA, DIA && EARLY, MARK>(P, PT, B,
+                                                                                                          lo, hi);
+    else  // more than 64 lanes: every lane of every state
+        expand_body<S, K, false, BATCH, true, false, false, false, false, false, true, false, false, MARK>(P, PT, B, lo,
+                                                                                                       hi);
 }
 
 #ifndef RMC_SHAPE_S  // non-template kernels: in the common object only
@@ -1616,12 +1538,20 @@ static int sym_variant() {
     return v;
 }
 
-// Sharded expansion variant (RMC_DIST_VARIANT): 1 (default) = the lane-superset
-// walk over class-sorted windows, 0 = every lane.
+// Sharded expansion variant (RMC_DIST_VARIANT; same-box A/B at one rank on
+// RCCL, profiles/r03/ab/dist_*): 7 (default) = send markers in the local set
+// (a lossless sent-cache; the probe loop is the single-GPU loop), no diamond
+// skipping: 329-333 ms per MCraftBench BFS against 311-316 ms unsharded;
+// 6 = markers with diamond skipping (341 ms: the owner routing and the
+// diamond together cost more registers than the probes they save); 4 = the
+// lossy sent-cache, no diamonds (342-346 ms); 1 = the sent-cache with
+// diamonds decided before hashing (round-3 start, 366 ms); 0 = every lane.
+// Measured and removed: 3 waves/SIMD, 6 probes in flight, the owner decided
+// in the flush (390 ms: a reservation atomic per 64 entries).
 static int dist_variant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_VARIANT");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 7;
     }();
     return v;
 }
@@ -1664,6 +1594,10 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                PT, B, a, b);
+        } else if (S == 3 && K == 4 && expand_variant() == 8) {  // A/B (bench shape): windows of 16 tiles
+            if constexpr (S == 3 && K == 4)
+                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3((unsigned)g), dim3(256),
+                                   0, st, P, PT, B, a, b);
         } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
@@ -1679,44 +1613,27 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     } else if (which == 3) {
         if constexpr (SYM)
             hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
-        else {
+        else if (dist_variant() == 7) {  // default: send markers, no diamond skipping
+            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>), dim3((unsigned)g), dim3(256),
+                               0, st, P, PT, B, a, b);
+        } else {
             bool ab = false;
-            if constexpr (S == 3 && K == 4) {  // A/B variants, bench shape only: 2 = 3 waves/SIMD (no
-                ab = true;  // spills), 3 = 6 probes in flight, 4 = no diamond skipping, 5 = diamonds, not EARLY,
-                            // 6 = 5 with send markers in the local set (flush_mark), 7 = 6 without diamonds,
-                            // 8 = 6 with the owner decided in the flush (flush_mark_own), 9 = 8 without diamonds
-                if (dist_variant() == 2)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 3>), dim3((unsigned)g), dim3(256), 0, st, P,
-                                       PT, B, a, b);
-                else if (dist_variant() == 3)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, 6, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
-                                       b);
-                else if (dist_variant() == 4)
+            if constexpr (S == 3 && K == 4) {  // A/B variants, bench shape only: 4 = sent-cache, no diamond
+                ab = true;                     // skipping; 6 = send markers with diamond skipping
+                if (dist_variant() == 4)
                     hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>), dim3((unsigned)g), dim3(256), 0,
                                        st, P, PT, B, a, b);
-                else if (dist_variant() == 5)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false>), dim3((unsigned)g), dim3(256),
-                                       0, st, P, PT, B, a, b);
                 else if (dist_variant() == 6)
                     hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>), dim3((unsigned)g),
-                                       dim3(256), 0, st, P, PT, B, a, b);
-                else if (dist_variant() == 7)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>), dim3((unsigned)g),
-                                       dim3(256), 0, st, P, PT, B, a, b);
-                else if (dist_variant() == 8)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true, true>), dim3((unsigned)g),
-                                       dim3(256), 0, st, P, PT, B, a, b);
-                else if (dist_variant() == 9)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true, true>), dim3((unsigned)g),
                                        dim3(256), 0, st, P, PT, B, a, b);
                 else
                     ab = false;
             }
             if (ab) {
-            } else if (dist_variant() == 1) {
+            } else if (dist_variant() == 1) {  // sent-cache, diamond skipping decided before hashing
                 hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
                                    b);
-            } else {
+            } else {  // 0: sent-cache, every lane
                 hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
                                    b);
             }
@@ -1785,6 +1702,11 @@ RMC_SHAPES(RMC_SHAPE_DECLS)
 #define RMC_DEFINE_SHAPE_(SS, KK) RMC_DEFINE_SHAPE(SS, KK)
 RMC_DEFINE_SHAPE_(RMC_SHAPE_S, RMC_SHAPE_K)
 #else
+bool dist_uses_sent_cache() {
+    const int v = dist_variant();
+    return !(v == 7 || (v == 6));  // markers live in the fingerprint set (variant 6: bench shape only)
+}
+
 hipError_t set_fp_salt(u64 seed, hipStream_t st) {
     const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
     hipError_t e = hipSuccess;
