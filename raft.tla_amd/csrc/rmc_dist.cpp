@@ -295,8 +295,9 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         u64 cursor = lo, ovf_known = 0, ovf_done = 0;
         const u64 frontier = hi - lo;
         // at least D.split rounds for a large level, so one round's exchange
-        // overlaps the next round's expansion
-        const u64 split_cap = frontier >= (1ull << 21) ? (frontier + D.split - 1) / (u64)D.split : frontier;
+        // overlaps the next round's expansion (one rank exchanges nothing)
+        const u64 split_cap =
+            (W > 1 && frontier >= (1ull << 21)) ? (frontier + D.split - 1) / (u64)D.split : frontier;
         u64 round_states[2] = {0, 0};  // states expanded by the round held in each set
         int round_kind[2] = {0, 0};    // 0 empty, 1 expansion, 2 drain
         // enqueue the expansion (or the drain of parked keys) of round k into set k & 1
@@ -412,6 +413,21 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             if (global_more && !next_queued) {
                 if (int rc = enqueue_A(k + 1)) return rc;
                 next_queued = true;
+            }
+            // nothing crosses this rank this round (always so at one rank): no
+            // phase 1 or 2 and no second read-back.  RCCL point-to-point groups
+            // pair ranks, so the others go on without this one; the host
+            // transport's all-to-all is a collective of every rank, so there
+            // only a world of one skips.
+            bool idle = !verify && (D.rccl || W == 1) && tot_in == 0;
+            for (int p = 0; p < W; ++p) idle = idle && scnt[(size_t)p] == 0;
+            if (idle) {
+                HIPCHK(c, hipEventRecord(S.ev_free, D.xs));
+                HIPCHK(c, hipEventRecord(S.x1, D.xs));
+                S.xtimed = 1;
+                D.chunks += 1;
+                if (!global_more) break;
+                continue;
             }
             // ---- phase 1: keys to their owners, replies back; phase 2 sizes
             HIPCHK(c, hipMemsetAsync(D.sa, 0, 16 * (u64)W, D.xs));
@@ -629,7 +645,11 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     const u64 RB = (u64)(c->NW + 4) * 4;
     D.sent_slots = slots;
     D.in_cap = W * kcap;
-    bool ok = hipStreamCreateWithFlags(&D.xs, hipStreamNonBlocking) == hipSuccess;
+    // the exchange stream at the highest priority: its kernels (owner insert,
+    // materialise, store, RCCL's) take CUs as soon as expansion blocks retire
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    bool ok = hipStreamCreateWithPriority(&D.xs, hipStreamNonBlocking, prio_hi) == hipSuccess;
     // full-state verification ships every remote successor: no sent-cache
     // (the default kernel keeps send markers in the fingerprint set instead)
     if (!c->sh.verify && (c->sh.sym || dist_uses_sent_cache())) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;

@@ -8,8 +8,10 @@ made on one GPU:
   per_rank.json  dist_worker output of that run (stored states per rank)
 
 Per level L, every rank r:
-  expand   t1[L] / N * imbalance * k_dist       (k_dist: sharded / unsharded
-                                                 kernel time at one rank)
+  expand   f + (t1[L] - f) * share[L, r] * k_dist  (share: the rank's states of
+                                                 the level; f: the fixed cost of a
+                                                 level, the smallest t1; k_dist:
+                                                 sharded / unsharded kernel time)
   insert   keys_in[L, r] * c_probe              (owner-side random probes)
   rounds   R[L] * (2 * a_sync + 4 * a_coll + 5 * a_launch)
   bytes    (8 + 1) B per key + RB per state, over min(N-1, 7) xGMI links
@@ -53,12 +55,16 @@ def main():
         keys_in[lvl][r] += tin
         states[lvl][r] += st
     pr = json.load(open(pr_path))
+    accept = pr["states_sent"] / max(1, pr["keys_sent"])  # phase-2 states per phase-1 key
     stored = [p["stored"] for p in pr["per_rank"]]
     imb = max(stored) / (sum(stored) / len(stored))
     RB = 56
+    # fixed per-level cost on one GPU: the smallest level time (a few thousand states)
+    f_level = min(t1.values())
     print(json.dumps({"levels": len(t1), "T1_s": total1, "sum_t1": sum(t1.values()), "rounds_total":
                       sum(len(v) for v in rounds.values()), "imbalance_stored": imb,
-                      "keys_in_total": sum(sum(v.values()) for v in keys_in.values())}))
+                      "keys_in_total": sum(sum(v.values()) for v in keys_in.values()),
+                      "accepted_per_key": accept, "f_level_us": f_level * 1e6}))
     for k_dist in (1.0, 1.06):
         for a_sync, a_coll, a_launch, a_level in ((10e-6, 15e-6, 5e-6, 40e-6), (20e-6, 30e-6, 8e-6, 80e-6),
                                                   (40e-6, 60e-6, 10e-6, 150e-6)):
@@ -70,12 +76,13 @@ def main():
                     R = max(1, len(rounds.get(L, ())))
                     per_rank = []
                     for r in range(n):
-                        # the expansion share of rank r: its states of this level (when logged) else 1/N
+                        # the expansion share of rank r: its states of this level (when logged) else 1/N;
+                        # a level's fixed cost (launch + read-back, f_level) does not shrink with N
                         st = states[L][r] if states[L] else None
                         share = (st / max(1, sum(states[L].values()))) if st is not None else 1.0 / n
-                        e = t * share * k_dist
+                        e = f_level + max(0.0, t - f_level) * share * k_dist
                         ins = keys_in[L][r] * c_probe
-                        byts = keys_in[L][r] * 9 + 0.25 * keys_in[L][r] * RB
+                        byts = keys_in[L][r] * 9 + accept * keys_in[L][r] * RB
                         x = byts / (link_bw * min(n - 1, 7))
                         per_rank.append((e, ins, x))
                     e, ins, x = max(per_rank, key=lambda v: sum(v))
