@@ -140,6 +140,12 @@ def host_cpu_info():
     except (OSError, ValueError):
         pass
     usable = min(allowed, quota) if quota else allowed
+    # the job's CPU share when the launcher states one (the GPU pool sets
+    # OMP_NUM_THREADS to the box's share of its host cores)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(share) if share.isdigit() and int(share) > 0 else None
+    if share:
+        usable = min(usable, share)
     model, phys = platform.processor() or "?", set()
     try:
         cur = {}
@@ -156,7 +162,8 @@ def host_cpu_info():
             phys.add((cur.get("physical id"), cur.get("core id")))
     except OSError:
         pass
-    return {"nproc": nproc, "affinity_cpus": allowed, "cgroup_quota_cpus": quota, "usable": usable,
+    return {"nproc": nproc, "affinity_cpus": allowed, "cgroup_quota_cpus": quota, "omp_num_threads": share,
+            "usable": usable,
             "physical_cores": len(phys) or None, "model": model}
 
 
@@ -358,10 +365,14 @@ def main(argv=None):
                                           "chunks": ld.chunks, "exchange_s": round(ld.exchange_seconds, 6),
                                           "kernel_s": round(ld.expand_kernel_seconds, 6)})
     per_step = dt / a.steps
-    # algorithmic bytes per run (DESIGN.md "Roofline"): one random 64-B granule
-    # per fingerprint probe + the new state written, read back as frontier,
-    # its 8-B parent pointer and 8-B fingerprint
-    b_alg = NP * 64 + D * (2 * W + 16)
+    # algorithmic bytes per run, SURVEY.md §8(d)'s per-unit figure:
+    # one random 64-B HBM granule per generated successor (the fingerprint-set
+    # probe/insert TLC's algorithm makes for it) + for every distinct state the
+    # state written, read back as frontier, its 8-B parent ref and 8-B fingerprint
+    b_alg = G * 64 + D * (2 * W + 16)
+    # what the kernel actually issues: stuttering, out-of-CONSTRAINT and
+    # commuting-diamond successors are never probed (NP probes, one 64-B granule each)
+    b_issued = NP * 64 + D * (2 * W + 16)
     ks = kern / a.steps
     nlaunch = max(1, launches // a.steps)
     achieved = b_alg / ks / 1e9 if ks > 0 else 0.0
@@ -402,7 +413,11 @@ def main(argv=None):
                       else "k_expand_dist (librmc's sharded expansion kernel)",
             "kernel_ms_per_step": ks * 1e3,
             "launches_per_step": nlaunch, "alg_bytes_per_launch": b_alg / nlaunch,
-            "alg_bytes_per_step": b_alg, "probes_per_step": NP,
+            "alg_bytes_per_step": b_alg, "alg_bytes_def": "G*64 + D*(2W+16) (SURVEY.md 8(d))",
+            "issued_bytes_per_step": b_issued,
+            "issued_frac": (b_issued / ks / 1e9 / HBM_PEAK_GBS) if ks > 0 else 0.0,
+            "traffic_frac": (traffic * nlaunch / ks / 1e9 / HBM_PEAK_GBS) if (traffic and ks > 0) else None,
+            "probes_per_step": NP,
             "probe_rate_per_s": NP / ks if ks > 0 else 0.0,
             "probe_ceiling_per_s": r_max,
             "frac_of_probe_ceiling": (NP / ks / r_max) if (ks > 0 and r_max) else None,

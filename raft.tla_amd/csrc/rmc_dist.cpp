@@ -645,11 +645,12 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     const u64 RB = (u64)(c->NW + 4) * 4;
     D.sent_slots = slots;
     D.in_cap = W * kcap;
-    // the exchange stream at the highest priority: its kernels (owner insert,
-    // materialise, store, RCCL's) take CUs as soon as expansion blocks retire
+    // (RMC_DIST_XPRIO=1: the exchange stream at the highest priority, A/B)
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    bool ok = hipStreamCreateWithPriority(&D.xs, hipStreamNonBlocking, prio_hi) == hipSuccess;
+    const char* xp = getenv("RMC_DIST_XPRIO");
+    bool ok = hipStreamCreateWithPriority(&D.xs, hipStreamNonBlocking, (xp && atoi(xp)) ? prio_hi : prio_lo) ==
+              hipSuccess;
     // full-state verification ships every remote successor: no sent-cache
     // (the default kernel keeps send markers in the fingerprint set instead)
     if (!c->sh.verify && (c->sh.sym || dist_uses_sent_cache())) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;

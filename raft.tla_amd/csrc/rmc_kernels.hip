@@ -1505,7 +1505,8 @@ static u64 expand_grid() {
 // Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
 // profiles/r02/ab/, profiles/r03/ab/): 6 (default) = commuting-diamond
 // skipping (7.18 G instead of 10.41 G probes per MCraftBench BFS: 315 vs
-// 337-340 ms) on the lane-superset walk over class-sorted windows;
+// 337-340 ms) on the lane-superset walk over class-sorted windows of 16 tiles
+// (308.2-309.3 vs 310.9-312.4 ms for 8 tiles, variant 8, same box);
 // 7 = 6 with the stutter, CONSTRAINT and commuting-diamond decisions taken
 // before the lane hashes (317-322 ms: the split costs more than the hashes
 // it saves); without the diamond, 6 is the round-2 kernel: the lane-superset walk over class-sorted
@@ -1594,13 +1595,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                PT, B, a, b);
-        } else if (S == 3 && K == 4 && expand_variant() == 8) {  // A/B (bench shape): windows of 16 tiles
-            if constexpr (S == 3 && K == 4)
-                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3((unsigned)g), dim3(256),
-                                   0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
+        } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {  // windows of 8 tiles (round-2 size)
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
                                B, a, b);
+        } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {  // default: windows of 16 tiles (4096 states)
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3((unsigned)g), dim3(256), 0,
+                               st, P, PT, B, a, b);
         } else {  // 1, and shapes with more than 64 lanes
             hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3((unsigned)g), dim3(256), 0, st,
                                P, PT, B, a, b);
