@@ -428,7 +428,9 @@ def main(argv=None):
         out["sharded"] = {"in_library": "rmc_shard + rmc_run_bfs (two-phase fingerprint-first exchange)",
                           "transport": transport, "chunks_rank0": ld.chunks, "keys_sent_rank0": ld.keys_sent,
                           "states_sent_rank0": ld.states_sent, "stored_rank0": ld.stored_here,
-                          "exchange_s_rank0": round(ld.exchange_seconds, 6), "keys_per_dest": a.keys_per_dest,
+                          "exchange_s_rank0": round(ld.exchange_seconds, 6),
+                          "host_wait_s_rank0": round(ld.exchange_wait_seconds, 6),
+                          "rounds_parked_keys_rank0": ld.parked, "keys_per_dest": a.keys_per_dest,
                           "per_rank": per_rank}
         out["roofline"]["note"] = ("per-rank kernel time of rank 0; achieved = the job's algorithmic bytes / "
                                    "world / rank 0's kernel time")

@@ -294,10 +294,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         lvl_now = depth;
         u64 cursor = lo, ovf_known = 0, ovf_done = 0;
         const u64 frontier = hi - lo;
-        // at least D.split rounds for a large level, so one round's exchange
-        // overlaps the next round's expansion (one rank exchanges nothing)
-        const u64 split_cap =
-            (W > 1 && frontier >= (1ull << 21)) ? (frontier + D.split - 1) / (u64)D.split : frontier;
+        // at least D.split rounds for a large level, so one round's count
+        // exchange and read-back overlap the next round's expansion (at one
+        // rank too: without the split the one-rank bench loses 8 ms to them)
+        const u64 split_cap = frontier >= (1ull << 21) ? (frontier + D.split - 1) / (u64)D.split : frontier;
         u64 round_states[2] = {0, 0};  // states expanded by the round held in each set
         int round_kind[2] = {0, 0};    // 0 empty, 1 expansion, 2 drain
         // enqueue the expansion (or the drain of parked keys) of round k into set k & 1
