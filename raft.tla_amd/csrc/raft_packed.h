@@ -123,6 +123,8 @@ struct Params {
                     // capacity, and a successor beyond it is an error (capacity_exceeded), not filtered
     u64 fp_mask;  // full-state verification mode: fingerprint bits kept (~0 = all; fewer only
                   // to provoke collisions in tests, rmc_set_fp_bits)
+    u32 ldesc[64];  // per-lane descriptor for lanes < 64 (lane_desc): family | index in family << 4 |
+                    // acting server << 12 (7: none or per message); filled by fill_lane_desc
 };
 
 // Lane table: Restart S, Timeout S, RequestVote S^2,
@@ -272,30 +274,30 @@ RMC_HD void receive_lane(const u64 (&w)[S], u32 msg, int k, Delta& d) {
     }
 }
 
-// Compute the delta of lane `lane` (0 <= lane < Lanes<S,K>::N) on parent (w, m).
+// The delta of action instance (family fam, index t in the family; i, j its
+// servers: RequestVote / AppendEntries (i, j) = (t / S, t % S), ClientRequest
+// (i, v) = (t / VMAX, t % VMAX), the other server actions i = t) on parent (w, m).
+// fam is a runtime value (a kernel argument or a per-lane descriptor), so the
+// family dispatch stays a branch tree: as compile-time constants the compiler
+// if-converts every family into straight-line selects and the kernel needs 4x
+// the registers.
 template <int S, int K>
-RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Params& P, Delta& d) {
-    // Offsets read from the kernel argument (equal to Lanes<S,K>::off): as
-    // opaque runtime values they keep the family dispatch a branch tree; as
-    // compile-time constants the compiler if-converts every family into
-    // straight-line selects and the kernel needs 4x the registers.
-    struct {
-        const int* o;
-        RMC_HD int off(int f) const { return o[f]; }
-    } L{P.off};
+RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, int i, int j, const Params& P,
+                         Delta& d) {
     d.srv = -1;
     d.rm = -1;
     d.has_add = 0;
     d.add = 0;
     d.en = 0;
     d.w_new = 0;
-    if (lane < L.off(1)) {  // Restart(i) :136-143
-        const int i = lane;
+    switch (fam) {
+    case 0: {  // Restart(i) :136-143
         d.srv = i;
         d.w_new = selw<S>(w, i) & RESTART_KEEP;
         d.en = 1;
-    } else if (lane < L.off(2)) {  // Timeout(i) :146-154
-        const int i = lane - L.off(1);
+        break;
+    }
+    case 1: {  // Timeout(i) :146-154
         const u64 wi = selw<S>(w, i);
         const u32 st = w_st(wi);
         if (st == FOLLOWER || st == CANDIDATE) {
@@ -308,16 +310,18 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.w_new = wn;
             d.en = 1;
         }
-    } else if (lane < L.off(3)) {  // RequestVote(i, j) :157-166 (no i /= j guard)
-        const int t = lane - L.off(2), i = t / S, j = t % S;
+        break;
+    }
+    case 2: {  // RequestVote(i, j) :157-166 (no i /= j guard)
         const u64 wi = selw<S>(w, i);
         if (w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u)) {
             d.add = m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16);
             d.has_add = 1;
             d.en = 1;
         }
-    } else if (lane < L.off(4)) {  // BecomeLeader(i) :195-203
-        const int i = lane - L.off(3);
+        break;
+    }
+    case 3: {  // BecomeLeader(i) :195-203
         const u64 wi = selw<S>(w, i);
         const u32 vg = w_vg<S>(wi);
         const bool ok = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
@@ -333,22 +337,24 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.w_new = wn;
             d.en = 1;
         }
-    } else if (lane < L.off(5)) {  // ClientRequest(i, v) :206-213
-        const int t = lane - L.off(4), i = t / VMAX, v = t % VMAX;
+        break;
+    }
+    case 4: {  // ClientRequest(i, v) :206-213 (v = j)
         const u64 wi = selw<S>(w, i);
-        if (v < P.V && w_st(wi) == LEADER) {
+        if (j < P.V && w_st(wi) == LEADER) {
             const u32 len = w_len(wi);
             if (len >= (u32)LOG_CAP) {
                 d.w_new = wi | (1ull << 63);  // Len = 4: out of every allowed constraint
             } else {
-                u64 wn = setbits(wi, LOG_SH + ENT_W * (int)len, ENT_W, w_ct(wi) | ((u32)v << 4));
+                u64 wn = setbits(wi, LOG_SH + ENT_W * (int)len, ENT_W, w_ct(wi) | ((u32)j << 4));
                 d.w_new = setbits(wn, LEN_SH, 2, len + 1);
             }
             d.srv = i;
             d.en = 1;
         }
-    } else if (lane < L.off(6)) {  // AdvanceCommitIndex(i) :219-236
-        const int i = lane - L.off(5);
+        break;
+    }
+    case 5: {  // AdvanceCommitIndex(i) :219-236
         const u64 wi = selw<S>(w, i);
         if (w_st(wi) == LEADER) {
             const u32 len = w_len(wi);
@@ -365,8 +371,9 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.w_new = wn;
             d.en = 1;
         }
-    } else if (lane < L.off(7)) {  // AppendEntries(i, j) :171-192
-        const int t = lane - L.off(6), i = t / S, j = t % S;
+        break;
+    }
+    case 6: {  // AppendEntries(i, j) :171-192
         const u64 wi = selw<S>(w, i);
         if (i != j && w_st(wi) == LEADER) {
             const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
@@ -381,26 +388,54 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
             d.has_add = 1;
             d.en = 1;
         }
-    } else if (lane < L.off(8)) {  // Receive(m) :388-403
-        const int k = lane - L.off(7);
-        const u32 sl = selm<K>(m, k);
-        if (sl) receive_lane<S, K>(w, sl & MSG_MASK, k, d);
-    } else if (lane < L.off(9)) {  // DuplicateMessage(m) :410-412
-        const int k = lane - L.off(8);
-        const u32 sl = selm<K>(m, k);
+        break;
+    }
+    case 7: {  // Receive(m) :388-403
+        const u32 sl = selm<K>(m, t);
+        if (sl) receive_lane<S, K>(w, sl & MSG_MASK, t, d);
+        break;
+    }
+    case 8: {  // DuplicateMessage(m) :410-412
+        const u32 sl = selm<K>(m, t);
         if (sl) {
             d.add = sl & MSG_MASK;
             d.has_add = 1;
             d.en = 1;
         }
-    } else {  // DropMessage(m) :415-417
-        const int k = lane - L.off(9);
-        const u32 sl = selm<K>(m, k);
+        break;
+    }
+    default: {  // DropMessage(m) :415-417
+        const u32 sl = selm<K>(m, t);
         if (sl) {
-            d.rm = k;
+            d.rm = t;
             d.en = 1;
         }
+        break;
     }
+    }
+}
+
+// Compute the delta of lane `lane` (0 <= lane < Lanes<S,K>::N) on parent (w, m).
+template <int S, int K>
+RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Params& P, Delta& d) {
+    // offsets read from the kernel argument (equal to Lanes<S,K>::off): a branch tree
+    int fam = 0;
+#pragma unroll
+    for (int k = 1; k <= 9; ++k) fam += lane >= P.off[k] ? 1 : 0;
+    int o = 0;
+#pragma unroll
+    for (int k = 0; k <= 9; ++k) o = fam == k ? P.off[k] : o;
+    const int t = lane - o;
+    const int i = (fam == 2 || fam == 6) ? t / S : fam == 4 ? t / VMAX : t;
+    const int j = (fam == 2 || fam == 6) ? t % S : fam == 4 ? t % VMAX : 0;
+    lane_delta_f<S, K>(w, m, fam, t, i, j, P, d);
+}
+
+// The same from a lane descriptor (Params.ldesc, lanes < 64: lane_desc).
+template <int S, int K>
+RMC_HD void lane_delta_desc(const u64 (&w)[S], const u32 (&m)[K], u32 desc, const Params& P, Delta& d) {
+    const int fam = (int)(desc & 15u), t = (int)((desc >> 4) & 255u);
+    lane_delta_f<S, K>(w, m, fam, t, (int)((desc >> 16) & 15u), (int)((desc >> 20) & 15u), P, d);
 }
 
 // Apply a delta: fingerprint and CONSTRAINT (parent assumed in-constraint).
@@ -799,6 +834,23 @@ RMC_HD int count_of(const u32 (&m)[K], u32 msg) {
     return (int)c;
 }
 
+// Per-lane descriptor (Params.ldesc): the family, the index inside it and the
+// server whose word the lane's action writes (7: none, or the message's mdest
+// for Receive) — what diamond_skip needs of lane b, read with one scalar load
+// instead of recomputed from the family offsets in every lane of every state.
+// Bits: family 0-3, index in the family 4-11, acting server 12-14 (7: none or
+// per message), lane_delta_f's i 16-19 and j 20-23.
+RMC_HD u32 lane_desc(const Params& P, int lane, int S) {
+    const int f = lane_family(P, lane), t = lane - family_off(P, f);
+    const int srv = (f == 0 || f == 1 || f == 3 || f == 5) ? t : (f == 2 || f == 6) ? t / S : f == 4 ? t / VMAX : 7;
+    const int i = (f == 2 || f == 6) ? t / S : f == 4 ? t / VMAX : t;
+    const int j = (f == 2 || f == 6) ? t % S : f == 4 ? t % VMAX : 0;
+    return (u32)f | ((u32)t << 4) | ((u32)srv << 12) | ((u32)(i & 15) << 16) | ((u32)(j & 15) << 20);
+}
+RMC_HD void fill_lane_desc(Params& P, int S) {
+    for (int l = 0; l < 64; ++l) P.ldesc[l] = l < P.off[10] ? lane_desc(P, l, S) : 0u;
+}
+
 // Per expanded state: a's side of the test (lane a = act, its footprint).
 struct Diamond {
     u64 ord;   // a's instance order key; 0 = no skipping from this state
@@ -824,6 +876,19 @@ RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diam
     if ((foot & FOOT_ADD) && count_of<K>(m, madd) == 1) delta += 1;       // a created the key
     if ((foot & FOOT_CONSUMED) && count_of<K>(m, mact) == 0) delta -= 1;  // a removed its last copy
     dm.dom = P.max_msgs + delta;
+}
+// b's side from lane b's descriptor (lanes < 64): the same test as diamond_skip.
+template <int S, int K>
+RMC_HD bool diamond_skip_desc(const u32 (&m)[K], int b, u32 desc, const Delta& db, int nmsg_b, const Diamond& dm) {
+    const int fb = (int)(desc & 15u), tb = (int)((desc >> 4) & 255u), sd = (int)((desc >> 12) & 7u);
+    const u32 mb = fb >= 7 ? (selm<K>(m, tb) & MSG_MASK) : 0xFFFFFFFDu;
+    const u64 ob = ((u64)fb << 40) | (fb < 7 ? (u64)b : (u64)mb) | (1ull << 48);
+    if (!(ob < dm.ord)) return false;  // dm.ord = 0: never
+    const int sb = sd < 7 ? sd : fb == 7 ? (int)m_dst(mb) : -1;
+    if (sb >= 0 && sb == dm.srv) return false;
+    const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
+    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
+    return nmsg_b <= dm.dom;
 }
 // b's side: lane b with delta db on t (m = t's bag), nmsg_b = |DOMAIN| of b(t).
 template <int S, int K>

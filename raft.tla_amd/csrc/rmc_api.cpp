@@ -78,6 +78,7 @@ void fill_params(rmc_ctx* c) {
     const int sizes[10] = {S, S, S * S, S, S * VMAX, S, S * S, K, K, K};  // = Lanes<S,K>
     P.off[0] = 0;
     for (int f = 0; f < 10; ++f) P.off[f + 1] = P.off[f] + sizes[f];
+    fill_lane_desc(P, S);
     // permutations of 0..S-1 in lexicographic order (identity first), 3 bits per id
     memset(&c->PT, 0, sizeof c->PT);
     {

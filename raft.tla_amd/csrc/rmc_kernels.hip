@@ -771,7 +771,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 int tied = 0;  // SYMMETRY: signatures tie, deferred to k_ties
                 if (lane < nl) {
                     Delta d;
-                    lane_delta<S, K>(w, m, lane, P, d);
+                    if constexpr (SORT) lane_delta_desc<S, K>(w, m, P.ldesc[SORT ? lane : 0], P, d);  // scalar descriptor
+                    else lane_delta<S, K>(w, m, lane, P, d);
                     const int en = d.en && live;
                     g += (u32)en;
                     u64 h = 0;
@@ -797,7 +798,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         if constexpr (EARLY) {
                             const bool stutter = d.rm < 0 && !d.has_add && (d.srv < 0 || d.w_new == selw<S>(w, d.srv));
                             in_model = !stutter && delta_bounds_pre<S, K>(m, pmx, d, P, &nmb) &&
-                                       !diamond_skip<S, K>(m, lane, d, nmb, dm, P);
+                                       !(SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d, nmb, dm)
+                                              : diamond_skip<S, K>(m, lane, d, nmb, dm, P));
                             h = in_model ? delta_hash_pre<S, K>(w, m, pmx, d, DIST ? &hwn : nullptr) : h0;
                         } else {
                             if constexpr (PRE)
@@ -805,7 +807,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                                                               DIST ? &hwn : nullptr);
                             else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
                             if constexpr (DIA)
-                                if (in_model && h != h0 && diamond_skip<S, K>(m, lane, d, nmb, dm, P)) in_model = 0;
+                                if (in_model && h != h0 &&
+                                    (SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d, nmb, dm)
+                                          : diamond_skip<S, K>(m, lane, d, nmb, dm, P)))
+                                    in_model = 0;
                         }
                         if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
                     }
@@ -1009,11 +1014,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE :
 // (deferred to k_ties).  INC: keys from the parent's frame (canon_delta_inc);
 // otherwise every lane hashes its whole permuted successor (canon_delta).
 // WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
-template <int S, int K, int BATCH, bool INC, int WPE = 5, bool WS = false>
+template <int S, int K, int BATCH, bool INC, int WPE = 5, bool WS = false, int WT = 8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? WPE : 1))) void k_expand_sym(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, true, BATCH, false, false, false, INC, true, true, false>(P, PT, B, lo, hi);
+        expand_body<S, K, true, BATCH, false, false, false, INC, true, true, false, false, false, false, WT>(P, PT, B, lo,
+                                                                                                          hi);
     else
         expand_body<S, K, true, BATCH, false, false, false, INC>(P, PT, B, lo, hi);
 }
@@ -1584,6 +1590,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             else if (sym_variant() == 4)
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
+            else if (S == 3 && K == 4 && sym_variant() == 5) {  // A/B (bench shape): windows of 16 tiles
+                if constexpr (S == 3 && K == 4)
+                    hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true, 16>), dim3((unsigned)g), dim3(256), 0,
+                                       st, P, PT, B, a, b);
+            }
             else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);

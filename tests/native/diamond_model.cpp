@@ -164,6 +164,8 @@ struct Model {
                         u64 h2 = 0;
                         delta_fp<S, K>(w, m, h0, d, P, &h2, &nmb);
                         if (diamond_skip<S, K>(m, lane, d, nmb, dm, P) != sk) ++o.mismatch;
+                        // the lane-descriptor form the sorted kernels use decides the same
+                        if (lane < 64 && diamond_skip_desc<S, K>(m, lane, P.ldesc[lane], d, nmb, dm) != sk) ++o.mismatch;
                     }
                     if (sk) {
                         ++o.skipped;
@@ -203,6 +205,7 @@ int run(int V, int mt, int ml, int mm, int md, int levels, u64 cap) {
     Model<S, K> X;
     X.P.V = V; X.P.max_term = mt; X.P.max_log = ml; X.P.max_msgs = mm; X.P.max_dup = md; X.P.diamond = 1;
     for (int f = 0; f <= 10; ++f) X.P.off[f] = Lanes<S, K>::off(f);
+    fill_lane_desc(X.P, S);
     auto a = X.bfs(levels, false, cap);
     auto b = X.bfs(levels, true, cap);
     u64 da = 0, db = 0;
