@@ -511,41 +511,39 @@ RMC_HD u64 sel64(const u64 (&a)[N], int i) {
 template <int S, int K>
 RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
                         const Params& P, u64* h, int* nmsg_out = nullptr, u64* hw_new = nullptr) {
-    u64 hh = pm.h0;
-    int nmsg = pm.nmsg;
-    if (d.srv >= 0) {
-        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
-        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
-        const u64 wo = selw<S>(w, d.srv);
-        const u64 ho = sel64<S>(pm.hw, d.srv);
-        const u64 hn = d.w_new != wo ? hS(d.w_new, (u32)d.srv) : ho;
-        hh += hn - ho;
-        if (hw_new) *hw_new = hn;  // the new word's mix (the sharded owner reuses it)
-    }
-    if (d.rm >= 0) {
-        const u32 sl = selm<K>(m, d.rm);
-        hh -= sel64<K>(pm.hm, d.rm);
-        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
-        else nmsg -= 1;
-    }
-    if (d.has_add) {
-        int found = -1;
+    // Branch-light: the bounds are predicates and selects; only the three
+    // mixes (new server word, decremented slot, added / incremented slot) sit
+    // under a branch, so a wave skips a mix no lane of it needs.  (Every early
+    // return of a per-lane condition costs the wave an exec-mask save, test
+    // and restore in scalar instructions.)
+    const bool has_s = d.srv >= 0, has_r = d.rm >= 0, has_a = d.has_add != 0;
+    bool ok = !has_s || ((d.w_new >> 63) == 0 &&  // term 16 or Len 4: beyond every bound
+                         (int)w_ct(d.w_new) <= P.max_term && (int)w_len(d.w_new) <= P.max_log);
+    const u64 wo = selw<S>(w, d.srv), ho = sel64<S>(pm.hw, d.srv);
+    u64 hn = ho;
+    if (ok && has_s && d.w_new != wo) hn = hS(d.w_new, (u32)d.srv);
+    if (hw_new) *hw_new = hn;  // the new word's mix (the sharded owner reuses it)
+    u64 hh = pm.h0 + (hn - ho);
+    const u32 slr = selm<K>(m, d.rm);
+    const bool dec = has_r && m_cnt(slr) > 1;  // the removed message keeps a copy
+    u64 hr = 0;
+    if (ok && dec) hr = hM(slr - CNT_ONE);
+    hh += has_r ? hr - sel64<K>(pm.hm, d.rm) : 0ull;
+    int nmsg = pm.nmsg - ((has_r && !dec) ? 1 : 0);
+    int found = -1;
 #pragma unroll
-        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
-        if (found >= 0) {
-            const u32 sl = selm<K>(m, found);
-            if ((int)m_cnt(sl) + 1 > P.max_dup) return 0;
-            hh += hM(sl + CNT_ONE) - sel64<K>(pm.hm, found);
-        } else {
-            if (1 > P.max_dup) return 0;
-            nmsg += 1;
-            hh += hM(d.add | CNT_ONE);
-        }
-    }
-    if (nmsg > P.max_msgs) return 0;
+    for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+    const bool inc = has_a && found >= 0;  // the added message is already in the bag
+    const u32 sla = selm<K>(m, found);
+    ok = ok && (!has_a || (inc ? (int)m_cnt(sla) + 1 <= P.max_dup : 1 <= P.max_dup));
+    nmsg += (has_a && !inc) ? 1 : 0;
+    ok = ok && nmsg <= P.max_msgs;
+    u64 ha = 0;
+    if (ok && has_a) ha = hM(inc ? sla + CNT_ONE : (d.add | CNT_ONE));
+    hh += has_a ? ha - (inc ? sel64<K>(pm.hm, found) : 0ull) : 0ull;
     *h = hh;
     if (nmsg_out) *nmsg_out = nmsg;
-    return 1;
+    return ok ? 1 : 0;
 }
 
 // delta_fp_pre split in two, so a lane can decide to skip its probe before it
@@ -880,15 +878,14 @@ RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diam
 // b's side from lane b's descriptor (lanes < 64): the same test as diamond_skip.
 template <int S, int K>
 RMC_HD bool diamond_skip_desc(const u32 (&m)[K], int b, u32 desc, const Delta& db, int nmsg_b, const Diamond& dm) {
+    // one predicate, no early returns (see delta_fp_pre on branches)
     const int fb = (int)(desc & 15u), tb = (int)((desc >> 4) & 255u), sd = (int)((desc >> 12) & 7u);
     const u32 mb = fb >= 7 ? (selm<K>(m, tb) & MSG_MASK) : 0xFFFFFFFDu;
     const u64 ob = ((u64)fb << 40) | (fb < 7 ? (u64)b : (u64)mb) | (1ull << 48);
-    if (!(ob < dm.ord)) return false;  // dm.ord = 0: never
     const int sb = sd < 7 ? sd : fb == 7 ? (int)m_dst(mb) : -1;
-    if (sb >= 0 && sb == dm.srv) return false;
     const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
-    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
-    return nmsg_b <= dm.dom;
+    return (ob < dm.ord) & !(sb >= 0 && sb == dm.srv) & (mb != dm.k0) & (mb != dm.k1) & (kb1 != dm.k0) &
+           (kb1 != dm.k1) & (nmsg_b <= dm.dom);
 }
 // b's side: lane b with delta db on t (m = t's bag), nmsg_b = |DOMAIN| of b(t).
 template <int S, int K>

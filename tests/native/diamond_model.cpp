@@ -148,12 +148,29 @@ struct Model {
                 for (int i = 0; i < S; ++i) w[i] = W[t * S + i];
                 for (int q = 0; q < K; ++q) m[q] = M[t * K + q];
                 const u64 h0 = state_fp<S, K>(w, m);
+                ParentMix<S, K> pm;
+                parent_mix<S, K>(w, m, pm);
                 for (int lane = 0; lane < nl; ++lane) {
                     Delta d;
                     lane_delta<S, K>(w, m, lane, P, d);
+                    if (lane < 64) {  // the descriptor path of the sorted kernels gives the same delta
+                        Delta dd;
+                        lane_delta_desc<S, K>(w, m, P.ldesc[lane], P, dd);
+                        if (dd.en != d.en || dd.srv != d.srv || dd.rm != d.rm || dd.has_add != d.has_add ||
+                            (d.en && (dd.w_new != d.w_new || dd.add != d.add)))
+                            ++o.mismatch;
+                    }
                     if (!d.en) continue;
                     ++o.generated;
                     u64 h = 0;
+                    {  // the kernels' precomputed-mix form decides and hashes the same
+                        u64 hp = 0;
+                        int np = 0, nf = 0;
+                        u64 hf = 0;
+                        const int a1 = delta_fp<S, K>(w, m, h0, d, P, &hf, &nf);
+                        const int a2 = delta_fp_pre<S, K>(w, m, pm, d, P, &hp, &np);
+                        if (a1 != a2 || (a1 && (hf != hp || nf != np))) ++o.mismatch;
+                    }
                     if (!delta_fp<S, K>(w, m, h0, d, P, &h)) continue;
                     if (h == h0) continue;  // stutter
                     const bool sk = skippable(t, m, lane, d);
