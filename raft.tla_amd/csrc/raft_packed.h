@@ -171,9 +171,73 @@ RMC_HD u32 selm(const u32 (&m)[K], int i) {
     return r;
 }
 
-// Receive(m) raft.tla:388-403 for bag slot k (message `msg`).
+// Receive(m) raft.tla:388-403 for bag slot k (message `msg`), branch-light:
+// every case of the receive tree is a predicate and its effect a select, so a
+// wave whose lanes hold messages of different types and outcomes runs one
+// straight-line block instead of a tree of exec-masked branches (their
+// scalar bookkeeping cost as much issue as the vector work).  Indices into
+// the log are clamped so that the reads of cases not taken stay defined.
 template <int S, int K>
 RMC_HD void receive_lane(const u64 (&w)[S], u32 msg, int k, Delta& d) {
+    const u32 i = m_dst(msg), j = m_src(msg), mterm = m_term(msg), mt = m_type(msg);
+    const u64 wi = selw<S>(w, (int)i);
+    const u32 ct = w_ct(wi), st = w_st(wi), len = w_len(wi);
+    const bool up = mterm > ct, lt = mterm < ct;  // UpdateTerm :373-379 (m stays); stale
+    const bool rvq = !up && mt == RVQ, rvp = !up && mt == RVP, aeq = !up && mt == AEQ, aep = !up && mt == AEP;
+    // HandleRequestVoteRequest :244-263 (mterm <= ct here)
+    const u32 mlt = (msg >> 12) & 15u, mli = (msg >> 16) & 3u, lterm = w_last_term(wi), vf = w_vf(wi);
+    const bool grant = mterm == ct && (mlt > lterm || (mlt == lterm && mli >= len)) && (vf == NILV || vf == j);
+    // HandleAppendEntriesRequest :347-356; pe = mprevLogIndex + 1 (mprevLogIndex = -1,
+    // Smokeraft.tla:35, fails both disjuncts of logOk)
+    const u32 pe = (msg >> 12) & 7u, pterm = (msg >> 15) & 15u;
+    const u32 nent = (msg >> 19) & 1u, ent = (msg >> 20) & 31u, mci = (msg >> 25) & 3u;
+    const u32 pidx = pe - 1u;
+    const u32 e_prev = (pe >= 2u && pe - 2u < (u32)LOG_CAP) ? pe - 2u : 0u;  // log[mprevLogIndex], 0-based
+    const u32 e_idx = (pe >= 1u && pe - 1u < (u32)LOG_CAP) ? pe - 1u : 0u;   // log[index], index = pe
+    const bool log_ok = pe == 1u || (pe > 1u && pidx <= len && pterm == ent_term(w_ent(wi, e_prev)));
+    const bool reject = aeq && (lt || (st == FOLLOWER && !log_ok));          // :281-293
+    const bool ret = aeq && !reject && st == CANDIDATE;                      // ReturnToFollowerState :295-299
+    const bool fol = aeq && !reject && st == FOLLOWER;                       // (a Leader: no branch)
+    const bool term_eq = len >= pe && ent_term(w_ent(wi, e_idx)) == ent_term(ent);
+    const bool done = fol && (nent == 0u || term_eq);
+    // AppendEntriesAlreadyDone :301-317: UNCHANGED logVars after commitIndex' =
+    // m.mcommitIndex is a TLC equality test, enabled only when they are equal
+    const bool done_en = done && mci == w_ci(wi);
+    const bool confl = fol && !done && len >= pe;               // ConflictAppendEntriesRequest :319-325
+    const bool noconf = fol && !done && !confl && len == pidx;  // NoConflictAppendEntriesRequest :327-331
+    // the words of the cases that change one
+    const u64 wn_up = setbits(setbits(setbits(wi, CT_SH, 4, mterm), ST_SH, 2, FOLLOWER), VF_SH, 3, NILV);
+    const u64 wn_rvq = grant ? setbits(wi, VF_SH, 3, j) : wi;
+    const u64 wn_rvp = lt ? wi  // DropStaleResponse :382-385; else HandleRequestVoteResponse :267-279
+                          : wi | (1ull << (SL<S>::VR + (int)j)) | ((u64)((msg >> 12) & 1u) << (SL<S>::VG + (int)j));
+    const u64 wn_ret = setbits(wi, ST_SH, 2, FOLLOWER);
+    const u32 lm1 = len ? len - 1u : 0u;  // Conflict: drop the LAST entry (len >= pe >= 1), m stays
+    const u64 wn_confl = setbits(setbits(wi, LOG_SH + ENT_W * (int)lm1, ENT_W, 0), LEN_SH, 2, lm1);
+    const u32 lc = len < (u32)LOG_CAP ? len : (u32)LOG_CAP - 1u;  // NoConflict appends (Len = 4: out of every bound)
+    const u64 wn_noconf = len >= (u32)LOG_CAP ? (setbits(wi, LEN_SH, 2, 3) | (1ull << 63))
+                                              : setbits(setbits(wi, LOG_SH + ENT_W * (int)lc, ENT_W, ent), LEN_SH, 2, len + 1u);
+    const u32 mm = (msg >> 13) & 3u, nis = bits(wi, SL<S>::NI + 2 * (int)j, 2);  // HandleAppendEntriesResponse :360-370
+    const u64 wn_aep = lt ? wi
+                     : ((msg >> 12) & 1u) ? setbits(setbits(wi, SL<S>::NI + 2 * (int)j, 2, mm), SL<S>::MI + 2 * (int)j, 2, mm)
+                                          : setbits(wi, SL<S>::NI + 2 * (int)j, 2, nis ? nis - 1u : 0u);  // Max({ni-1, 1})
+    d.srv = (int)i;
+    d.w_new = up ? wn_up : rvq ? wn_rvq : rvp ? wn_rvp : ret ? wn_ret : confl ? wn_confl : noconf ? wn_noconf
+            : aep ? wn_aep : wi;
+    // Reply :102-103: an RVResp carries mlog = log[i] (len + entries bits); AEResp
+    // FALSE / 0 on reject, TRUE / mprevLogIndex + Len(entries) when already done
+    const u32 hdr = rvq ? m_hdr(RVP, i, j, ct) : m_hdr(AEP, i, j, ct);
+    d.has_add = (rvq || reject || done_en) ? 1 : 0;
+    d.add = !d.has_add ? 0u
+          : rvq ? hdr | ((grant ? 1u : 0u) << 12) | (bits(wi, LEN_SH, 17) << 13)
+          : done_en ? hdr | (1u << 12) | ((pidx + nent) << 13) : hdr;
+    d.rm = (rvq || rvp || reject || done_en || aep) ? k : -1;
+    d.en = (up || rvq || rvp || reject || ret || done_en || confl || noconf || aep) ? 1 : 0;
+}
+
+// Receive(m) as a decision tree (the round-2 form; the host model checks
+// receive_lane against it on every Receive lane).
+template <int S, int K>
+RMC_HD void receive_lane_branchy(const u64 (&w)[S], u32 msg, int k, Delta& d) {
     const u32 i = m_dst(msg), j = m_src(msg), mterm = m_term(msg), mt = m_type(msg);
     const u64 wi = selw<S>(w, (int)i);
     const u32 ct = w_ct(wi), st = w_st(wi), len = w_len(wi);
