@@ -354,6 +354,10 @@ RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, i
     d.add = 0;
     d.en = 0;
     d.w_new = 0;
+    // fam is wave-uniform in the kernels (scalar branches); the enabling
+    // conditions inside a family are per state, so they are predicates and
+    // selects rather than branches (each divergent branch costs the wave an
+    // exec-mask save, test and restore)
     switch (fam) {
     case 0: {  // Restart(i) :136-143
         d.srv = i;
@@ -364,94 +368,89 @@ RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, i
     case 1: {  // Timeout(i) :146-154
         const u64 wi = selw<S>(w, i);
         const u32 st = w_st(wi);
-        if (st == FOLLOWER || st == CANDIDATE) {
-            const u32 ct1 = w_ct(wi) + 1;
-            u64 wn = setbits(wi, ST_SH, 2, CANDIDATE);
-            wn = setbits(wn, VF_SH, 3, NILV);
-            wn &= ~(((u64)SL<S>::SMASK << SL<S>::VR) | ((u64)SL<S>::SMASK << SL<S>::VG));
-            wn = setbits(wn, CT_SH, 4, ct1 & 15u) | ((u64)(ct1 >> 4) << 63);  // bit 63: term overflow
-            d.srv = i;
-            d.w_new = wn;
-            d.en = 1;
-        }
+        const bool ok = st == FOLLOWER || st == CANDIDATE;
+        const u32 ct1 = w_ct(wi) + 1;
+        u64 wn = setbits(wi, ST_SH, 2, CANDIDATE);
+        wn = setbits(wn, VF_SH, 3, NILV);
+        wn &= ~(((u64)SL<S>::SMASK << SL<S>::VR) | ((u64)SL<S>::SMASK << SL<S>::VG));
+        wn = setbits(wn, CT_SH, 4, ct1 & 15u) | ((u64)(ct1 >> 4) << 63);  // bit 63: term overflow
+        d.srv = ok ? i : -1;
+        d.w_new = ok ? wn : 0ull;
+        d.en = ok ? 1 : 0;
         break;
     }
     case 2: {  // RequestVote(i, j) :157-166 (no i /= j guard)
         const u64 wi = selw<S>(w, i);
-        if (w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u)) {
-            d.add = m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16);
-            d.has_add = 1;
-            d.en = 1;
-        }
+        const bool ok = w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u);
+        d.add = ok ? m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16) : 0u;
+        d.has_add = ok ? 1 : 0;
+        d.en = ok ? 1 : 0;
         break;
     }
     case 3: {  // BecomeLeader(i) :195-203
         const u64 wi = selw<S>(w, i);
         const u32 vg = w_vg<S>(wi);
-        const bool ok = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
-        if (w_st(wi) == CANDIDATE && ok) {
-            u64 wn = setbits(wi, ST_SH, 2, LEADER);
-            const u64 lenv = w_len(wi);  // nextIndex = Len + 1, stored minus one
-            u64 ni = 0;
+        const bool quorum = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
+        const bool ok = w_st(wi) == CANDIDATE && quorum;
+        u64 wn = setbits(wi, ST_SH, 2, LEADER);
+        const u64 lenv = w_len(wi);  // nextIndex = Len + 1, stored minus one
+        u64 ni = 0;
 #pragma unroll
-            for (int q = 0; q < S; ++q) ni |= lenv << (2 * q);
-            wn = setbits(wn, SL<S>::NI, 2 * S, ni);
-            wn = setbits(wn, SL<S>::MI, 2 * S, 0);
-            d.srv = i;
-            d.w_new = wn;
-            d.en = 1;
-        }
+        for (int q = 0; q < S; ++q) ni |= lenv << (2 * q);
+        wn = setbits(wn, SL<S>::NI, 2 * S, ni);
+        wn = setbits(wn, SL<S>::MI, 2 * S, 0);
+        d.srv = ok ? i : -1;
+        d.w_new = ok ? wn : 0ull;
+        d.en = ok ? 1 : 0;
         break;
     }
     case 4: {  // ClientRequest(i, v) :206-213 (v = j)
         const u64 wi = selw<S>(w, i);
-        if (j < P.V && w_st(wi) == LEADER) {
-            const u32 len = w_len(wi);
-            if (len >= (u32)LOG_CAP) {
-                d.w_new = wi | (1ull << 63);  // Len = 4: out of every allowed constraint
-            } else {
-                u64 wn = setbits(wi, LOG_SH + ENT_W * (int)len, ENT_W, w_ct(wi) | ((u32)j << 4));
-                d.w_new = setbits(wn, LEN_SH, 2, len + 1);
-            }
-            d.srv = i;
-            d.en = 1;
-        }
+        const bool ok = j < P.V && w_st(wi) == LEADER;
+        const u32 len = w_len(wi), lc = len < (u32)LOG_CAP ? len : (u32)LOG_CAP - 1u;
+        const u64 wn = len >= (u32)LOG_CAP ? wi | (1ull << 63)  // Len = 4: out of every allowed constraint
+                     : setbits(setbits(wi, LOG_SH + ENT_W * (int)lc, ENT_W, w_ct(wi) | ((u32)j << 4)), LEN_SH, 2,
+                               len + 1);
+        d.srv = ok ? i : -1;
+        d.w_new = ok ? wn : 0ull;
+        d.en = ok ? 1 : 0;
         break;
     }
     case 5: {  // AdvanceCommitIndex(i) :219-236
         const u64 wi = selw<S>(w, i);
-        if (w_st(wi) == LEADER) {
-            const u32 len = w_len(wi);
-            u32 best = 0;
-            for (u32 idx = 1; idx <= len; ++idx) {
-                u32 agree = 1u << i;
+        const bool ok = w_st(wi) == LEADER;
+        const u32 len = w_len(wi);
+        u32 best = 0;
 #pragma unroll
-                for (int q = 0; q < S; ++q) agree |= (w_mi<S>(wi, q) >= idx ? 1u : 0u) << q;
-                if (2 * __builtin_popcount(agree) > S) best = idx;  // Max(agreeIndexes)
-            }
-            u64 wn = wi;
-            if (best > 0 && ent_term(w_ent(wi, best - 1)) == w_ct(wi)) wn = setbits(wi, CI_SH, 2, best);
-            d.srv = i;
-            d.w_new = wn;
-            d.en = 1;
+        for (u32 idx = 1; idx <= (u32)LOG_CAP; ++idx) {  // agreeIndexes over 1..Len(log[i])
+            u32 agree = 1u << i;
+#pragma unroll
+            for (int q = 0; q < S; ++q) agree |= (w_mi<S>(wi, q) >= idx ? 1u : 0u) << q;
+            best = (idx <= len && 2 * __builtin_popcount(agree) > S) ? idx : best;  // Max(agreeIndexes)
         }
+        const u32 bc = best ? best - 1u : 0u;
+        const u64 wn = (best > 0 && ent_term(w_ent(wi, bc)) == w_ct(wi)) ? setbits(wi, CI_SH, 2, best) : wi;
+        d.srv = ok ? i : -1;
+        d.w_new = ok ? wn : 0ull;
+        d.en = ok ? 1 : 0;
         break;
     }
     case 6: {  // AppendEntries(i, j) :171-192
         const u64 wi = selw<S>(w, i);
-        if (i != j && w_st(wi) == LEADER) {
-            const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
-            const u32 prev = ni - 1;
-            const u32 pterm = (prev > 0 && prev <= len) ? ent_term(w_ent(wi, prev - 1)) : 0u;
-            const u32 last = len < ni ? len : ni;  // Min({Len(log[i]), nextIndex[i][j]})
-            const u32 nent = ni <= last ? 1u : 0u; // SubSeq(log[i], ni, last): 0 or 1 entry
-            const u32 ent = nent ? w_ent(wi, ni - 1) : 0u;
-            const u32 ci = w_ci(wi), mci = ci < last ? ci : last;
-            d.add = m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | ((prev + 1u) << 12) | (pterm << 15) | (nent << 19) |
-                    (ent << 20) | (mci << 25);
-            d.has_add = 1;
-            d.en = 1;
-        }
+        const bool ok = i != j && w_st(wi) == LEADER;
+        const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
+        const u32 prev = ni - 1;
+        const u32 pc = (prev > 0 && prev <= len) ? prev - 1u : 0u;
+        const u32 pterm = (prev > 0 && prev <= len) ? ent_term(w_ent(wi, pc)) : 0u;
+        const u32 last = len < ni ? len : ni;  // Min({Len(log[i]), nextIndex[i][j]})
+        const u32 nent = ni <= last ? 1u : 0u; // SubSeq(log[i], ni, last): 0 or 1 entry
+        const u32 ent = nent ? w_ent(wi, ni - 1) : 0u;
+        const u32 ci = w_ci(wi), mci = ci < last ? ci : last;
+        d.add = ok ? m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | ((prev + 1u) << 12) | (pterm << 15) | (nent << 19) |
+                         (ent << 20) | (mci << 25)
+                   : 0u;
+        d.has_add = ok ? 1 : 0;
+        d.en = ok ? 1 : 0;
         break;
     }
     case 7: {  // Receive(m) :388-403
@@ -461,19 +460,15 @@ RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, i
     }
     case 8: {  // DuplicateMessage(m) :410-412
         const u32 sl = selm<K>(m, t);
-        if (sl) {
-            d.add = sl & MSG_MASK;
-            d.has_add = 1;
-            d.en = 1;
-        }
+        d.add = sl & MSG_MASK;
+        d.has_add = sl ? 1 : 0;
+        d.en = sl ? 1 : 0;
         break;
     }
     default: {  // DropMessage(m) :415-417
         const u32 sl = selm<K>(m, t);
-        if (sl) {
-            d.rm = t;
-            d.en = 1;
-        }
+        d.rm = sl ? t : -1;
+        d.en = sl ? 1 : 0;
         break;
     }
     }
@@ -575,39 +570,44 @@ RMC_HD u64 sel64(const u64 (&a)[N], int i) {
 template <int S, int K>
 RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
                         const Params& P, u64* h, int* nmsg_out = nullptr, u64* hw_new = nullptr) {
-    // Branch-light: the bounds are predicates and selects; only the three
-    // mixes (new server word, decremented slot, added / incremented slot) sit
-    // under a branch, so a wave skips a mix no lane of it needs.  (Every early
-    // return of a per-lane condition costs the wave an exec-mask save, test
-    // and restore in scalar instructions.)
-    const bool has_s = d.srv >= 0, has_r = d.rm >= 0, has_a = d.has_add != 0;
-    bool ok = !has_s || ((d.w_new >> 63) == 0 &&  // term 16 or Len 4: beyond every bound
-                         (int)w_ct(d.w_new) <= P.max_term && (int)w_len(d.w_new) <= P.max_log);
-    const u64 wo = selw<S>(w, d.srv), ho = sel64<S>(pm.hw, d.srv);
-    u64 hn = ho;
-    if (ok && has_s && d.w_new != wo) hn = hS(d.w_new, (u32)d.srv);
-    if (hw_new) *hw_new = hn;  // the new word's mix (the sharded owner reuses it)
-    u64 hh = pm.h0 + (hn - ho);
-    const u32 slr = selm<K>(m, d.rm);
-    const bool dec = has_r && m_cnt(slr) > 1;  // the removed message keeps a copy
-    u64 hr = 0;
-    if (ok && dec) hr = hM(slr - CNT_ONE);
-    hh += has_r ? hr - sel64<K>(pm.hm, d.rm) : 0ull;
-    int nmsg = pm.nmsg - ((has_r && !dec) ? 1 : 0);
-    int found = -1;
+    // early returns on purpose: a branch-light form (bounds as predicates, only
+    // the mixes under branches) measured 306 vs 289-294 ms per MCraftBench BFS —
+    // out-of-model lanes then pay for the whole computation
+    u64 hh = pm.h0;
+    int nmsg = pm.nmsg;
+    if (d.srv >= 0) {
+        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
+        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
+        const u64 wo = selw<S>(w, d.srv);
+        const u64 ho = sel64<S>(pm.hw, d.srv);
+        const u64 hn = d.w_new != wo ? hS(d.w_new, (u32)d.srv) : ho;
+        hh += hn - ho;
+        if (hw_new) *hw_new = hn;  // the new word's mix (the sharded owner reuses it)
+    }
+    if (d.rm >= 0) {
+        const u32 sl = selm<K>(m, d.rm);
+        hh -= sel64<K>(pm.hm, d.rm);
+        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
+        else nmsg -= 1;
+    }
+    if (d.has_add) {
+        int found = -1;
 #pragma unroll
-    for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
-    const bool inc = has_a && found >= 0;  // the added message is already in the bag
-    const u32 sla = selm<K>(m, found);
-    ok = ok && (!has_a || (inc ? (int)m_cnt(sla) + 1 <= P.max_dup : 1 <= P.max_dup));
-    nmsg += (has_a && !inc) ? 1 : 0;
-    ok = ok && nmsg <= P.max_msgs;
-    u64 ha = 0;
-    if (ok && has_a) ha = hM(inc ? sla + CNT_ONE : (d.add | CNT_ONE));
-    hh += has_a ? ha - (inc ? sel64<K>(pm.hm, found) : 0ull) : 0ull;
+        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
+        if (found >= 0) {
+            const u32 sl = selm<K>(m, found);
+            if ((int)m_cnt(sl) + 1 > P.max_dup) return 0;
+            hh += hM(sl + CNT_ONE) - sel64<K>(pm.hm, found);
+        } else {
+            if (1 > P.max_dup) return 0;
+            nmsg += 1;
+            hh += hM(d.add | CNT_ONE);
+        }
+    }
+    if (nmsg > P.max_msgs) return 0;
     *h = hh;
     if (nmsg_out) *nmsg_out = nmsg;
-    return ok ? 1 : 0;
+    return 1;
 }
 
 // delta_fp_pre split in two, so a lane can decide to skip its probe before it
@@ -942,14 +942,15 @@ RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diam
 // b's side from lane b's descriptor (lanes < 64): the same test as diamond_skip.
 template <int S, int K>
 RMC_HD bool diamond_skip_desc(const u32 (&m)[K], int b, u32 desc, const Delta& db, int nmsg_b, const Diamond& dm) {
-    // one predicate, no early returns (see delta_fp_pre on branches)
     const int fb = (int)(desc & 15u), tb = (int)((desc >> 4) & 255u), sd = (int)((desc >> 12) & 7u);
     const u32 mb = fb >= 7 ? (selm<K>(m, tb) & MSG_MASK) : 0xFFFFFFFDu;
     const u64 ob = ((u64)fb << 40) | (fb < 7 ? (u64)b : (u64)mb) | (1ull << 48);
+    if (!(ob < dm.ord)) return false;  // dm.ord = 0: never (the common exit)
     const int sb = sd < 7 ? sd : fb == 7 ? (int)m_dst(mb) : -1;
+    if (sb >= 0 && sb == dm.srv) return false;
     const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
-    return (ob < dm.ord) & !(sb >= 0 && sb == dm.srv) & (mb != dm.k0) & (mb != dm.k1) & (kb1 != dm.k0) &
-           (kb1 != dm.k1) & (nmsg_b <= dm.dom);
+    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
+    return nmsg_b <= dm.dom;
 }
 // b's side: lane b with delta db on t (m = t's bag), nmsg_b = |DOMAIN| of b(t).
 template <int S, int K>
