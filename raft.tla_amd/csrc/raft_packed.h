@@ -171,73 +171,11 @@ RMC_HD u32 selm(const u32 (&m)[K], int i) {
     return r;
 }
 
-// Receive(m) raft.tla:388-403 for bag slot k (message `msg`), branch-light:
-// every case of the receive tree is a predicate and its effect a select, so a
-// wave whose lanes hold messages of different types and outcomes runs one
-// straight-line block instead of a tree of exec-masked branches (their
-// scalar bookkeeping cost as much issue as the vector work).  Indices into
-// the log are clamped so that the reads of cases not taken stay defined.
+// Receive(m) raft.tla:388-403 for bag slot k (message `msg`).  (A branch-free
+// form — every case a predicate, its effect a select — measured neutral on the
+// bench model and 6-17 % slower on S = 5 and simulation: profiles/r03/ab/.)
 template <int S, int K>
 RMC_HD void receive_lane(const u64 (&w)[S], u32 msg, int k, Delta& d) {
-    const u32 i = m_dst(msg), j = m_src(msg), mterm = m_term(msg), mt = m_type(msg);
-    const u64 wi = selw<S>(w, (int)i);
-    const u32 ct = w_ct(wi), st = w_st(wi), len = w_len(wi);
-    const bool up = mterm > ct, lt = mterm < ct;  // UpdateTerm :373-379 (m stays); stale
-    const bool rvq = !up && mt == RVQ, rvp = !up && mt == RVP, aeq = !up && mt == AEQ, aep = !up && mt == AEP;
-    // HandleRequestVoteRequest :244-263 (mterm <= ct here)
-    const u32 mlt = (msg >> 12) & 15u, mli = (msg >> 16) & 3u, lterm = w_last_term(wi), vf = w_vf(wi);
-    const bool grant = mterm == ct && (mlt > lterm || (mlt == lterm && mli >= len)) && (vf == NILV || vf == j);
-    // HandleAppendEntriesRequest :347-356; pe = mprevLogIndex + 1 (mprevLogIndex = -1,
-    // Smokeraft.tla:35, fails both disjuncts of logOk)
-    const u32 pe = (msg >> 12) & 7u, pterm = (msg >> 15) & 15u;
-    const u32 nent = (msg >> 19) & 1u, ent = (msg >> 20) & 31u, mci = (msg >> 25) & 3u;
-    const u32 pidx = pe - 1u;
-    const u32 e_prev = (pe >= 2u && pe - 2u < (u32)LOG_CAP) ? pe - 2u : 0u;  // log[mprevLogIndex], 0-based
-    const u32 e_idx = (pe >= 1u && pe - 1u < (u32)LOG_CAP) ? pe - 1u : 0u;   // log[index], index = pe
-    const bool log_ok = pe == 1u || (pe > 1u && pidx <= len && pterm == ent_term(w_ent(wi, e_prev)));
-    const bool reject = aeq && (lt || (st == FOLLOWER && !log_ok));          // :281-293
-    const bool ret = aeq && !reject && st == CANDIDATE;                      // ReturnToFollowerState :295-299
-    const bool fol = aeq && !reject && st == FOLLOWER;                       // (a Leader: no branch)
-    const bool term_eq = len >= pe && ent_term(w_ent(wi, e_idx)) == ent_term(ent);
-    const bool done = fol && (nent == 0u || term_eq);
-    // AppendEntriesAlreadyDone :301-317: UNCHANGED logVars after commitIndex' =
-    // m.mcommitIndex is a TLC equality test, enabled only when they are equal
-    const bool done_en = done && mci == w_ci(wi);
-    const bool confl = fol && !done && len >= pe;               // ConflictAppendEntriesRequest :319-325
-    const bool noconf = fol && !done && !confl && len == pidx;  // NoConflictAppendEntriesRequest :327-331
-    // the words of the cases that change one
-    const u64 wn_up = setbits(setbits(setbits(wi, CT_SH, 4, mterm), ST_SH, 2, FOLLOWER), VF_SH, 3, NILV);
-    const u64 wn_rvq = grant ? setbits(wi, VF_SH, 3, j) : wi;
-    const u64 wn_rvp = lt ? wi  // DropStaleResponse :382-385; else HandleRequestVoteResponse :267-279
-                          : wi | (1ull << (SL<S>::VR + (int)j)) | ((u64)((msg >> 12) & 1u) << (SL<S>::VG + (int)j));
-    const u64 wn_ret = setbits(wi, ST_SH, 2, FOLLOWER);
-    const u32 lm1 = len ? len - 1u : 0u;  // Conflict: drop the LAST entry (len >= pe >= 1), m stays
-    const u64 wn_confl = setbits(setbits(wi, LOG_SH + ENT_W * (int)lm1, ENT_W, 0), LEN_SH, 2, lm1);
-    const u32 lc = len < (u32)LOG_CAP ? len : (u32)LOG_CAP - 1u;  // NoConflict appends (Len = 4: out of every bound)
-    const u64 wn_noconf = len >= (u32)LOG_CAP ? (setbits(wi, LEN_SH, 2, 3) | (1ull << 63))
-                                              : setbits(setbits(wi, LOG_SH + ENT_W * (int)lc, ENT_W, ent), LEN_SH, 2, len + 1u);
-    const u32 mm = (msg >> 13) & 3u, nis = bits(wi, SL<S>::NI + 2 * (int)j, 2);  // HandleAppendEntriesResponse :360-370
-    const u64 wn_aep = lt ? wi
-                     : ((msg >> 12) & 1u) ? setbits(setbits(wi, SL<S>::NI + 2 * (int)j, 2, mm), SL<S>::MI + 2 * (int)j, 2, mm)
-                                          : setbits(wi, SL<S>::NI + 2 * (int)j, 2, nis ? nis - 1u : 0u);  // Max({ni-1, 1})
-    d.srv = (int)i;
-    d.w_new = up ? wn_up : rvq ? wn_rvq : rvp ? wn_rvp : ret ? wn_ret : confl ? wn_confl : noconf ? wn_noconf
-            : aep ? wn_aep : wi;
-    // Reply :102-103: an RVResp carries mlog = log[i] (len + entries bits); AEResp
-    // FALSE / 0 on reject, TRUE / mprevLogIndex + Len(entries) when already done
-    const u32 hdr = rvq ? m_hdr(RVP, i, j, ct) : m_hdr(AEP, i, j, ct);
-    d.has_add = (rvq || reject || done_en) ? 1 : 0;
-    d.add = !d.has_add ? 0u
-          : rvq ? hdr | ((grant ? 1u : 0u) << 12) | (bits(wi, LEN_SH, 17) << 13)
-          : done_en ? hdr | (1u << 12) | ((pidx + nent) << 13) : hdr;
-    d.rm = (rvq || rvp || reject || done_en || aep) ? k : -1;
-    d.en = (up || rvq || rvp || reject || ret || done_en || confl || noconf || aep) ? 1 : 0;
-}
-
-// Receive(m) as a decision tree (the round-2 form; the host model checks
-// receive_lane against it on every Receive lane).
-template <int S, int K>
-RMC_HD void receive_lane_branchy(const u64 (&w)[S], u32 msg, int k, Delta& d) {
     const u32 i = m_dst(msg), j = m_src(msg), mterm = m_term(msg), mt = m_type(msg);
     const u64 wi = selw<S>(w, (int)i);
     const u32 ct = w_ct(wi), st = w_st(wi), len = w_len(wi);
@@ -354,10 +292,10 @@ RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, i
     d.add = 0;
     d.en = 0;
     d.w_new = 0;
-    // fam is wave-uniform in the kernels (scalar branches); the enabling
-    // conditions inside a family are per state, so they are predicates and
-    // selects rather than branches (each divergent branch costs the wave an
-    // exec-mask save, test and restore)
+    // fam is wave-uniform in the sorted kernels (scalar branches).  The enabling
+    // conditions inside a family stay branches: written as predicates + selects
+    // they were neutral on the bench model and 4-17 % slower on S = 5 and
+    // simulation (profiles/r03/ab/lane_code_c1_c2_c3_r03t.jsonl)
     switch (fam) {
     case 0: {  // Restart(i) :136-143
         d.srv = i;
@@ -368,89 +306,94 @@ RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, i
     case 1: {  // Timeout(i) :146-154
         const u64 wi = selw<S>(w, i);
         const u32 st = w_st(wi);
-        const bool ok = st == FOLLOWER || st == CANDIDATE;
-        const u32 ct1 = w_ct(wi) + 1;
-        u64 wn = setbits(wi, ST_SH, 2, CANDIDATE);
-        wn = setbits(wn, VF_SH, 3, NILV);
-        wn &= ~(((u64)SL<S>::SMASK << SL<S>::VR) | ((u64)SL<S>::SMASK << SL<S>::VG));
-        wn = setbits(wn, CT_SH, 4, ct1 & 15u) | ((u64)(ct1 >> 4) << 63);  // bit 63: term overflow
-        d.srv = ok ? i : -1;
-        d.w_new = ok ? wn : 0ull;
-        d.en = ok ? 1 : 0;
+        if (st == FOLLOWER || st == CANDIDATE) {
+            const u32 ct1 = w_ct(wi) + 1;
+            u64 wn = setbits(wi, ST_SH, 2, CANDIDATE);
+            wn = setbits(wn, VF_SH, 3, NILV);
+            wn &= ~(((u64)SL<S>::SMASK << SL<S>::VR) | ((u64)SL<S>::SMASK << SL<S>::VG));
+            wn = setbits(wn, CT_SH, 4, ct1 & 15u) | ((u64)(ct1 >> 4) << 63);  // bit 63: term overflow
+            d.srv = i;
+            d.w_new = wn;
+            d.en = 1;
+        }
         break;
     }
     case 2: {  // RequestVote(i, j) :157-166 (no i /= j guard)
         const u64 wi = selw<S>(w, i);
-        const bool ok = w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u);
-        d.add = ok ? m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16) : 0u;
-        d.has_add = ok ? 1 : 0;
-        d.en = ok ? 1 : 0;
+        if (w_st(wi) == CANDIDATE && !((w_vr<S>(wi) >> j) & 1u)) {
+            d.add = m_hdr(RVQ, (u32)i, (u32)j, w_ct(wi)) | (w_last_term(wi) << 12) | (w_len(wi) << 16);
+            d.has_add = 1;
+            d.en = 1;
+        }
         break;
     }
     case 3: {  // BecomeLeader(i) :195-203
         const u64 wi = selw<S>(w, i);
         const u32 vg = w_vg<S>(wi);
-        const bool quorum = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
-        const bool ok = w_st(wi) == CANDIDATE && quorum;
-        u64 wn = setbits(wi, ST_SH, 2, LEADER);
-        const u64 lenv = w_len(wi);  // nextIndex = Len + 1, stored minus one
-        u64 ni = 0;
+        const bool ok = P.bug_quorum ? vg != 0u : (2 * __builtin_popcount(vg) > S);
+        if (w_st(wi) == CANDIDATE && ok) {
+            u64 wn = setbits(wi, ST_SH, 2, LEADER);
+            const u64 lenv = w_len(wi);  // nextIndex = Len + 1, stored minus one
+            u64 ni = 0;
 #pragma unroll
-        for (int q = 0; q < S; ++q) ni |= lenv << (2 * q);
-        wn = setbits(wn, SL<S>::NI, 2 * S, ni);
-        wn = setbits(wn, SL<S>::MI, 2 * S, 0);
-        d.srv = ok ? i : -1;
-        d.w_new = ok ? wn : 0ull;
-        d.en = ok ? 1 : 0;
+            for (int q = 0; q < S; ++q) ni |= lenv << (2 * q);
+            wn = setbits(wn, SL<S>::NI, 2 * S, ni);
+            wn = setbits(wn, SL<S>::MI, 2 * S, 0);
+            d.srv = i;
+            d.w_new = wn;
+            d.en = 1;
+        }
         break;
     }
     case 4: {  // ClientRequest(i, v) :206-213 (v = j)
         const u64 wi = selw<S>(w, i);
-        const bool ok = j < P.V && w_st(wi) == LEADER;
-        const u32 len = w_len(wi), lc = len < (u32)LOG_CAP ? len : (u32)LOG_CAP - 1u;
-        const u64 wn = len >= (u32)LOG_CAP ? wi | (1ull << 63)  // Len = 4: out of every allowed constraint
-                     : setbits(setbits(wi, LOG_SH + ENT_W * (int)lc, ENT_W, w_ct(wi) | ((u32)j << 4)), LEN_SH, 2,
-                               len + 1);
-        d.srv = ok ? i : -1;
-        d.w_new = ok ? wn : 0ull;
-        d.en = ok ? 1 : 0;
+        if (j < P.V && w_st(wi) == LEADER) {
+            const u32 len = w_len(wi);
+            if (len >= (u32)LOG_CAP) {
+                d.w_new = wi | (1ull << 63);  // Len = 4: out of every allowed constraint
+            } else {
+                u64 wn = setbits(wi, LOG_SH + ENT_W * (int)len, ENT_W, w_ct(wi) | ((u32)j << 4));
+                d.w_new = setbits(wn, LEN_SH, 2, len + 1);
+            }
+            d.srv = i;
+            d.en = 1;
+        }
         break;
     }
     case 5: {  // AdvanceCommitIndex(i) :219-236
         const u64 wi = selw<S>(w, i);
-        const bool ok = w_st(wi) == LEADER;
-        const u32 len = w_len(wi);
-        u32 best = 0;
+        if (w_st(wi) == LEADER) {
+            const u32 len = w_len(wi);
+            u32 best = 0;
+            for (u32 idx = 1; idx <= len; ++idx) {
+                u32 agree = 1u << i;
 #pragma unroll
-        for (u32 idx = 1; idx <= (u32)LOG_CAP; ++idx) {  // agreeIndexes over 1..Len(log[i])
-            u32 agree = 1u << i;
-#pragma unroll
-            for (int q = 0; q < S; ++q) agree |= (w_mi<S>(wi, q) >= idx ? 1u : 0u) << q;
-            best = (idx <= len && 2 * __builtin_popcount(agree) > S) ? idx : best;  // Max(agreeIndexes)
+                for (int q = 0; q < S; ++q) agree |= (w_mi<S>(wi, q) >= idx ? 1u : 0u) << q;
+                if (2 * __builtin_popcount(agree) > S) best = idx;  // Max(agreeIndexes)
+            }
+            u64 wn = wi;
+            if (best > 0 && ent_term(w_ent(wi, best - 1)) == w_ct(wi)) wn = setbits(wi, CI_SH, 2, best);
+            d.srv = i;
+            d.w_new = wn;
+            d.en = 1;
         }
-        const u32 bc = best ? best - 1u : 0u;
-        const u64 wn = (best > 0 && ent_term(w_ent(wi, bc)) == w_ct(wi)) ? setbits(wi, CI_SH, 2, best) : wi;
-        d.srv = ok ? i : -1;
-        d.w_new = ok ? wn : 0ull;
-        d.en = ok ? 1 : 0;
         break;
     }
     case 6: {  // AppendEntries(i, j) :171-192
         const u64 wi = selw<S>(w, i);
-        const bool ok = i != j && w_st(wi) == LEADER;
-        const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
-        const u32 prev = ni - 1;
-        const u32 pc = (prev > 0 && prev <= len) ? prev - 1u : 0u;
-        const u32 pterm = (prev > 0 && prev <= len) ? ent_term(w_ent(wi, pc)) : 0u;
-        const u32 last = len < ni ? len : ni;  // Min({Len(log[i]), nextIndex[i][j]})
-        const u32 nent = ni <= last ? 1u : 0u; // SubSeq(log[i], ni, last): 0 or 1 entry
-        const u32 ent = nent ? w_ent(wi, ni - 1) : 0u;
-        const u32 ci = w_ci(wi), mci = ci < last ? ci : last;
-        d.add = ok ? m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | ((prev + 1u) << 12) | (pterm << 15) | (nent << 19) |
-                         (ent << 20) | (mci << 25)
-                   : 0u;
-        d.has_add = ok ? 1 : 0;
-        d.en = ok ? 1 : 0;
+        if (i != j && w_st(wi) == LEADER) {
+            const u32 len = w_len(wi), ni = w_ni<S>(wi, (u32)j);
+            const u32 prev = ni - 1;
+            const u32 pterm = (prev > 0 && prev <= len) ? ent_term(w_ent(wi, prev - 1)) : 0u;
+            const u32 last = len < ni ? len : ni;  // Min({Len(log[i]), nextIndex[i][j]})
+            const u32 nent = ni <= last ? 1u : 0u; // SubSeq(log[i], ni, last): 0 or 1 entry
+            const u32 ent = nent ? w_ent(wi, ni - 1) : 0u;
+            const u32 ci = w_ci(wi), mci = ci < last ? ci : last;
+            d.add = m_hdr(AEQ, (u32)i, (u32)j, w_ct(wi)) | ((prev + 1u) << 12) | (pterm << 15) | (nent << 19) |
+                    (ent << 20) | (mci << 25);
+            d.has_add = 1;
+            d.en = 1;
+        }
         break;
     }
     case 7: {  // Receive(m) :388-403
@@ -460,34 +403,62 @@ RMC_HD void lane_delta_f(const u64 (&w)[S], const u32 (&m)[K], int fam, int t, i
     }
     case 8: {  // DuplicateMessage(m) :410-412
         const u32 sl = selm<K>(m, t);
-        d.add = sl & MSG_MASK;
-        d.has_add = sl ? 1 : 0;
-        d.en = sl ? 1 : 0;
+        if (sl) {
+            d.add = sl & MSG_MASK;
+            d.has_add = 1;
+            d.en = 1;
+        }
         break;
     }
     default: {  // DropMessage(m) :415-417
         const u32 sl = selm<K>(m, t);
-        d.rm = sl ? t : -1;
-        d.en = sl ? 1 : 0;
+        if (sl) {
+            d.rm = t;
+            d.en = 1;
+        }
         break;
     }
     }
 }
 
 // Compute the delta of lane `lane` (0 <= lane < Lanes<S,K>::N) on parent (w, m).
+// The family dispatch is a chain on the offsets read from the kernel argument
+// (equal to Lanes<S,K>::off), each branch calling lane_delta_f with a constant
+// family, so only that family's body is inlined there (computing the family
+// first and switching on it measured 57 % slower on the >64-lane S = 5 kernel).
 template <int S, int K>
 RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Params& P, Delta& d) {
-    // offsets read from the kernel argument (equal to Lanes<S,K>::off): a branch tree
-    int fam = 0;
-#pragma unroll
-    for (int k = 1; k <= 9; ++k) fam += lane >= P.off[k] ? 1 : 0;
-    int o = 0;
-#pragma unroll
-    for (int k = 0; k <= 9; ++k) o = fam == k ? P.off[k] : o;
-    const int t = lane - o;
-    const int i = (fam == 2 || fam == 6) ? t / S : fam == 4 ? t / VMAX : t;
-    const int j = (fam == 2 || fam == 6) ? t % S : fam == 4 ? t % VMAX : 0;
-    lane_delta_f<S, K>(w, m, fam, t, i, j, P, d);
+    const int* o = P.off;
+    if (lane < o[1]) {
+        lane_delta_f<S, K>(w, m, 0, lane, lane, 0, P, d);
+    } else if (lane < o[2]) {
+        const int t = lane - o[1];
+        lane_delta_f<S, K>(w, m, 1, t, t, 0, P, d);
+    } else if (lane < o[3]) {
+        const int t = lane - o[2];
+        lane_delta_f<S, K>(w, m, 2, t, t / S, t % S, P, d);
+    } else if (lane < o[4]) {
+        const int t = lane - o[3];
+        lane_delta_f<S, K>(w, m, 3, t, t, 0, P, d);
+    } else if (lane < o[5]) {
+        const int t = lane - o[4];
+        lane_delta_f<S, K>(w, m, 4, t, t / VMAX, t % VMAX, P, d);
+    } else if (lane < o[6]) {
+        const int t = lane - o[5];
+        lane_delta_f<S, K>(w, m, 5, t, t, 0, P, d);
+    } else if (lane < o[7]) {
+        const int t = lane - o[6];
+        lane_delta_f<S, K>(w, m, 6, t, t / S, t % S, P, d);
+    } else if (lane < o[8]) {
+        const int t = lane - o[7];
+        lane_delta_f<S, K>(w, m, 7, t, 0, 0, P, d);
+    } else if (lane < o[9]) {
+        const int t = lane - o[8];
+        lane_delta_f<S, K>(w, m, 8, t, 0, 0, P, d);
+    } else {
+        const int t = lane - o[9];
+        lane_delta_f<S, K>(w, m, 9, t, 0, 0, P, d);
+    }
 }
 
 // The same from a lane descriptor (Params.ldesc, lanes < 64: lane_desc).

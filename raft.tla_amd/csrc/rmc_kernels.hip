@@ -13,6 +13,8 @@
 //             (no dedup) — the differential-test entry point (rmc_expand).
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "raft_packed.h"
 #include "rmc_internal.h"
@@ -1499,12 +1501,31 @@ static hipError_t launch_sim_t(const Params& P, const u32* inits, u64 n_init, u6
 // is one block round and every window sorts more tiles; 309.7 vs 315.6 ms per
 // MCraftBench BFS against 2048, profiles/r03/ab/).  The other grid-stride
 // kernels run 2048 blocks.
-static u64 expand_grid() {
+static u64 expand_grid_env() {
     static u64 v = [] {
         const char* e = getenv("RMC_EXPAND_GRID");
         const long long x = e ? atoll(e) : 0;
-        return x >= 64 && x <= (1 << 20) ? (u64)x : (u64)1024;
+        return x >= 64 && x <= (1 << 20) ? (u64)x : (u64)0;
     }();
+    return v;
+}
+// One round of resident blocks of kernel `k` on this device (blocks per CU at
+// its register / LDS occupancy x CUs), cached per kernel and device: 1024 for
+// the 4-wave sorted kernels, 1280 for the 5-wave every-lane kernel (a fixed
+// 1024 left a fifth of the CUs' slots idle on S = 5: 0.339 s vs 0.289 s).
+static u64 resident_grid(const void* k) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, u64> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find({k, dev});
+    if (it != cache.end()) return it->second;
+    int nb = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const u64 v = (u64)nb * (u64)cus;
+    cache[{k, dev}] = v;
     return v;
 }
 
@@ -1574,11 +1595,16 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    // grid-stride kernels: about 8 resident 256-thread blocks per CU x 256 CUs;
-    // the expansion kernels (4 waves/SIMD) one round of resident blocks
-    // (SYMMETRY keeps 2048: 79.7 vs 81.5 ms on the MCraftBench bounds)
-    const u64 grid = ((which == 0 && !SYM) || which == 3) ? expand_grid() : (u64)2048;
+    // grid-stride kernels: 2048 blocks; the plain and sharded expansion kernels
+    // one round of resident blocks (resident_grid at their launch below;
+    // SYMMETRY keeps 2048: 79.7 vs 81.5 ms on the MCraftBench bounds)
+    const u64 grid = (u64)2048;
     const u64 g = blocks < grid ? blocks : grid;
+    // the expansion kernels' grid: RMC_EXPAND_GRID, else one round of resident blocks
+    auto eg = [&](const void* k) -> unsigned {
+        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(k);
+        return (unsigned)(blocks < want ? blocks : want);
+    };
     if (which == 0) {
         if constexpr (SYM) {
             if (verify)
@@ -1599,53 +1625,53 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
         } else if (verify) {
-            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, false, kBatch, false, true>)))), dim3(256), 0, st, P, PT,
                                B, a, b);
         } else if (expand_variant() == 4 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 0>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 0>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 0>)))), dim3(256), 0, st, P, PT, B, a, b);
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, true>)))), dim3(256), 0, st, P,
                                PT, B, a, b);
         } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {  // windows of 8 tiles (round-2 size)
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT,
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false>)))), dim3(256), 0, st, P, PT,
                                B, a, b);
         } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {  // default: windows of 16 tiles (4096 states)
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3((unsigned)g), dim3(256), 0,
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, false, 16>)))), dim3(256), 0,
                                st, P, PT, B, a, b);
         } else {  // 1, and shapes with more than 64 lanes
-            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3((unsigned)g), dim3(256), 0, st,
+            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, false, kBatch, false, false, true>)))), dim3(256), 0, st,
                                P, PT, B, a, b);
         }
     } else if (which == 3 && verify) {  // sharded full-state verification: every lane, hits compared
-        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, SYM, kBatch, true, true>)))), dim3(256), 0, st, P, PT, B, a,
                            b);
     } else if (which == 11) {
         hipLaunchKernelGGL((k_compare_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
     } else if (which == 3) {
         if constexpr (SYM)
-            hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
+            hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, SYM, kBatch, true>)))), dim3(256), 0, st, P, PT, B, a, b);
         else if (dist_variant() == 7) {  // default: send markers, no diamond skipping
-            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>), dim3((unsigned)g), dim3(256),
+            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false, false, true>)))), dim3(256),
                                0, st, P, PT, B, a, b);
         } else {
             bool ab = false;
             if constexpr (S == 3 && K == 4) {  // A/B variants, bench shape only: 4 = sent-cache, no diamond
                 ab = true;                     // skipping; 6 = send markers with diamond skipping
                 if (dist_variant() == 4)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>), dim3((unsigned)g), dim3(256), 0,
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false>)))), dim3(256), 0,
                                        st, P, PT, B, a, b);
                 else if (dist_variant() == 6)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>), dim3((unsigned)g),
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, true, false, true>)))),
                                        dim3(256), 0, st, P, PT, B, a, b);
                 else
                     ab = false;
             }
             if (ab) {
             } else if (dist_variant() == 1) {  // sent-cache, diamond skipping decided before hashing
-                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true>)))), dim3(256), 0, st, P, PT, B, a,
                                    b);
             } else {  // 0: sent-cache, every lane
-                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a,
+                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, false>)))), dim3(256), 0, st, P, PT, B, a,
                                    b);
             }
         }

@@ -119,7 +119,7 @@ struct Model {
         return true;
     }
 
-    struct Out { std::vector<u64> level_new; u64 generated = 0, probes = 0, skipped = 0, mismatch = 0, recv_mismatch = 0; };
+    struct Out { std::vector<u64> level_new; u64 generated = 0, probes = 0, skipped = 0, mismatch = 0; };
 
     Out bfs(int max_levels, bool skip, u64 cap) {
         Out o;
@@ -150,18 +150,6 @@ struct Model {
                 const u64 h0 = state_fp<S, K>(w, m);
                 ParentMix<S, K> pm;
                 parent_mix<S, K>(w, m, pm);
-                for (int q = 0; q < K; ++q) {  // branch-light Receive == the decision tree, every slot
-                    if (!m[q]) continue;
-                    Delta a{}, b{};
-                    a.srv = b.srv = -1; a.rm = b.rm = -1;
-                    receive_lane<S, K>(w, m[q] & MSG_MASK, q, a);
-                    receive_lane_branchy<S, K>(w, m[q] & MSG_MASK, q, b);
-                    if (a.en != b.en || (a.en && (a.srv != b.srv || a.rm != b.rm || a.has_add != b.has_add ||
-                                                  a.w_new != b.w_new || (a.has_add && a.add != b.add)))) {
-                        ++o.mismatch;
-                        ++o.recv_mismatch;
-                    }
-                }
                 for (int lane = 0; lane < nl; ++lane) {
                     Delta d;
                     lane_delta<S, K>(w, m, lane, P, d);
