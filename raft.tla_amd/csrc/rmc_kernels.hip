@@ -619,7 +619,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
           bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
-          bool MARK = false, int WTILES = 8>
+          bool MARK = false, int WTILES = 8, bool UPROBE = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -862,7 +862,9 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                            : remote ? (B.sent ? B.sent[(key[b] >> 8) & B.smask] : 0ull)
                                     : B.table[key[b] & B.tmask];
                 } else {
-                    cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
+                    // UPROBE: every lane loads (a lane without a key reads slot 0, a
+                    // valid address), so the loads need no exec-mask branches
+                    cur[b] = (UPROBE || key[b]) ? B.table[key[b] & B.tmask] : 0ull;
                 }
             }
 #pragma unroll
@@ -872,6 +874,17 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             u32 hitbits = 0;  // verification: probes that found their key (slot parked in s_key)
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
+                if constexpr (UPROBE && !VERIFY && !SENTC) {  // one branch per probe: around its CAS
+                    const bool live = key[b] != 0;
+                    slowbits |= (u32)(live && cur[b] != 0 && cur[b] != key[b]) << b;
+                    if (live && cur[b] == 0) {
+                        const u64 prev = atomicCAS((unsigned long long*)&B.table[key[b] & B.tmask], 0ull,
+                                                   (unsigned long long)key[b]);
+                        newbits |= (u32)(prev == 0) << b;
+                        slowbits |= (u32)(prev != 0 && prev != key[b]) << b;
+                    }
+                    continue;
+                }
                 if (!key[b]) continue;
                 if (cur[b] == key[b]) {
                     if constexpr (VERIFY) {
@@ -1003,12 +1016,13 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
-template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8>
+template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8,
+          bool UP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT>(P, PT, B, lo,
-                                                                                                       hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT, UP>(P, PT, B,
+                                                                                                           lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1632,6 +1646,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, true>)))), dim3(256), 0, st, P,
                                PT, B, a, b);
+        } else if (S == 3 && K == 4 && expand_variant() == 9) {  // A/B (bench shape): unconditional probe loads
+            if constexpr (S == 3 && K == 4)
+                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, true>),
+                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false,
+                                                                                         false, 16, true>)))),
+                                   dim3(256), 0, st, P, PT, B, a, b);
         } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {  // windows of 8 tiles (round-2 size)
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false>)))), dim3(256), 0, st, P, PT,
                                B, a, b);
