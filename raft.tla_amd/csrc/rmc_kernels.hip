@@ -179,7 +179,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
         B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
-        B.foot[ni] = make_foot<S, K>(m, lane, d, P);
+        if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = make_foot<S, K>(m, lane, d, P);  // diamonds: sorted kernels only
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
@@ -246,7 +246,7 @@ __device__ __forceinline__ void flush_new_sorted(const Params& P, const DevBufs&
         store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
         B.parent[ni] = B.ref_tag | (lo + rel);
         B.act[ni] = (uint8_t)lane;
-        B.foot[ni] = make_foot<S, K>(m, lane, d, P);
+        if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = make_foot<S, K>(m, lane, d, P);  // diamonds: sorted kernels only
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
     }
@@ -519,7 +519,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
         B.parent[slot] = B.ref_tag | (lo + rel);
         B.act[slot] = (uint8_t)lane;
-        B.foot[slot] = make_foot<S, K>(m, lane, d, P);
+        if constexpr (Lanes<S, K>::N <= 64) B.foot[slot] = make_foot<S, K>(m, lane, d, P);
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
     }
@@ -602,7 +602,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
         store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
         B.parent[slot] = B.ref_tag | (lo + rel);
         B.act[slot] = (uint8_t)lane;
-        B.foot[slot] = make_foot<S, K>(m, lane, d, P);
+        if constexpr (Lanes<S, K>::N <= 64) B.foot[slot] = make_foot<S, K>(m, lane, d, P);
         const int v = check_invariants<S, K>(wo, mo, P);
         if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
     }
@@ -816,8 +816,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         }
                         if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
                     }
-                    if (P.unbounded && en && !in_model)  // a depth-bounded unconstrained model outgrew the encoding
-                        if (const int f = capacity_exceeded<S, K>(m, d, P)) atomicOr(&B.ctr->overflow, (u32)f << 8);
                     if (in_model && (SYM || h != h0)) {
                         key = h;
                         if constexpr (VERIFY) key &= P.fp_mask;
@@ -1007,6 +1005,29 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         if (me == 0 && vchk) atomicAdd((unsigned long long*)&B.ctr->vchecked, (unsigned long long)vchk);
         if (me == 0 && vcol) atomicAdd((unsigned long long*)&B.ctr->collisions, (unsigned long long)vcol);
     }
+}
+
+// Depth-bounded unconstrained models (Params.unbounded): a successor that takes
+// an unbounded field past the packed capacity stops the search with
+// RMC_E_CAPACITY naming the field.  A separate pass over the launch's states,
+// run only for such models, so the expansion kernels carry no code for it
+// (in their lane loop it cost 8 % of the S = 5 kernel's instructions).
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_capacity_check(const Params P, const DevBufs B, u64 lo, u64 hi) {
+    constexpr int NW = 2 * S + K;
+    const int nl = P.off[10];
+    u32 bad = 0;
+    for (u64 t = lo + (u64)blockIdx.x * 256 + threadIdx.x; t < hi; t += (u64)gridDim.x * 256) {
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + t * (u64)NW, w, m);
+        for (int lane = 0; lane < nl; ++lane) {
+            Delta d;
+            lane_delta<S, K>(w, m, lane, P, d);
+            if (d.en) bad |= (u32)capacity_exceeded<S, K>(m, d, P);  // 0 for in-model successors
+        }
+    }
+    if (bad) atomicOr(&B.ctr->overflow, bad << 8);
 }
 
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false>
@@ -1581,19 +1602,20 @@ static int sym_variant() {
 }
 
 // Sharded expansion variant (RMC_DIST_VARIANT; same-box A/B at one rank on
-// RCCL, profiles/r03/ab/dist_*): 7 (default) = send markers in the local set
-// (a lossless sent-cache; the probe loop is the single-GPU loop), no diamond
-// skipping: 329-333 ms per MCraftBench BFS against 311-316 ms unsharded;
-// 6 = markers with diamond skipping (341 ms: the owner routing and the
-// diamond together cost more registers than the probes they save); 4 = the
-// lossy sent-cache, no diamonds (342-346 ms); 1 = the sent-cache with
+// RCCL, profiles/r03/ab/dist_* and final_lane_code_r03u.jsonl): 6 (default) =
+// send markers in the local set (a lossless sent-cache; the probe loop is the
+// single-GPU loop) with diamond skipping: 322.7-323.9 ms per MCraftBench BFS
+// against 290.9-294.0 unsharded, once the per-lane descriptors freed the
+// registers (before them: 341 ms, and 7 was best); 7 = markers without
+// diamonds (357.7-360.3 ms now, 329-333 before the descriptors); 4 = the
+// lossy sent-cache, no diamonds (bench shape); 1 = the sent-cache with
 // diamonds decided before hashing (round-3 start, 366 ms); 0 = every lane.
 // Measured and removed: 3 waves/SIMD, 6 probes in flight, the owner decided
 // in the flush (390 ms: a reservation atomic per 64 entries).
 static int dist_variant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_VARIANT");
-        return e ? atoi(e) : 7;
+        return e ? atoi(e) : 6;
     }();
     return v;
 }
@@ -1670,29 +1692,34 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     } else if (which == 3) {
         if constexpr (SYM)
             hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, SYM, kBatch, true>)))), dim3(256), 0, st, P, PT, B, a, b);
-        else if (dist_variant() == 7) {  // default: send markers, no diamond skipping
-            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false, false, true>)))), dim3(256),
-                               0, st, P, PT, B, a, b);
+        else if (dist_variant() == 6) {  // default: send markers with diamond skipping
+            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>),
+                               dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, true, false, true>)))),
+                               dim3(256), 0, st, P, PT, B, a, b);
+        } else if (dist_variant() == 7) {  // send markers, no diamond skipping
+            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>),
+                               dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false, false, true>)))),
+                               dim3(256), 0, st, P, PT, B, a, b);
         } else {
             bool ab = false;
-            if constexpr (S == 3 && K == 4) {  // A/B variants, bench shape only: 4 = sent-cache, no diamond
-                ab = true;                     // skipping; 6 = send markers with diamond skipping
+            if constexpr (S == 3 && K == 4) {  // A/B variant, bench shape only: 4 = sent-cache, no diamonds
+                ab = true;
                 if (dist_variant() == 4)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false>)))), dim3(256), 0,
-                                       st, P, PT, B, a, b);
-                else if (dist_variant() == 6)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, true, false, true>)))),
+                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>),
+                                       dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false>)))),
                                        dim3(256), 0, st, P, PT, B, a, b);
                 else
                     ab = false;
             }
             if (ab) {
             } else if (dist_variant() == 1) {  // sent-cache, diamond skipping decided before hashing
-                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true>)))), dim3(256), 0, st, P, PT, B, a,
-                                   b);
+                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>),
+                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true>)))), dim3(256), 0,
+                                   st, P, PT, B, a, b);
             } else {  // 0: sent-cache, every lane
-                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, false>)))), dim3(256), 0, st, P, PT, B, a,
-                                   b);
+                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>),
+                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, false>)))), dim3(256), 0,
+                                   st, P, PT, B, a, b);
             }
         }
     } else if (which == 8) {  // a = keys per destination block (max); out = replies
@@ -1714,6 +1741,8 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         hipLaunchKernelGGL((k_list<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, in, a, out, cap,
                            count);
     }
+    if ((which == 0 || which == 3) && P.unbounded)  // depth-bounded unconstrained model: the capacity pass
+        hipLaunchKernelGGL((k_capacity_check<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
     return hipGetLastError();
 }
 
@@ -1761,7 +1790,7 @@ RMC_DEFINE_SHAPE_(RMC_SHAPE_S, RMC_SHAPE_K)
 #else
 bool dist_uses_sent_cache() {
     const int v = dist_variant();
-    return !(v == 7 || (v == 6));  // markers live in the fingerprint set (variant 6: bench shape only)
+    return !(v == 6 || v == 7);  // markers live in the fingerprint set
 }
 
 hipError_t set_fp_salt(u64 seed, hipStream_t st) {
