@@ -703,7 +703,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     c->B.world = (u32)world;
     c->B.ref_tag = (u64)rank << 48;
     const char* om = getenv("RMC_OWNER");  // partition: 0 fingerprint, 1 server-0 word, 2 servers 0+1
-    c->B.owner_mode = om ? (u32)std::min(2, std::max(0, atoi(om))) : 2u;
+    c->B.owner_mode = om ? (u32)std::min(3, std::max(0, atoi(om))) : 2u;
     // SYMMETRY: the states of one orbit must meet at one owner, so the owner is
     // a function of the canonical fingerprint (server words differ across the orbit)
     if (c->sh.sym) c->B.owner_mode = 0;

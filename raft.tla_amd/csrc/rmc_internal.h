@@ -35,7 +35,7 @@ struct DevBufs {
     Counters* ctr;
     // sharded mode (rank/world > 1 GPU processes; single mode: rank 0, world 1)
     u32 rank, world;
-    u32 owner_mode;            // 0: by fingerprint, 1: by server 0 word, 2: by servers 0+1 words (default)
+    u32 owner_mode;            // 0: by fingerprint, 1: by server 0 word, 2: by servers 0+1 words (default), 3: all words
     u64 ref_tag;               // (rank << 48): parent refs are global (rank, index)
     u64* sent;                 // lossy cache of fingerprints already shipped to their owner
     u64 smask;                 // sent-cache slots - 1

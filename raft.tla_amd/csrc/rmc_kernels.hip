@@ -414,25 +414,45 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable 
 // fingerprint's own component mix hS(w, i): the expansion kernel has the
 // parent's mixes and the new word's mix at hand, so routing a successor costs
 // no extra mix64 (and no extra registers) in its lane loop.
-__device__ __forceinline__ u32 owner_state(u64 key, u64 w0, u64 w1, const DevBufs& B) {
+// Number of server words the owner hashes: mode 1 one, 2 two, 3 all S.
+template <int S>
+__device__ __forceinline__ int owner_words(const DevBufs& B) {
+    return B.owner_mode >= 3 ? S : (int)B.owner_mode;
+}
+template <int S>
+__device__ __forceinline__ u32 owner_state(u64 key, const u64 (&w)[S], const DevBufs& B) {
     if (B.owner_mode == 0) return owner_of(key, B.world);
-    return owner_of(hS(w0, 0u) + (B.owner_mode == 2 ? hS(w1, 1u) : 0ull), B.world);
+    const int nw = owner_words<S>(B);
+    u64 h = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) h += i < nw ? hS(w[i], (u32)i) : 0ull;
+    return owner_of(h, B.world);
+}
+// Owner of a successor from the parent's words (kernels without the parent's mixes).
+template <int S>
+__device__ __forceinline__ u32 owner_succ_w(u64 key, const Delta& d, const u64 (&w)[S], const DevBufs& B) {
+    if (B.owner_mode == 0) return owner_of(key, B.world);
+    if (d.srv < 0 || d.srv >= owner_words<S>(B)) return B.rank;
+    u64 ws[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) ws[i] = i == d.srv ? d.w_new : w[i];
+    return owner_state<S>(key, ws, B);
 }
 // Owner of a successor from the parent's word mixes (pm.hw) and the new word's
-// mix hn (delta_fp_pre / delta_hash_pre): a lane that leaves servers 0 and 1
-// alone (mode 2; mode 1: server 0) keeps its parent's owner — this rank, since
-// a state is stored by its owner.
+// mix hn (delta_fp_pre / delta_hash_pre): a lane that leaves the hashed words
+// alone keeps its parent's owner — this rank, since a state is stored by its
+// owner.
 template <int S, int K>
 __device__ __forceinline__ u32 owner_succ(u64 key, const Delta& d, const ParentMix<S, K>& pm, u64 hn,
                                           const DevBufs& B) {
     if (B.world == 1) return 0;
     if (B.owner_mode == 0) return owner_of(key, B.world);
-    if (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2)) {
-        const u64 a = d.srv == 0 ? hn : pm.hw[0];
-        const u64 b = B.owner_mode == 2 ? (d.srv == 1 ? hn : pm.hw[1]) : 0ull;
-        return owner_of(a + b, B.world);
-    }
-    return B.rank;
+    const int nw = owner_words<S>(B);
+    if (d.srv < 0 || d.srv >= nw) return B.rank;
+    u64 h = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) h += i < nw ? (i == d.srv ? hn : pm.hw[i]) : 0ull;
+    return owner_of(h, B.world);
 }
 
 template <int S, int K>
@@ -826,9 +846,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                                 s_own[b][threadIdx.x] = (uint8_t)(
                                     B.world == 1 ? 0u
                                     : B.owner_mode == 0 ? owner_of(key, B.world)
-                                    : (d.srv == 0 || (d.srv == 1 && B.owner_mode == 2))
-                                        ? owner_state(key, d.srv == 0 ? d.w_new : w[0], d.srv == 1 ? d.w_new : w[1], B)
-                                        : B.rank);
+                                    : owner_succ_w<S>(key, d, w, B));
                         }
                     }
                 }
@@ -1376,7 +1394,7 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
         key &= P.fp_mask;  // ~0 unless a verification test weakens the fingerprint
         key = key ? key : 1ull;
         // sharded mode: only the owner of an initial state stores it
-        if (owner_state(key, w[0], w[1], B) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        if (owner_state<S>(key, w, B) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
     }
     Delta d;  // identity delta: the state itself
     d.srv = -1; d.rm = -1; d.has_add = 0; d.add = 0; d.en = 1; d.w_new = 0;
