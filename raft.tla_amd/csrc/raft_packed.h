@@ -678,6 +678,18 @@ RMC_HD u32 state_class(const u64* ws) {
     if constexpr (S <= 3) return roles;
     return lead | (cand << S);
 }
+// The finer window-sort class (< 256): the roles and the number of messages,
+// whose slots decide the Receive / Duplicate / Drop lanes a state enables.
+template <int S, int K>
+RMC_HD u32 state_class_fine(const u64* ws) {
+    const u32* ms = reinterpret_cast<const u32*>(ws + S);
+    int nmsg = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) nmsg += ms[q] ? 1 : 0;
+    const u32 c = state_class<S>(ws);
+    if constexpr (S <= 3) return c * 9u + (u32)(nmsg < 8 ? nmsg : 8);  // <= 242
+    return c | ((u32)(nmsg < 3 ? nmsg : 3) << (S + 1));                 // S + 3 <= 8 bits
+}
 template <int S, int K>
 RMC_HD u64 lane_superset(const u64 (&w)[S], const u32 (&m)[K], int V) {
     typedef Lanes<S, K> L;

@@ -639,7 +639,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
           bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
-          bool MARK = false, int WTILES = 8, bool UPROBE = false>
+          bool MARK = false, int WTILES = 8, bool UPROBE = false, bool WFINE = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -660,7 +660,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     constexpr int WT = WSORT ? WTILES : 1;  // tiles per window
     __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
     __shared__ uint8_t s_wcls[WSORT ? 256 * WT : 1];  // WSORT: class of each window position
-    __shared__ u32 s_wbin[WSORT ? 64 : 1];            // WSORT: class counters / cursors
+    constexpr int NBIN = WFINE ? 256 : 64;            // WFINE: roles x messages classes
+    __shared__ u32 s_wbin[WSORT ? NBIN : 1];          // WSORT: class counters / cursors
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
@@ -697,26 +698,32 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     if constexpr (WSORT) {
         wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
         __syncthreads();  // the previous window's s_ord is consumed
-        if (threadIdx.x < 64) s_wbin[threadIdx.x] = 0;
+        if (threadIdx.x < NBIN) s_wbin[threadIdx.x] = 0;
         __syncthreads();
         for (int k = 0; k < (int)wt; ++k) {
             const u32 p = (u32)k * 256u + threadIdx.x;
             if (p < wn) {
-                const u32 c = state_class<S>(reinterpret_cast<const u64*>(B.store + (lo + win + p) * (u64)NW));
+                const u64* st = reinterpret_cast<const u64*>(B.store + (lo + win + p) * (u64)NW);
+                const u32 c = WFINE ? state_class_fine<S, K>(st) : state_class<S>(st);
                 s_wcls[p] = (uint8_t)c;
                 atomicAdd(&s_wbin[c], 1u);
             }
         }
         __syncthreads();
-        if (threadIdx.x < 64) {  // exclusive scan of the 64 counters (wave 0)
-            const u32 v = s_wbin[threadIdx.x];
-            u32 incl = v;
+        if (threadIdx.x < 64) {  // exclusive scan of the counters (wave 0; NBIN / 64 per lane)
+            constexpr int PER = NBIN / 64;
+            u32 v[PER], tot = 0;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) { v[q] = s_wbin[threadIdx.x * PER + q]; tot += v[q]; }
+            u32 incl = tot;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
                 const u32 t = (u32)__shfl_up((int)incl, off);
                 if ((int)threadIdx.x >= off) incl += t;
             }
-            s_wbin[threadIdx.x] = incl - v;
+            u32 ex = incl - tot;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) { s_wbin[threadIdx.x * PER + q] = ex; ex += v[q]; }
         }
         __syncthreads();
         for (int k = 0; k < (int)wt; ++k) {
@@ -1056,12 +1063,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
 template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8,
-          bool UP = false>
+          bool UP = false, bool WF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT, UP>(P, PT, B,
-                                                                                                           lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT, UP, WF>(
+            P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1686,6 +1693,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, true>)))), dim3(256), 0, st, P,
                                PT, B, a, b);
+        } else if (S == 3 && K == 4 && expand_variant() == 10) {  // A/B (bench shape): roles x messages classes
+            if constexpr (S == 3 && K == 4)
+                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, true>),
+                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false,
+                                                                                         false, 16, false, true>)))),
+                                   dim3(256), 0, st, P, PT, B, a, b);
         } else if (S == 3 && K == 4 && expand_variant() == 9) {  // A/B (bench shape): unconditional probe loads
             if constexpr (S == 3 && K == 4)
                 hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, true>),
