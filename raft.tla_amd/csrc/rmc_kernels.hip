@@ -639,7 +639,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
           bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
-          bool MARK = false, int WTILES = 8, bool UPROBE = false, bool WFINE = false>
+          bool MARK = false, int WTILES = 8, bool UPROBE = false, bool WFINE = true>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -660,7 +660,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     constexpr int WT = WSORT ? WTILES : 1;  // tiles per window
     __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
     __shared__ uint8_t s_wcls[WSORT ? 256 * WT : 1];  // WSORT: class of each window position
-    constexpr int NBIN = WFINE ? 256 : 64;            // WFINE: roles x messages classes
+    constexpr int NBIN = WFINE ? 256 : 64;            // WFINE (default): roles x message-count classes
     __shared__ u32 s_wbin[WSORT ? NBIN : 1];          // WSORT: class counters / cursors
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
 template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8,
-          bool UP = false, bool WF = false>
+          bool UP = false, bool WF = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
@@ -1593,7 +1593,9 @@ static u64 resident_grid(const void* k) {
 // profiles/r02/ab/, profiles/r03/ab/): 6 (default) = commuting-diamond
 // skipping (7.18 G instead of 10.41 G probes per MCraftBench BFS: 315 vs
 // 337-340 ms) on the lane-superset walk over class-sorted windows of 16 tiles
-// (308.2-309.3 vs 310.9-312.4 ms for 8 tiles, variant 8, same box);
+// (308.2-309.3 vs 310.9-312.4 ms for 8 tiles, variant 8, same box), classes by
+// roles x message count (270.8-279.6 vs 279.4-286.0 ms by roles only, variant
+// 10; profiles/r03/ab/window_classes_r03ab2.jsonl);
 // 7 = 6 with the stutter, CONSTRAINT and commuting-diamond decisions taken
 // before the lane hashes (317-322 ms: the split costs more than the hashes
 // it saves); without the diamond, 6 is the round-2 kernel: the lane-superset walk over class-sorted
@@ -1693,11 +1695,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, true>)))), dim3(256), 0, st, P,
                                PT, B, a, b);
-        } else if (S == 3 && K == 4 && expand_variant() == 10) {  // A/B (bench shape): roles x messages classes
+        } else if (S == 3 && K == 4 && expand_variant() == 10) {  // A/B (bench shape): window classes by roles only
             if constexpr (S == 3 && K == 4)
-                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, true>),
+                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, false>),
                                    dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false,
-                                                                                         false, 16, false, true>)))),
+                                                                                         false, 16, false, false>)))),
                                    dim3(256), 0, st, P, PT, B, a, b);
         } else if (S == 3 && K == 4 && expand_variant() == 9) {  // A/B (bench shape): unconditional probe loads
             if constexpr (S == 3 && K == 4)
