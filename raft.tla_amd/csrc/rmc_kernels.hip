@@ -1676,14 +1676,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             else if (sym_variant() == 1)
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
-            else if (sym_variant() == 4)
+            else if (sym_variant() == 4)  // default: windows of 16 tiles (72.1-72.7 vs 75.0-75.3 ms for 8)
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true, 16>), dim3((unsigned)g), dim3(256), 0, st,
+                                   P, PT, B, a, b);
+            else if (sym_variant() == 5)  // windows of 8 tiles
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else if (S == 3 && K == 4 && sym_variant() == 5) {  // A/B (bench shape): windows of 16 tiles
-                if constexpr (S == 3 && K == 4)
-                    hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true, 16>), dim3((unsigned)g), dim3(256), 0,
-                                       st, P, PT, B, a, b);
-            }
             else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
