@@ -639,7 +639,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 // diamonds"; P.diamond = 0 turns it off at run time).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
           bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
-          bool MARK = false, int WTILES = 8, bool UPROBE = false, bool WFINE = true>
+          bool MARK = false, int WTILES = 8, bool UPROBE = false, bool WFINE = true, int PIPE = 0>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -657,6 +657,13 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     static_assert(!SORT || BATCH * 7 <= 64, "SORT packs a batch's lanes 7 bits each into one u64");
     static_assert(!(SORT && FSORT && (SYM || DIST)), "class-sorted flushes are built for the plain kernel only");
     static_assert(!WSORT || SORT, "WSORT needs SORT");
+    // PIPE: a probe's load is issued as soon as its key is known, so the loads
+    // overlap the lane code of the batch's later lanes (266-272 vs 271-279 ms
+    // per bench BFS, profiles/r03/ab/probe_issue_r03pipe*.jsonl).  Measured and
+    // removed: issuing per half batch (268-274 ms), and the window's next state
+    // prefetched into registers as well (269-272 ms, 2 VGPRs spilled).
+    static_assert(PIPE == 0 || (!SYM && !VERIFY && !SENTC && !UPROBE), "PIPE: the plain and marker kernels");
+    // (the marker kernel measured no gain from it at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int WT = WSORT ? WTILES : 1;  // tiles per window
     __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
     __shared__ uint8_t s_wcls[WSORT ? 256 * WT : 1];  // WSORT: class of each window position
@@ -789,6 +796,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     lp |= ln << (7 * b);
                 }
             }
+            u64 cur_p[PIPE ? BATCH : 1];  // PIPE: the probes issued during (a)
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
             // Rolled under SYMMETRY: one copy of the canonicalisation in flight.
             // (Rolling the plain kernel too, one copy of the lane code instead of
@@ -858,6 +866,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     }
                 }
                 s_key[b][threadIdx.x] = key;
+                if constexpr (PIPE != 0) cur_p[b] = key ? B.table[key & B.tmask] : 0ull;
                 if constexpr (TIEDEFER) {  // one queue atomic per wave and lane, not per tied successor
                     const u64 bal = __ballot(tied);
                     if (bal) {
@@ -887,7 +896,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 } else {
                     // UPROBE: every lane loads (a lane without a key reads slot 0, a
                     // valid address), so the loads need no exec-mask branches
-                    cur[b] = (UPROBE || key[b]) ? B.table[key[b] & B.tmask] : 0ull;
+                    if constexpr (PIPE != 0) cur[b] = cur_p[PIPE ? b : 0];
+                    else cur[b] = (UPROBE || key[b]) ? B.table[key[b] & B.tmask] : 0ull;
                 }
             }
 #pragma unroll
@@ -1063,11 +1073,11 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
 // class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
 template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8,
-          bool UP = false, bool WF = true>
+          bool UP = false, bool WF = true, int PI = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT, UP, WF>(
+        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT, UP, WF, PI>(
             P, PT, B, lo, hi);
 }
 
@@ -1606,6 +1616,8 @@ static u64 resident_grid(const void* k) {
 // instead of windows (322 ms).  Measured and removed: mixes recomputed per lane
 // (−2.5 %), 6 waves/SIMD, the delta loop rolled, 5-wave caps of 4 and 6 (spills),
 // flushes and windows both sorted.
+// Round 3, last: 6 issues each probe's load as soon as its key is known (PIPE);
+// 14 is the same kernel issuing the batch's 8 loads after its lane code.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
@@ -1639,6 +1651,8 @@ static int sym_variant() {
 // diamonds decided before hashing (round-3 start, 366 ms); 0 = every lane.
 // Measured and removed: 3 waves/SIMD, 6 probes in flight, the owner decided
 // in the flush (390 ms: a reservation atomic per 64 entries).
+// Measured and removed: 6 with the probe loads issued during the lane code
+// (PIPE; 308.7-309.7 vs 307.4-308.7 ms at one rank, no gain).
 static int dist_variant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_VARIANT");
@@ -1708,7 +1722,15 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {  // windows of 8 tiles (round-2 size)
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false>)))), dim3(256), 0, st, P, PT,
                                B, a, b);
-        } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {  // default: windows of 16 tiles (4096 states)
+        } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
+            // default: windows of 16 tiles (4096 states), probe loads issued during the
+            // lane code where the registers allow it (K = 8 shapes would spill 10-13 VGPRs)
+            constexpr int PI = K <= 4 ? 1 : 0;
+            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, true, PI>),
+                               dim3(eg(reinterpret_cast<const void*>(
+                                   &(k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, true, PI>)))),
+                               dim3(256), 0, st, P, PT, B, a, b);
+        } else if (expand_variant() == 14 && Lanes<S, K>::N <= 64) {  // A/B: 6 with the probes issued after the batch
             hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, false, 16>)))), dim3(256), 0,
                                st, P, PT, B, a, b);
         } else {  // 1, and shapes with more than 64 lanes
