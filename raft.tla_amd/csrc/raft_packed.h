@@ -831,9 +831,16 @@ RMC_HD void materialise(const u64 (&w)[S], const u32 (&m)[K], const Delta& d, u6
 // levels and depth are unchanged (tests/native/diamond_model.cpp checks it
 // on whole BFS runs).  Not under SYMMETRY (canonical representatives break
 // the instance order).
+// Footprint word: bits 0-29 the message a acted on, 30-59 the message a added
+// (both full 30-bit messages), 60-63 the flags below.  Every bit is taken.
 constexpr u64 FOOT_VALID = 1ull << 63, FOOT_ACT = 1ull << 62, FOOT_ADD = 1ull << 61, FOOT_CONSUMED = 1ull << 60;
-// sharded verification records only: the owner had seen this key (compare, do not store)
-constexpr u64 FOOT_SEEN = 1ull << 59;
+constexpr u64 FOOT_MSG_BITS = (u64)MSG_MASK | ((u64)MSG_MASK << 30);
+static_assert((FOOT_MSG_BITS & (FOOT_VALID | FOOT_ACT | FOOT_ADD | FOOT_CONSUMED)) == 0,
+              "footprint flags overlap the message fields");
+// Sharded verification records only: the owner had seen this key (compare, do
+// not store).  It lives in the record's global parent-ref word, whose bits
+// 48-55 hold the rank (< kMaxWorld = 64) and 40-47 the lane: bit 63 is free.
+constexpr u64 REF_SEEN = 1ull << 63;
 
 // Family of a lane from the runtime offsets (wave-uniform lanes: scalar compares).
 RMC_HD int lane_family(const Params& P, int lane) {

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -582,7 +583,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (resume) {
         c->res.left_on_queue = 0;
         c->res.seconds = 0;
-        HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
+        HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
         c->h_ctr->count = c->level_start.back();
         if (int rc = reset_counters(c, true)) return rc;
         depth = c->resume_depth;
@@ -604,7 +605,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     }
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
-    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (int rc = reset_counters(c, false)) return rc;
 
     // ---- Init (raft.tla:125-129): one initial state
@@ -775,9 +776,13 @@ int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
 // of levels 1..depth.  The fingerprint set is not written: rmc_recover rebuilds
 // it from the states (k_rehash), one pass over the store.
 namespace {
+// The header embeds the ABI structs rmc_config and rmc_result, so its size is
+// written too and must match: a struct that grows changes kCkptVersion.
+constexpr uint32_t kCkptVersion = 3;  // 3: rmc_result with parked / exchange_wait_seconds
 struct CkptHeader {
     char magic[8];
     uint32_t version, nw;
+    uint32_t header_bytes, pad_;
     rmc_config cfg;
     uint64_t count, nlevels;
     int32_t depth;
@@ -835,7 +840,8 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     CkptHeader h{};
     h.shard = c->dist.on ? (c->dist.rank | (c->dist.world << 16)) : 0;
     memcpy(h.magic, kCkptMagic, 8);
-    h.version = 2;  // 2: rmc_config with device_window, spilled checkpoints
+    h.version = kCkptVersion;
+    h.header_bytes = (uint32_t)sizeof(CkptHeader);
     h.nw = (uint32_t)c->NW;
     h.cfg = c->cfg;
     h.count = c->level_start.back();
@@ -870,8 +876,17 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     CkptHeader h{};
     int rc = 0;
     std::vector<u64> ls;
-    if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 2)
+    // the fixed prefix first (magic, version): an older version is refused by
+    // name before its differently laid-out remainder is interpreted
+    const size_t pre = offsetof(CkptHeader, header_bytes);
+    if (fread(&h, pre, 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0)
         rc = fail(c, RMC_E_IO, "recover: not an rmc checkpoint");
+    else if (h.version != kCkptVersion)
+        rc = fail(c, RMC_E_IO, "recover: checkpoint format version " + std::to_string(h.version) +
+                                   " (this build reads version " + std::to_string(kCkptVersion) +
+                                   "); recreate the checkpoint with this build");
+    else if (fread((char*)&h + pre, sizeof h - pre, 1, f) != 1 || h.header_bytes != (uint32_t)sizeof(CkptHeader))
+        rc = fail(c, RMC_E_IO, "recover: checkpoint header truncated or of another layout");
     else if (h.shard != (c->dist.on ? (c->dist.rank | (c->dist.world << 16)) : 0))
         rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another shard layout (rank / world), or of a "
                                   "single-GPU run recovered on a sharded ctx or the reverse");
@@ -920,7 +935,7 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     // diamond skipping (FOOT_VALID clear), the levels after it with
     HIPCHK(c, hipMemsetAsync(c->spill.on ? c->spill.foot : c->B.foot, 0,
                              (c->spill.on ? c->spill.win : c->B.cap) * 8, c->st));
-    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
     if (s) get(c->spill.h_parent, s * 8);
     if (!rc) rc = move_file(c, f, dparent, (h.count - s) * 8, false);

@@ -206,7 +206,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (c->B.sent) HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
     const bool verify = c->sh.verify;
     if (verify && !resume) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
-    HIPCHK(c, set_fp_salt(c->cfg.seed, c->st));
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (resume) c->h_ctr->count = c->level_start.back();
     if (int rc = reset_counters(c, resume)) return rc;
     // ---- Init (raft.tla:125-129): stored by its owner only

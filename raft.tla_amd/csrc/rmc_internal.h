@@ -115,8 +115,9 @@ hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st);
 // sent-cache B.sent, or send markers in the fingerprint set?
 bool dist_uses_sent_cache();
 
-// Fingerprint salt for the kernels of this device (0 = default hash).
-hipError_t set_fp_salt(u64 seed, hipStream_t st);
+// Fingerprint salt for the kernels of shape sh on this device (0 = default
+// hash); returns after the copy (the staging value lives on the caller's stack).
+hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st);
 
 // Random-probe microbenchmark over table[mask + 1] (mode 0 loads, 1 CAS).
 hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st);

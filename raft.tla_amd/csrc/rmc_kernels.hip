@@ -1181,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
 // the record {state, global parent ref | lane << 40} into owner d's state
 // outbox.  Grid over (destination, key index).
 // Full-state verification (B.sidx set): every key is shipped, the ones the
-// owner had seen flagged FOOT_SEEN, so the owner compares them with its state.
+// owner had seen flagged REF_SEEN (parent-ref word), so the owner compares them with its state.
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, const DevBufs B, const uint8_t* reply,
                                                             u64 per_dest, u64 i0) {
@@ -1212,10 +1212,10 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
         materialise<S, K>(w, m, dl, wo, mo);
         u32* r = B.st_out + ((u64)d * B.scap + slot) * (u64)RW;
         store_state<S, K>(r, wo, mo);
-        const u64 ref = B.ref_tag | ((u64)lane << 40) | pidx;
+        const u64 ref = B.ref_tag | ((u64)lane << 40) | pidx | (seen ? REF_SEEN : 0ull);
         r[NW] = (u32)ref;
         r[NW + 1] = (u32)(ref >> 32);
-        const u64 ft = make_foot<S, K>(m, lane, dl, P) | (seen ? FOOT_SEEN : 0ull);
+        const u64 ft = make_foot<S, K>(m, lane, dl, P);
         r[NW + 2] = (u32)ft;
         r[NW + 3] = (u32)(ft >> 32);
     }
@@ -1232,7 +1232,7 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
     for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < n; t0 += (u64)gridDim.x * 256ull) {
         const u64 t = t0 + threadIdx.x;
         // verification mode also receives the states the owner had seen (compared by k_compare_remote)
-        const bool live = t < n && !(inbox[t * (u64)RW + NW + 3] & (u32)(FOOT_SEEN >> 32));
+        const bool live = t < n && !(inbox[t * (u64)RW + NW + 1] & (u32)(REF_SEEN >> 32));
         const u64 bal = __ballot(live);
         if (!bal) continue;
         const int leader = __ffsll((long long)bal) - 1;
@@ -1251,7 +1251,7 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
         load_state<S, K>(r, w, m);
         store_state<S, K>(B.store + ni * (u64)NW, w, m);
         const u64 ref = (u64)r[NW] | ((u64)r[NW + 1] << 32);
-        B.parent[ni] = ref & ~(0xFFull << 40);
+        B.parent[ni] = ref & ~((0xFFull << 40) | REF_SEEN);
         B.act[ni] = (uint8_t)(ref >> 40);
         B.foot[ni] = (u64)r[NW + 2] | ((u64)r[NW + 3] << 32);
         const int v = check_invariants<S, K>(w, m, P);
@@ -1260,7 +1260,7 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
 }
 
 // Sharded full-state verification, owner side: every received record the
-// owner had already seen (FOOT_SEEN) is compared with the stored state that
+// owner had already seen (REF_SEEN) is compared with the stored state that
 // owns its fingerprint's slot (published by k_publish before this runs); a
 // difference is a fingerprint collision.
 template <int S, int K, bool SYM>
@@ -1270,7 +1270,7 @@ __global__ __launch_bounds__(256) void k_compare_remote(const Params P, const Pe
     u64 vchk = 0, vcol = 0;
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n; t += (u64)gridDim.x * 256ull) {
         const u32* r = inbox + t * (u64)RW;
-        if (!(r[NW + 3] & (u32)(FOOT_SEEN >> 32))) continue;
+        if (!(r[NW + 1] & (u32)(REF_SEEN >> 32))) continue;
         PackedState<S, K> o;
         load_state<S, K>(r, o.w, o.m);
         const u64 key = verify_key<S, K, SYM>(o.w, o.m, P, PT);
@@ -1834,9 +1834,12 @@ RMC_SHAPES(RMC_SHAPE_DECLS)
         return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, st);        \
     }                                                                                                           \
     hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, hipStream_t st) {                                        \
-        static u64 h_salt;                                                                                      \
-        h_salt = salt;                                                                                          \
-        return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &h_salt, sizeof h_salt, 0, hipMemcpyHostToDevice, st); \
+        /* staged on this call's stack and waited for: concurrent callers (one host */                          \
+        /* thread per GPU in rmc-tlc -gpus N) share no staging buffer */                                        \
+        const u64 h_salt = salt;                                                                                \
+        const hipError_t e =                                                                                    \
+            hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &h_salt, sizeof h_salt, 0, hipMemcpyHostToDevice, st); \
+        return e != hipSuccess ? e : hipStreamSynchronize(st);                                                  \
     }
 #define RMC_DEFINE_SHAPE_(SS, KK) RMC_DEFINE_SHAPE(SS, KK)
 RMC_DEFINE_SHAPE_(RMC_SHAPE_S, RMC_SHAPE_K)
@@ -1846,14 +1849,14 @@ bool dist_uses_sent_cache() {
     return !(v == 6 || v == 7);  // markers live in the fingerprint set
 }
 
-hipError_t set_fp_salt(u64 seed, hipStream_t st) {
+hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st) {
     const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
-    hipError_t e = hipSuccess;
+    // only the ctx's shape object runs its kernels
 #define RMC_SET_SALT(SS, KK) \
-    if ((e = set_fp_salt_shape_##SS##_##KK(salt, st)) != hipSuccess) return e;
+    if (sh.S == SS && sh.K == KK) return set_fp_salt_shape_##SS##_##KK(salt, st);
     RMC_SHAPES(RMC_SET_SALT)
 #undef RMC_SET_SALT
-    return hipStreamSynchronize(st);  // the staged host copies are static per object
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,

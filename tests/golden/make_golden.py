@@ -60,6 +60,10 @@ CONFIGS = {
     "sym_bug_one_leader": (3, 2, 3, 1, 3, 1, 1, 2, 1, 0),
     # config 3, wider bounds (specs/MCraft5Wide.cfg): the first 9 levels
     "s5_wide_prefix9": (5, 2, 3, 2, 4, 1, 0, 1, 0, 9),
+    # 3-entry logs with 2 values: an RVP's mlog then fills the message's top bit
+    # (bit 29), which a sharded record once shared with its "seen" flag
+    "tiny2_log3": (2, 2, 3, 3, 2, 1, 0, 1, 0, 0),
+    "s3_log3_prefix14": (3, 2, 3, 3, 2, 1, 0, 1, 0, 14),
     # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
     "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }

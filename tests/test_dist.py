@@ -68,6 +68,7 @@ def test_host_transport_gloo(nproc, tmp_path):
                                                 ("small", 4, "gloo"), ("s5_prefix9", 2, "gloo"),
                                                 ("small_sym", 2, "gloo"), ("bounded_sym_prefix16", 3, "gloo"),
                                                 ("msgs5_dup2_prefix9", 2, "gloo"), ("s4_prefix10", 3, "gloo"),
+                                                ("tiny2_log3", 2, "gloo"), ("s3_log3_prefix14", 2, "gloo"),
                                                 ("small", 1, "nccl")])
 def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
     """The sharded BFS inside librmc (rmc_shard + rmc_run_bfs), through the C
@@ -167,7 +168,7 @@ def test_sharded_outbox_overflow_is_recovered(case, nproc, overlap, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,nproc", [("small", 2), ("small", 4), ("small_sym", 3)])
+@pytest.mark.parametrize("case,nproc", [("small", 2), ("small", 4), ("small_sym", 3), ("s3_log3_prefix14", 2)])
 def test_sharded_verification(case, nproc, tmp_path):
     """Full-state verification on a sharded search: every
     fingerprint hit, local or at the owner of a remote successor, is compared

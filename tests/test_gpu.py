@@ -52,7 +52,7 @@ def test_kat_first_levels():
 
 BFS_CASES = ["bounded_full", "tiny2", "messages_tiny2", "elections_small", "tiny2_v2", "small", "small_sym", "s3_v1_msgs1", "bounded_prefix14",
              "bounded_sym_prefix16", "msgs5_dup2_prefix9", "s4_prefix10", "s5_prefix9", "isprefix_small",
-             "isprefix_s3v1_log2", "s4_sym_prefix16", "s5_sym_prefix16"]
+             "isprefix_s3v1_log2", "s4_sym_prefix16", "s5_sym_prefix16", "tiny2_log3", "s3_log3_prefix14"]
 
 
 @pytest.mark.parametrize("name", BFS_CASES)
@@ -273,6 +273,14 @@ def test_recover_rejects_another_model(tmp_path):
             ck.recover(str(tmp_path / "ck"))
         with pytest.raises(rmc.RmcError, match="not an rmc checkpoint|cannot open"):
             ck.recover(str(tmp_path / "missing"))
+    # a checkpoint of an older format (version 2: a shorter rmc_result in the
+    # header) is refused by its version, before its fields are read
+    raw = bytearray(open(tmp_path / "ck", "rb").read())
+    raw[8:12] = (2).to_bytes(4, "little")
+    (tmp_path / "ck2").write_bytes(bytes(raw))
+    with rmc.Checker(cfg_from(dict(g["params"], max_depth=5))) as ck:
+        with pytest.raises(rmc.RmcError, match="format version 2"):
+            ck.recover(str(tmp_path / "ck2"))
 
 
 FRONT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "front_models.json")))
