@@ -167,10 +167,13 @@ def host_cpu_info():
             "physical_cores": len(phys) or None, "model": model}
 
 
-def cpu_baseline(cfg, levels, fix_cfg, gpu_fix):
+def cpu_baseline(cfg, levels, fix_cfg, gpu_fix, gpu_levels=None):
     """C oracle (test infrastructure, kind "port") on the host cores this job
     may use: (1) the first `levels` BFS levels of the bench model, (2) a
-    complete fixpoint of `fix_cfg` timed next to the GPU on the same model."""
+    complete fixpoint of `fix_cfg` timed next to the GPU on the same model.
+    gpu_levels: the bench model's per-level (new states, cumulative generated)
+    from one untimed GPU run; `prefix_agree` says whether the oracle's first
+    levels equal them."""
     import rmc
     from tests import oracle_c
     info = host_cpu_info()
@@ -180,15 +183,22 @@ def cpu_baseline(cfg, levels, fix_cfg, gpu_fix):
         return oracle_c.bfs(c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,
                             bug=int(bool(c.flags & rmc.FLAG_BUG_QUORUM)), inv=c.invariants,
                             sym=int(bool(c.flags & rmc.FLAG_SYMMETRY)), threads=threads,
-                            max_levels=max_levels, capacity=capacity)[0]
+                            max_levels=max_levels, capacity=capacity)
 
-    r = run(cfg, levels, 1 << 27)
+    r, ln, _ = run(cfg, levels, 1 << 27)
     out = {"value": r.distinct / r.seconds, "unit": "distinct states/s", "cores": threads, "kind": "port",
            "host": info,
            "sample": f"C oracle (oracle/rmc_oracle.c, exact state set, {threads} threads) BFS levels 1..{r.depth} "
                      f"of the same model: {r.distinct} distinct / {r.generated} generated in {r.seconds:.2f} s"}
+    if gpu_levels is not None:
+        new, gen = gpu_levels
+        d = len(ln)
+        # the GPU's cumulative generated once level d exists (the callback of expanding level d - 1)
+        g_at = gen[d - 2] if 2 <= d <= len(gen) + 1 else None
+        out["prefix_agree"] = new[:d] == ln and g_at == r.generated
+        out["prefix_levels"] = d
     if fix_cfg is not None:
-        f = run(fix_cfg, 0, 1 << 27)
+        f = run(fix_cfg, 0, 1 << 27)[0]
         gd, gg, gdep, gt = gpu_fix
         out["fixpoint"] = {
             "model": gpu_fix_name(fix_cfg), "cpu_distinct": f.distinct, "cpu_generated": f.generated,
@@ -345,6 +355,7 @@ def main(argv=None):
         barrier()
         dt = time.perf_counter() - t0
         salt_check = None
+        gpu_levels = None
         if not sharded:  # untimed: same search under another fingerprint salt
             ck.set_seed(0x5A17ED)
             r2 = ck.run(record_levels=False)
@@ -352,6 +363,9 @@ def main(argv=None):
             salt_check = {"salt": 0x5A17ED, "distinct": r2.distinct, "generated": r2.generated,
                           "depth": r2.depth,
                           "agrees": (r2.distinct, r2.generated, r2.depth) == (D, G, depth)}
+            if rank == 0 and not a.no_cpu:  # untimed: per-level counts for the oracle prefix check
+                ck.run(record_levels=True)
+                gpu_levels = ([1] + [x[3] for x in ck.levels if x[3]], [x[1] for x in ck.levels])
     per_rank = None
     if dist is not None:
         import torch
@@ -445,7 +459,7 @@ def main(argv=None):
                 fk.run(record_levels=False)  # warm
                 fr = fk.run(record_levels=False)
             gpu_fix = (fr.distinct, fr.generated, fr.depth, fr.seconds)
-        out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_levels, fix_cfg, gpu_fix)
+        out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_levels, fix_cfg, gpu_fix, gpu_levels)
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:

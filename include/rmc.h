@@ -24,15 +24,29 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 3
+#define RMC_ABI_VERSION 4
 
-/* Capacity of the packed encoding (DESIGN.md "Packed state"). */
+/* Capacity of the packed encoding (DESIGN.md "Packed state"): the layout the
+ * BFS kernels run on when every bound fits it. */
 #define RMC_MAX_SERVERS 5
 #define RMC_MAX_VALUES 2
 #define RMC_MAX_LOG 3      /* MaxLogLen bound <= 3 */
 #define RMC_MAX_MSGS 8     /* |DOMAIN messages| bound <= 8 */
 #define RMC_MAX_TERM 14    /* MaxTerm bound <= 14 */
 #define RMC_MAX_DUP 3      /* per-message count bound <= 3 */
+/* Capacity of the wide encoding (DESIGN.md "Wide state"): a model with any
+ * bound beyond the packed capacity — or a field no CONSTRAINT bounds, under a
+ * depth bound or in simulation — runs on it (single GPU; no SYMMETRY,
+ * verification or spill).  A CONSTRAINT bound must stay below the wide
+ * capacity; an unbounded field is given the capacity itself, and a successor
+ * beyond it stops the search with RMC_E_CAPACITY naming the field. */
+#define RMC_WIDE_MAX_TERM 255
+#define RMC_WIDE_MAX_LOG 8
+#define RMC_WIDE_MAX_MSGS 16
+#define RMC_WIDE_MAX_DUP 255
+/* Sizes of the decoded state view (rmc_state_view): the wide capacity. */
+#define RMC_VIEW_LOG 8
+#define RMC_VIEW_MSGS 16
 
 /* Error codes. */
 #define RMC_OK 0
@@ -64,9 +78,9 @@ extern "C" {
                                            /* GPU; not with RMC_FLAG_VERIFY_STATES       */
 /* A model without a CONSTRAINT on some field (MCraft.cfg as shipped) runs only
  * under a depth bound (max_depth > 0, TLC -depth).  The front-end then gives
- * each unbounded field the packed capacity (RMC_MAX_TERM, RMC_MAX_LOG,
- * RMC_MAX_MSGS, RMC_MAX_DUP) and sets its bit here; the search stops with
- * RMC_E_CAPACITY, naming the field, the first time a successor needs more
+ * each unbounded field the wide capacity (RMC_WIDE_MAX_TERM, RMC_WIDE_MAX_LOG,
+ * RMC_WIDE_MAX_MSGS, RMC_WIDE_MAX_DUP) and sets its bit here; the search stops
+ * with RMC_E_CAPACITY, naming the field, the first time a successor needs more
  * than the capacity (it is never silently filtered as out of the model). */
 #define RMC_FLAG_UNBOUNDED_TERM (1u << 5)  /* no CONSTRAINT on currentTerm[i]            */
 #define RMC_FLAG_UNBOUNDED_LOG (1u << 6)   /* no CONSTRAINT on Len(log[i])               */
@@ -172,7 +186,7 @@ typedef struct rmc_msg_view {
     int32_t mtype, mterm, msource, mdest;
     int32_t mlastLogTerm, mlastLogIndex;                      /* RequestVoteRequest    */
     int32_t mvoteGranted, mlog_len;                           /* RequestVoteResponse   */
-    rmc_entry mlog[RMC_MAX_LOG];
+    rmc_entry mlog[RMC_VIEW_LOG];
     int32_t mprevLogIndex, mprevLogTerm, mentries_len;        /* AppendEntriesRequest  */
     rmc_entry mentries[1];
     int32_t mcommitIndex;
@@ -186,12 +200,12 @@ typedef struct rmc_state_view {
     int32_t votedFor[RMC_MAX_SERVERS];
     int32_t commitIndex[RMC_MAX_SERVERS];
     int32_t log_len[RMC_MAX_SERVERS];
-    rmc_entry log[RMC_MAX_SERVERS][RMC_MAX_LOG];
+    rmc_entry log[RMC_MAX_SERVERS][RMC_VIEW_LOG];
     uint32_t votesResponded[RMC_MAX_SERVERS];   /* bitmask over server ids */
     uint32_t votesGranted[RMC_MAX_SERVERS];
     int32_t nextIndex[RMC_MAX_SERVERS][RMC_MAX_SERVERS];
     int32_t matchIndex[RMC_MAX_SERVERS][RMC_MAX_SERVERS];
-    rmc_msg_view msgs[RMC_MAX_MSGS];
+    rmc_msg_view msgs[RMC_VIEW_MSGS];
 } rmc_state_view;
 
 /* One successor produced by rmc_expand (differential tests). */
@@ -277,6 +291,14 @@ int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_vi
  * ends that behaviour (counted in `truncated`). */
 #define RMC_SIM_WITHIN_CAPACITY 0
 #define RMC_SIM_TRUNCATE 1
+/* TLC's draw (SimulationWorker): a uniformly random enabled action — each
+ * instance of Restart .. AppendEntries (\E over the constant Server/Value sets
+ * expands into one action each), Receive, DuplicateMessage and DropMessage
+ * (\E m \in DOMAIN messages ranges over the state) one action each — then a
+ * uniformly random successor of that action; beyond the bounds it ends the
+ * behaviour like RMC_SIM_TRUNCATE.  Wide layout only (rmc_simulate refuses it
+ * on the packed one). */
+#define RMC_SIM_TLC 2
 typedef struct rmc_sim_config {
     uint64_t behaviours;       /* random behaviours to run                        */
     int32_t depth;             /* states per behaviour (TLC -depth, default 100)  */

@@ -581,87 +581,17 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
     return 1;
 }
 
-// delta_fp_pre split in two, so a lane can decide to skip its probe before it
-// hashes: the CONSTRAINT and |DOMAIN messages| of the successor ...
-template <int S, int K>
-RMC_HD int delta_bounds_pre(const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d, const Params& P,
-                            int* nmsg_out) {
-    int nmsg = pm.nmsg;
-    if (d.srv >= 0) {
-        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
-        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
-    }
-    if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
-    if (d.has_add) {
-        u32 cnt = 0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) cnt |= (m[q] && (m[q] & MSG_MASK) == d.add) ? m_cnt(m[q]) : 0u;
-        if ((int)cnt + 1 > P.max_dup) return 0;
-        nmsg += cnt ? 0 : 1;
-    }
-    *nmsg_out = nmsg;
-    return nmsg <= P.max_msgs;
-}
-// ... and the fingerprint of a successor known to be in the model (same value as delta_fp_pre).
-template <int S, int K>
-RMC_HD u64 delta_hash_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
-                          u64* hw_new = nullptr) {
-    u64 hh = pm.h0;
-    if (d.srv >= 0) {
-        const u64 wo = selw<S>(w, d.srv);
-        const u64 ho = sel64<S>(pm.hw, d.srv);
-        const u64 hn = d.w_new != wo ? hS(d.w_new, (u32)d.srv) : ho;
-        hh += hn - ho;
-        if (hw_new) *hw_new = hn;
-    }
-    if (d.rm >= 0) {
-        const u32 sl = selm<K>(m, d.rm);
-        hh -= sel64<K>(pm.hm, d.rm);
-        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
-    }
-    if (d.has_add) {
-        int found = -1;
-#pragma unroll
-        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
-        if (found >= 0) hh += hM(selm<K>(m, found) + CNT_ONE) - sel64<K>(pm.hm, found);
-        else hh += hM(d.add | CNT_ONE);
-    }
-    return hh;
-}
-
-// ---- wave homogeneity (the single-GPU expansion kernel) ------------------------------
+// ---- wave homogeneity (the expansion kernels' window sort) ------------------------------
 // A wave walks every action lane that ANY of its 64 states enables, so states
 // of one kind (same roles, same number of messages) should sit together.
-// succ_class: a byte that groups successors by the servers' roles and the
-// number of messages after the delta; the kernel's flush writes each batch
-// of new states sorted by it, so the next level's waves are mostly of one
-// kind.  lane_superset: the lanes a state can possibly enable (role and slot
-// occupancy only; a superset of the enabled lanes); OR-ed over a wave it is
-// the set of lanes the wave must walk.  Both are layout hints: the search is
-// the same whatever they return, as long as lane_superset is a superset.
-template <int S, int K>
-RMC_HD u32 succ_class(const u64 (&w)[S], const u32 (&m)[K], const Delta& d) {
-    int nmsg = 0;
-#pragma unroll
-    for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
-    if (d.rm >= 0 && m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
-    if (d.has_add) {
-        bool found = false;
-#pragma unroll
-        for (int q = 0; q < K; ++q) found |= m[q] && (m[q] & MSG_MASK) == d.add;
-        nmsg += found ? 0 : 1;
-    }
-    u32 roles = 0, lead = 0, cand = 0;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const u32 st = w_st(d.srv == i ? d.w_new : w[i]);
-        roles = roles * 3u + st;
-        lead |= (st == LEADER ? 1u : 0u) << i;
-        cand |= st == CANDIDATE ? 1u : 0u;
-    }
-    if constexpr (S <= 3) return roles * 9u + (u32)(nmsg < 8 ? nmsg : 8);  // <= 242
-    return lead | (cand << S) | ((u32)(nmsg < 3 ? nmsg : 3) << (S + 1));    // S + 3 <= 8 bits
-}
+// state_class_fine: a byte that groups states by the servers' roles and the
+// number of messages; every new state's class is stored next to it (B.cls,
+// one byte) when it is created, and the expansion kernel counting-sorts its
+// windows by it, reading 1 B per state instead of the state.  lane_superset:
+// the lanes a state can possibly enable (role and slot occupancy only; a
+// superset of the enabled lanes); OR-ed over a wave it is the set of lanes the
+// wave must walk.  Both are layout hints: the search is the same whatever they
+// return, as long as lane_superset is a superset.
 // The class of a stored state (the window sort of the expansion kernel): the
 // servers' roles, < 64 values (S <= 3: base-3 digits; else leader mask and
 // whether some server is a candidate).
@@ -678,15 +608,14 @@ RMC_HD u32 state_class(const u64* ws) {
     if constexpr (S <= 3) return roles;
     return lead | (cand << S);
 }
-// The finer window-sort class (< 256): the roles and the number of messages,
-// whose slots decide the Receive / Duplicate / Drop lanes a state enables.
+// The window-sort class (< 256): the roles and the number of messages, whose
+// slots decide the Receive / Duplicate / Drop lanes a state enables.
 template <int S, int K>
-RMC_HD u32 state_class_fine(const u64* ws) {
-    const u32* ms = reinterpret_cast<const u32*>(ws + S);
+RMC_HD u32 state_class_fine(const u64 (&w)[S], const u32 (&m)[K]) {
     int nmsg = 0;
 #pragma unroll
-    for (int q = 0; q < K; ++q) nmsg += ms[q] ? 1 : 0;
-    const u32 c = state_class<S>(ws);
+    for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
+    const u32 c = state_class<S>(w);
     if constexpr (S <= 3) return c * 9u + (u32)(nmsg < 8 ? nmsg : 8);  // <= 242
     return c | ((u32)(nmsg < 3 ? nmsg : 3) << (S + 1));                 // S + 3 <= 8 bits
 }
@@ -863,6 +792,18 @@ RMC_HD u64 make_foot(const u32 (&m)[K], int lane, const Delta& d, const Params& 
     if (lane >= P.off[7]) {
         const int q = lane - (lane < P.off[8] ? P.off[7] : lane < P.off[9] ? P.off[8] : P.off[9]);
         f |= FOOT_ACT | (u64)(selm<K>(m, q) & MSG_MASK);
+        if (d.rm >= 0) f |= FOOT_CONSUMED;
+    }
+    if (d.has_add) f |= FOOT_ADD | ((u64)(d.add & MSG_MASK) << 30);
+    return f;
+}
+
+// make_foot from lane a's descriptor (lanes < 64: no family-offset compares).
+template <int S, int K>
+RMC_HD u64 make_foot_desc(const u32 (&m)[K], u32 desc, const Delta& d) {
+    u64 f = FOOT_VALID;
+    if ((desc & 15u) >= 7u) {
+        f |= FOOT_ACT | (u64)(selm<K>(m, (int)((desc >> 4) & 255u)) & MSG_MASK);
         if (d.rm >= 0) f |= FOOT_CONSUMED;
     }
     if (d.has_add) f |= FOOT_ADD | ((u64)(d.add & MSG_MASK) << 30);
@@ -1203,8 +1144,7 @@ RMC_HD u64 sig_base(u64 w, u32 i) {
 // summed order-free.  Servers are ranked by (part 1, part 2) lexicographically:
 // part 1 leads, so an action that only adds, duplicates or drops a message
 // (RequestVote, AppendEntries, Duplicate, Drop: over half of the lanes) can
-// reorder only servers whose part 1 ties — which keeps most successors in
-// their parent's order (canon_delta_inc's cheap path).
+// reorder only servers whose part 1 ties.
 RMC_HD u32 sig_src(u32 sl) { return (sl & ~0xFCu) * 0x9E3779B1u + 0x7F4A7C15u; }
 RMC_HD u32 sig_dst(u32 sl) { return (sl & ~0xFCu) * 0x85EBCA77u + 0xC2B2AE3Du; }
 template <int S>
@@ -1352,98 +1292,6 @@ RMC_HD u64 canon_delta(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S
     Sig<S> sg;
     signatures<S, K + 1>(bs, ms, sg);
     return canon_sorted<S, K + 1, NOTIE>(ws, ms, sg, codes, np, tied);
-}
-
-// ---- incremental canonical keys (the single-GPU SYMMETRY hot loop) ------------------
-// A delta changes one server word and at most two bag slots, and most deltas
-// leave the servers' signature order alone.  The parent's frame is computed
-// once per expanded state: its per-server message signature sums, its
-// sorting permutation `lo` and the mixes of its components under `lo`.  A lane
-// then updates the signatures of the servers its delta touches, re-ranks them,
-// and — when the successor sorts by the same permutation — gets its key from
-// the parent's as canon_delta would (the same sum of the same mixes, mod 2^64),
-// re-mixing only the changed components: 1-3 mixes instead of S + K + 1.
-template <int S, int K>
-struct SymParent {
-    u64 hw[S];   // hS(perm_word(w[i], lo), pe(lo, i))
-    u64 h0;      // with the slots' hM(perm_slot(m[q], lo)): the fingerprint of lo(parent)
-    u32 ms[S];   // per-server message signature sums (Sig::m)
-    u32 lo;      // the parent's sorting permutation; ~0u when its signatures tie
-};
-template <int S, int K>
-RMC_HD void sym_parent(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], SymParent<S, K>& sp) {
-    Sig<S> sg;
-    signatures<S, K>(base, m, sg);
-#pragma unroll
-    for (int i = 0; i < S; ++i) sp.ms[i] = sg.m[i];
-    u32 tc;
-    const bool tie = sig_rank<S>(sg, &sp.lo, &tc);
-    if (tie) sp.lo = ~0u;
-    const u32 c = tie ? 0u : sp.lo;  // mixes unused when tied
-    sp.h0 = 0;
-#pragma unroll
-    for (int i = 0; i < S; ++i) { sp.hw[i] = hS(perm_word<S>(w[i], c), pe(c, (u32)i)); sp.h0 += sp.hw[i]; }
-#pragma unroll
-    for (int q = 0; q < K; ++q) sp.h0 += hM(perm_slot(m[q], c));
-}
-// Signature sums of one slot moved in (sgn = +1) or out (-1); 0 = no slot.
-template <int S>
-RMC_HD void sig_slot(u32 (&ms)[S], u32 sl, u32 sgn) {
-    const u32 a = sl ? sig_src(sl) * sgn : 0u, b = sl ? sig_dst(sl) * sgn : 0u;
-#pragma unroll
-    for (int i = 0; i < S; ++i) ms[i] += (m_src(sl) == (u32)i ? a : 0u) + (m_dst(sl) == (u32)i ? b : 0u);
-}
-// canon_delta<S, K, true> computed from the parent's frame.  Same result: the
-// key when the successor's signatures do not tie, *tied = 1 when they do.
-template <int S, int K>
-RMC_HD u64 canon_delta_inc(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], const SymParent<S, K>& sp,
-                           const Delta& d, const u32* codes, int np, int* tied) {
-    // the slots the delta changes: rm (old -> new) and the add (old -> new;
-    // old = 0 when the message is not in the bag yet)
-    const u32 rm_old = d.rm >= 0 ? selm<K>(m, d.rm) : 0u;
-    const u32 rm_new = m_cnt(rm_old) > 1 ? rm_old - CNT_ONE : 0u;
-    int found = -1;
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        const u32 sl = q == d.rm ? rm_new : m[q];
-        found = (d.has_add && sl && (sl & MSG_MASK) == d.add) ? q : found;
-    }
-    const u32 add_old = found < 0 ? 0u : found == d.rm ? rm_new : selm<K>(m, found);
-    const u32 add_new = d.has_add ? (found >= 0 ? add_old + CNT_ONE : (d.add | CNT_ONE)) : 0u;
-    Sig<S> sg;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        sg.b[i] = d.srv == i ? sig_base<S>(d.w_new, (u32)i) : base[i];
-        sg.m[i] = sp.ms[i];
-    }
-    sig_slot<S>(sg.m, rm_old, ~0u);
-    sig_slot<S>(sg.m, rm_new, 1u);
-    sig_slot<S>(sg.m, add_old, ~0u);
-    sig_slot<S>(sg.m, add_new, 1u);
-    u32 lo, tc;
-    if (sig_rank<S>(sg, &lo, &tc)) {
-        *tied = 1;
-        return 0;
-    }
-    if (lo == sp.lo && found != d.rm) {  // same frame (rm and add never share a slot; guarded anyway)
-        u64 h = sp.h0;
-        if (d.srv >= 0) h += hS(perm_word<S>(d.w_new, lo), pe(lo, (u32)d.srv)) - sel64<S>(sp.hw, d.srv);
-        // slot mixes are not kept per parent (registers): the old slots are re-mixed
-        h += hM(perm_slot(rm_new, lo)) - hM(perm_slot(rm_old, lo));
-        h += hM(perm_slot(add_new, lo)) - hM(perm_slot(add_old, lo));
-        return h;
-    }
-    // another order: the whole successor under its own sorting permutation
-    u64 ws[S];
-    u32 mq[K + 1];
-#pragma unroll
-    for (int i = 0; i < S; ++i) ws[i] = d.srv == i ? d.w_new : w[i];
-#pragma unroll
-    for (int q = 0; q < K; ++q) mq[q] = q == found ? add_new : q == d.rm ? rm_new : m[q];
-    mq[K] = (d.has_add && found < 0) ? add_new : 0u;
-    (void)codes;
-    (void)np;
-    return fp_perm<S, K + 1>(ws, mq, lo);
 }
 
 }  // namespace rmc

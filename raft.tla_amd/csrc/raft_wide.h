@@ -1,0 +1,564 @@
+// raft_wide.h — the wide state layout: raft.tla states beyond the packed capacity.
+//
+// The packed layout (raft_packed.h) holds terms <= 14 (15 for a successor
+// that the CONSTRAINT rejects), logs of <= 3 entries, <= 8 distinct messages
+// and counts <= 3: enough for every bounded model the BFS benchmarks, not for
+// the reference's own configurations, which bound nothing — MCraft.cfg as
+// shipped (terms grow at raft.tla:146-148, logs at :206-211, counts at
+// :410-412) and Smokeraft.cfg's depth-100 walks (Smokeraft.cfg:46-48).  This
+// layout is one byte per scalar field: terms and counts up to 255, logs of up
+// to 8 entries, up to 16 distinct messages, and a canonical form in which
+// byte equality is TLA+ value equality (fields a message type does not use
+// are 0; the bag is sorted by the message bytes; unused entries and slots are
+// 0).  The search on it is the same BFS (one lane per action instance, at most
+// one successor per lane) without the packed layout's
+// incremental tricks: a lane copies its parent, applies the action, and the
+// fingerprint hashes the whole 568-byte record.  Models whose bounds fit the
+// packed capacity never use it.
+//
+// Compiled for the host (codec) and for gfx950 (rmc_wide.hip).
+#pragma once
+#include <stdint.h>
+
+#include "raft_packed.h"
+
+namespace rmc {
+namespace wide {
+
+constexpr int WS = 5;    // servers held (= the packed layout's)
+constexpr int LW = 8;    // log entries per server
+constexpr int KW = 16;   // distinct messages in the bag
+constexpr int TMAX = 255, CMAX = 255;  // largest term / count a field holds
+constexpr uint8_t NIL = 255;           // votedFor = Nil
+
+struct WEnt {
+    uint8_t term, value;
+};
+// One message record (raft.tla:443-475): 24 bytes, fields a type does not use 0.
+struct alignas(8) WMsg {
+    uint8_t type, term, src, dst;  // mtype, mterm, msource, mdest
+    int8_t a;    // RVQ mlastLogTerm | RVP mvoteGranted | AEQ mprevLogIndex (-1: Smokeraft.tla:35) | AEP msuccess
+    uint8_t b;   // RVQ mlastLogIndex | AEQ mprevLogTerm | AEP mmatchIndex
+    uint8_t c;   // AEQ mcommitIndex
+    uint8_t n;   // AEQ Len(mentries) (<= 1) | RVP Len(mlog)
+    WEnt e[LW];  // AEQ mentries | RVP mlog (= log[i], raft.tla:259)
+};
+static_assert(sizeof(WMsg) == 24, "WMsg layout");
+// The ten variables of raft.tla:31-74.
+struct WState {
+    uint8_t ct[WS], st[WS], vf[WS], ci[WS], len[WS], vR[WS], vG[WS];
+    uint8_t nmsg;
+    uint8_t ni[WS][WS], mi[WS][WS];
+    uint8_t pad[2];
+    WEnt log[WS][LW];
+    uint8_t cnt[KW];
+    WMsg msg[KW];
+};
+constexpr int WWORDS = (int)(sizeof(WState) / 8);
+static_assert(sizeof(WState) % 8 == 0, "WState is read as u64 words");
+
+// Lane table with KW message lanes per bag family.
+struct WLanes {
+    int off[11];
+    RMC_HD void init(int S) {
+        const int n[10] = {S, S, S * S, S, S * VMAX, S, S * S, KW, KW, KW};
+        off[0] = 0;
+        for (int f = 0; f < 10; ++f) off[f + 1] = off[f] + n[f];
+    }
+    RMC_HD int family(int lane) const {
+        int f = 0;
+        while (f < 9 && lane >= off[f + 1]) ++f;
+        return f;
+    }
+};
+
+struct WModel {
+    int S, V;
+    int max_term, max_log, max_msgs, max_dup;  // CONSTRAINT bounds (<= the wide capacity)
+    int unbounded;  // fields with no CONSTRAINT (1 term, 2 log, 4 msgs, 8 dup): beyond the
+                    // wide capacity they are an error, not a filter
+    int bug_quorum, inv_mask;
+    WLanes L;
+};
+
+RMC_HD int wmemcmp(const void* a, const void* b, int n) {
+    const uint8_t* x = (const uint8_t*)a;
+    const uint8_t* y = (const uint8_t*)b;
+    for (int k = 0; k < n; ++k)
+        if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
+    return 0;
+}
+RMC_HD void wzero(void* p, int n) {
+    uint8_t* x = (uint8_t*)p;
+    for (int k = 0; k < n; ++k) x[k] = 0;
+}
+RMC_HD void wcopy(void* d, const void* s, int n) {
+    uint8_t* x = (uint8_t*)d;
+    const uint8_t* y = (const uint8_t*)s;
+    for (int k = 0; k < n; ++k) x[k] = y[k];
+}
+RMC_HD void wcopy_state(WState& d, const WState& s) {
+    u64* x = reinterpret_cast<u64*>(&d);
+    const u64* y = reinterpret_cast<const u64*>(&s);
+    for (int k = 0; k < WWORDS; ++k) x[k] = y[k];
+}
+
+// Message order of the canonical bag: the record as three u64 words compared in
+// turn (a total order; byte equality = record equality).  Host and device sort by it.
+RMC_HD int wmsg_cmp(const WMsg& a, const WMsg& b) {
+    const u64* x = reinterpret_cast<const u64*>(&a);
+    const u64* y = reinterpret_cast<const u64*>(&b);
+    for (int k = 0; k < 3; ++k)
+        if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
+    return 0;
+}
+RMC_HD void wmsg_zero(WMsg& m) {
+    u64* x = reinterpret_cast<u64*>(&m);
+    x[0] = x[1] = x[2] = 0;
+}
+
+RMC_HD int wquorum(const WModel& M, unsigned set) { return 2 * __builtin_popcount(set) > M.S; }  // raft.tla:81
+RMC_HD int wlast_term(const WState& s, int i) { return s.len[i] ? s.log[i][s.len[i] - 1].term : 0; }  // :84
+
+RMC_HD void winit(const WModel& M, WState& s) {  // Init raft.tla:113-129
+    wzero(&s, (int)sizeof s);
+    for (int i = 0; i < M.S; ++i) {
+        s.ct[i] = 1;
+        s.st[i] = FOLLOWER;
+        s.vf[i] = NIL;
+        for (int j = 0; j < M.S; ++j) s.ni[i][j] = 1;
+    }
+}
+
+// Lane results: not enabled, enabled (the successor is in t), or enabled with a
+// successor the wide layout cannot hold — the field it overflows (an error
+// for fields no CONSTRAINT bounds; the packed layout's capacity bits).
+enum : int { W_OFF = 0, W_ON = 1, W_TERM = 2, W_LOG = 3, W_MSGS = 4, W_DUP = 5 };
+RMC_HD int woverflow_bits(int code) { return code >= W_TERM ? 1 << (code - W_TERM) : 0; }
+
+// Would Bag (+) SetToBag({m}) fit (without changing s)?
+RMC_HD int wbag_fits(const WState& s, const WMsg& m) {
+    for (int k = 0; k < s.nmsg; ++k)
+        if (wmsg_cmp(s.msg[k], m) == 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
+    return s.nmsg >= KW ? W_MSGS : W_ON;
+}
+// Bag (+) SetToBag({m}) (raft.tla:88), kept sorted (call after wbag_fits).
+RMC_HD int wbag_add(WState& s, const WMsg& m) {
+    int k = 0;
+    for (; k < s.nmsg; ++k) {
+        const int c = wmsg_cmp(s.msg[k], m);
+        if (c == 0) {
+            if (s.cnt[k] >= CMAX) return W_DUP;
+            s.cnt[k] += 1;
+            return W_ON;
+        }
+        if (c > 0) break;
+    }
+    if (s.nmsg >= KW) return W_MSGS;
+    for (int q = s.nmsg; q > k; --q) {
+        s.msg[q] = s.msg[q - 1];
+        s.cnt[q] = s.cnt[q - 1];
+    }
+    s.msg[k] = m;
+    s.cnt[k] = 1;
+    s.nmsg += 1;
+    return W_ON;
+}
+// Bag (-) SetToBag({m}) (raft.tla:92) of the message in slot k: a count that
+// reaches 0 removes the key (Bags' (-)).
+RMC_HD void wbag_remove_at(WState& s, int k) {
+    if (--s.cnt[k]) return;
+    for (int q = k; q + 1 < s.nmsg; ++q) {
+        s.msg[q] = s.msg[q + 1];
+        s.cnt[q] = s.cnt[q + 1];
+    }
+    s.nmsg -= 1;
+    wmsg_zero(s.msg[s.nmsg]);
+    s.cnt[s.nmsg] = 0;
+}
+RMC_HD void wbag_remove(WState& s, const WMsg& m) {
+    for (int k = 0; k < s.nmsg; ++k)
+        if (wmsg_cmp(s.msg[k], m) == 0) {
+            wbag_remove_at(s, k);
+            return;
+        }
+}
+
+// Lane `lane` on s (raft.tla:136-417, one action instance): W_OFF when the
+// instance is not enabled, W_ON when it is (*t = the successor, if t is
+// given), else the field its successor overflows (W_TERM .. W_DUP; *t is not
+// written).  t == nullptr only evaluates the guard (the simulation's draw).
+RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
+    const int S = M.S;
+    const int f = M.L.family(lane), x = lane - M.L.off[f];
+    switch (f) {
+    case 0: {  // Restart(i) :136-143 — always enabled
+        const int i = x;
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        t->st[i] = FOLLOWER;
+        t->vR[i] = 0;
+        t->vG[i] = 0;
+        t->ci[i] = 0;
+        for (int j = 0; j < S; ++j) {
+            t->ni[i][j] = 1;
+            t->mi[i][j] = 0;
+        }
+        return W_ON;
+    }
+    case 1: {  // Timeout(i) :146-154
+        const int i = x;
+        if (s.st[i] != FOLLOWER && s.st[i] != CANDIDATE) return W_OFF;
+        if (s.ct[i] >= TMAX) return W_TERM;
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        t->st[i] = CANDIDATE;
+        t->ct[i] = (uint8_t)(s.ct[i] + 1);
+        t->vf[i] = NIL;
+        t->vR[i] = 0;
+        t->vG[i] = 0;
+        return W_ON;
+    }
+    case 2: {  // RequestVote(i, j) :157-166 (no i /= j guard)
+        const int i = x / S, j = x % S;
+        if (s.st[i] != CANDIDATE || ((s.vR[i] >> j) & 1u)) return W_OFF;
+        WMsg m;
+        wmsg_zero(m);
+        m.type = RVQ;
+        m.term = s.ct[i];
+        m.a = (int8_t)wlast_term(s, i);
+        m.b = s.len[i];
+        m.src = (uint8_t)i;
+        m.dst = (uint8_t)j;
+        const int fit = wbag_fits(s, m);
+        if (fit != W_ON || !t) return fit;
+        wcopy_state(*t, s);
+        return wbag_add(*t, m);
+    }
+    case 3: {  // BecomeLeader(i) :195-203
+        const int i = x;
+        if (s.st[i] != CANDIDATE) return W_OFF;
+        if (M.bug_quorum ? s.vG[i] == 0 : !wquorum(M, s.vG[i])) return W_OFF;
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        t->st[i] = LEADER;
+        for (int j = 0; j < S; ++j) {
+            t->ni[i][j] = (uint8_t)(s.len[i] + 1);
+            t->mi[i][j] = 0;
+        }
+        return W_ON;
+    }
+    case 4: {  // ClientRequest(i, v) :206-213
+        const int i = x / VMAX, v = x % VMAX;
+        if (v >= M.V || s.st[i] != LEADER) return W_OFF;
+        if (s.len[i] >= LW) return W_LOG;
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        t->log[i][s.len[i]].term = s.ct[i];
+        t->log[i][s.len[i]].value = (uint8_t)v;
+        t->len[i] = (uint8_t)(s.len[i] + 1);
+        return W_ON;
+    }
+    case 5: {  // AdvanceCommitIndex(i) :219-236
+        const int i = x;
+        if (s.st[i] != LEADER) return W_OFF;
+        if (!t) return W_ON;
+        int best = 0;
+        for (int idx = 1; idx <= s.len[i]; ++idx) {
+            unsigned agree = 1u << i;
+            for (int q = 0; q < S; ++q)
+                if (s.mi[i][q] >= idx) agree |= 1u << q;
+            if (wquorum(M, agree)) best = idx;  // Max(agreeIndexes)
+        }
+        wcopy_state(*t, s);
+        if (best > 0 && s.log[i][best - 1].term == s.ct[i]) t->ci[i] = (uint8_t)best;
+        return W_ON;
+    }
+    case 6: {  // AppendEntries(i, j) :171-192
+        const int i = x / S, j = x % S;
+        if (i == j || s.st[i] != LEADER) return W_OFF;
+        const int nidx = s.ni[i][j], len = s.len[i];
+        const int prev = nidx - 1;
+        const int last = len < nidx ? len : nidx;  // Min({Len(log[i]), nextIndex[i][j]})
+        WMsg m;
+        wmsg_zero(m);
+        m.type = AEQ;
+        m.term = s.ct[i];
+        m.a = (int8_t)prev;
+        m.b = (uint8_t)((prev > 0 && prev <= len) ? s.log[i][prev - 1].term : 0);
+        if (nidx <= last) {  // SubSeq(log[i], nextIndex, last): 0 or 1 entry
+            m.n = 1;
+            m.e[0] = s.log[i][nidx - 1];
+        }
+        m.c = (uint8_t)(s.ci[i] < last ? s.ci[i] : last);
+        m.src = (uint8_t)i;
+        m.dst = (uint8_t)j;
+        const int fit = wbag_fits(s, m);
+        if (fit != W_ON || !t) return fit;
+        wcopy_state(*t, s);
+        return wbag_add(*t, m);
+    }
+    case 7: {  // Receive(m) :388-403 for bag slot x
+        if (x >= s.nmsg) return W_OFF;
+        const WMsg& m = s.msg[x];
+        const int i = m.dst, j = m.src, ct = s.ct[i];
+        if (m.term > ct) {  // UpdateTerm :373-379 — m stays
+            if (!t) return W_ON;
+            wcopy_state(*t, s);
+            t->ct[i] = m.term;
+            t->st[i] = FOLLOWER;
+            t->vf[i] = NIL;
+            return W_ON;
+        }
+        if (m.type == RVQ) {  // HandleRequestVoteRequest :244-263
+            const int lt = wlast_term(s, i);
+            const int logok = m.a > lt || (m.a == lt && m.b >= s.len[i]);
+            const int grant = m.term == ct && logok && (s.vf[i] == NIL || s.vf[i] == j);
+            WMsg r;
+            wmsg_zero(r);
+            r.type = RVP;
+            r.term = (uint8_t)ct;
+            r.src = (uint8_t)i;
+            r.dst = (uint8_t)j;
+            r.a = (int8_t)grant;
+            r.n = s.len[i];
+            for (int e = 0; e < s.len[i]; ++e) r.e[e] = s.log[i][e];
+            const int fit = wbag_fits(s, r);  // Reply :102-103: add the response, then remove the request
+            if (fit != W_ON || !t) return fit;
+            const WMsg q = m;
+            wcopy_state(*t, s);
+            if (grant) t->vf[i] = (uint8_t)j;
+            wbag_add(*t, r);
+            wbag_remove(*t, q);
+            return W_ON;
+        }
+        if (m.type == RVP) {
+            if (!t) return W_ON;
+            wcopy_state(*t, s);
+            if (m.term == ct) {  // HandleRequestVoteResponse :267-279
+                t->vR[i] |= (uint8_t)(1u << j);
+                if (m.a) t->vG[i] |= (uint8_t)(1u << j);
+            }  // else DropStaleResponse :382-385
+            wbag_remove_at(*t, x);
+            return W_ON;
+        }
+        if (m.type == AEQ) {  // HandleAppendEntriesRequest :347-356
+            const int pidx = m.a;
+            const int logok = pidx == 0 || (pidx > 0 && pidx <= s.len[i] && m.b == s.log[i][pidx - 1].term);
+            WMsg r;
+            wmsg_zero(r);
+            r.type = AEP;
+            r.term = (uint8_t)ct;
+            r.src = (uint8_t)i;
+            r.dst = (uint8_t)j;
+            if (m.term < ct || (s.st[i] == FOLLOWER && !logok)) {  // Reject :281-293
+                const int fit = wbag_fits(s, r);
+                if (fit != W_ON || !t) return fit;
+                const WMsg q = m;
+                wcopy_state(*t, s);
+                wbag_add(*t, r);
+                wbag_remove(*t, q);
+                return W_ON;
+            }
+            if (s.st[i] == CANDIDATE) {  // ReturnToFollowerState :295-299 — m stays
+                if (!t) return W_ON;
+                wcopy_state(*t, s);
+                t->st[i] = FOLLOWER;
+                return W_ON;
+            }
+            if (s.st[i] != FOLLOWER) return W_OFF;  // a Leader: no branch is enabled
+            const int index = pidx + 1, len = s.len[i];
+            if (m.n == 0 || (len >= index && s.log[i][index - 1].term == m.e[0].term)) {
+                // AppendEntriesAlreadyDone :301-317: UNCHANGED logVars after binding
+                // commitIndex' is an equality test under TLC
+                if (m.c != s.ci[i]) return W_OFF;
+                r.a = 1;
+                r.b = (uint8_t)(pidx + m.n);
+                const int fit = wbag_fits(s, r);
+                if (fit != W_ON || !t) return fit;
+                const WMsg q = m;
+                wcopy_state(*t, s);
+                wbag_add(*t, r);
+                wbag_remove(*t, q);
+                return W_ON;
+            }
+            if (len >= index) {  // ConflictAppendEntriesRequest :319-325 — drops the LAST entry, m stays
+                if (!t) return W_ON;
+                wcopy_state(*t, s);
+                t->len[i] = (uint8_t)(len - 1);
+                t->log[i][len - 1].term = 0;
+                t->log[i][len - 1].value = 0;
+                return W_ON;
+            }
+            if (len == pidx) {  // NoConflictAppendEntriesRequest :327-331 — m stays
+                if (len >= LW) return W_LOG;
+                if (!t) return W_ON;
+                wcopy_state(*t, s);
+                t->log[i][len] = m.e[0];
+                t->len[i] = (uint8_t)(len + 1);
+                return W_ON;
+            }
+            return W_OFF;
+        }
+        // AEP
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        if (m.term == ct) {  // HandleAppendEntriesResponse :360-370 (no Leader guard)
+            if (m.a) {
+                t->ni[i][j] = (uint8_t)(m.b + 1);
+                t->mi[i][j] = m.b;
+            } else {
+                const int v = s.ni[i][j] - 1;
+                t->ni[i][j] = (uint8_t)(v < 1 ? 1 : v);
+            }
+        }  // else DropStaleResponse
+        wbag_remove_at(*t, x);
+        return W_ON;
+    }
+    case 8: {  // DuplicateMessage(m) :410-412
+        if (x >= s.nmsg) return W_OFF;
+        if (s.cnt[x] >= CMAX) return W_DUP;
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        t->cnt[x] += 1;
+        return W_ON;
+    }
+    default: {  // DropMessage(m) :415-417
+        if (x >= s.nmsg) return W_OFF;
+        if (!t) return W_ON;
+        wcopy_state(*t, s);
+        wbag_remove_at(*t, x);
+        return W_ON;
+    }
+    }
+}
+
+// CONSTRAINT of a successor the layout holds: 1 in the model, 0 filtered
+// (generated, neither stored nor checked).
+RMC_HD int win_model(const WModel& M, const WState& t) {
+    int ok = 1;
+    for (int i = 0; i < M.S; ++i) {
+        if (t.ct[i] > M.max_term) ok = 0;
+        if (t.len[i] > M.max_log) ok = 0;
+    }
+    if (t.nmsg > M.max_msgs) ok = 0;
+    for (int q = 0; q < t.nmsg; ++q)
+        if (t.cnt[q] > M.max_dup) ok = 0;
+    return ok;
+}
+
+// ---- invariants (raft.tla:482-492; the config-5 and proof invariants as restated
+// in specs/MCraftBounded.tla) --------------------------------------------------------
+RMC_HD int wtype_ok(const WModel& M, const WState& s) {  // raft.tla:482-492
+    for (int i = 0; i < M.S; ++i) {
+        if (s.st[i] > LEADER) return 0;
+        if (s.vf[i] != NIL && s.vf[i] >= M.S) return 0;
+        if ((s.vR[i] | s.vG[i]) >> M.S) return 0;
+        for (int j = 0; j < M.S; ++j)
+            if (s.ni[i][j] < 1) return 0;
+        for (int x = 0; x < s.len[i]; ++x)
+            if (s.log[i][x].value >= M.V) return 0;
+    }
+    for (int q = 0; q < s.nmsg; ++q) {
+        const WMsg& m = s.msg[q];
+        if (s.cnt[q] < 1 || m.src >= M.S || m.dst >= M.S) return 0;
+        for (int x = 0; x < m.n; ++x)
+            if (m.e[x].value >= M.V) return 0;
+    }
+    return 1;
+}
+RMC_HD int wcommitted_prefix_of(const WState& s, int j, int i) {  // IsPrefix(Committed(j), log[i])
+    const int c = s.ci[j] < s.len[j] ? s.ci[j] : s.len[j];
+    if (s.len[i] < c) return 0;
+    return wmemcmp(s.log[i], s.log[j], c * (int)sizeof(WEnt)) == 0;
+}
+// 0 = every named invariant holds, else the RMC_INV_* bit (index) of the first violated one + 1
+RMC_HD int wcheck_invariants(const WModel& M, const WState& s) {
+    const int S = M.S, mask = M.inv_mask;
+    if ((mask & 1) && !wtype_ok(M, s)) return 1;
+    if (mask & 2)  // OneLeaderPerTerm (ElectionSafety restated, raft.tla:1124)
+        for (int i = 0; i < S; ++i)
+            for (int j = i + 1; j < S; ++j)
+                if (s.st[i] == LEADER && s.st[j] == LEADER && s.ct[i] == s.ct[j]) return 2;
+    if (mask & 4)  // LogMatching raft.tla:1132-1136
+        for (int i = 0; i < S; ++i)
+            for (int j = 0; j < S; ++j) {
+                const int n = s.len[i] < s.len[j] ? s.len[i] : s.len[j];
+                for (int x = 1; x <= n; ++x)
+                    if (s.log[i][x - 1].term == s.log[j][x - 1].term &&
+                        wmemcmp(s.log[i], s.log[j], x * (int)sizeof(WEnt)) != 0)
+                        return 3;
+            }
+    if (mask & 8)  // MessagesInv raft.tla:941-946 (:910's m.dest read as m.mdest)
+        for (int q = 0; q < s.nmsg; ++q) {
+            const WMsg& m = s.msg[q];
+            const int src = m.src, dst = m.dst, cs = s.ct[src];
+            if (m.term > cs) return 4;  // :934-935
+            if (m.type == RVP && m.a && cs == s.ct[dst] && cs == m.term) {  // :903-910
+                const int ld = wlast_term(s, dst), ls = wlast_term(s, src);
+                if (!(ld > ls || (ld == ls && s.len[dst] >= s.len[src]))) return 4;
+            }
+            if (m.type == RVQ && s.st[src] == CANDIDATE && cs == m.term)  // :915-920
+                if (m.b != s.len[src] || m.a != wlast_term(s, src)) return 4;
+            if (m.type == AEQ && m.n > 0 && m.term == cs) {  // :924-930
+                const int p = m.a;
+                if (p + 1 < 1 || p + 1 > s.len[src]) return 4;
+                if (s.log[src][p].term != m.e[0].term || s.log[src][p].value != m.e[0].value) return 4;
+                if (p > 0 && p <= s.len[src] && s.log[src][p - 1].term != m.b) return 4;
+            }
+        }
+    if (mask & 16)  // LeaderVotesQuorum raft.tla:1033-1037
+        for (int i = 0; i < S; ++i) {
+            if (s.st[i] != LEADER) continue;
+            unsigned q = 0;
+            for (int j = 0; j < S; ++j)
+                if (s.ct[j] > s.ct[i] || (s.ct[j] == s.ct[i] && s.vf[j] == i)) q |= 1u << j;
+            if (!wquorum(M, q)) return 5;
+        }
+    if (mask & 32)  // CandidateTermNotInLog raft.tla:1041-1047
+        for (int i = 0; i < S; ++i) {
+            if (s.st[i] != CANDIDATE) continue;
+            unsigned q = 0;
+            for (int j = 0; j < S; ++j)
+                if (s.ct[j] == s.ct[i] && (s.vf[j] == i || s.vf[j] == NIL)) q |= 1u << j;
+            if (!wquorum(M, q)) continue;
+            for (int j = 0; j < S; ++j)
+                for (int n = 0; n < s.len[j]; ++n)
+                    if (s.log[j][n].term == s.ct[i]) return 6;
+        }
+    if (mask & 64)  // VotesGrantedInv raft.tla:1145-1153
+        for (int i = 0; i < S; ++i)
+            for (int j = 0; j < S; ++j)
+                if (((s.vG[i] >> j) & 1u) && s.ct[i] == s.ct[j] && !wcommitted_prefix_of(s, j, i)) return 7;
+    if (mask & 128)  // QuorumLogInv raft.tla:1157-1161
+        for (int i = 0; i < S; ++i) {
+            unsigned miss = 0;
+            for (int j = 0; j < S; ++j)
+                if (!wcommitted_prefix_of(s, i, j)) miss |= 1u << j;
+            if (wquorum(M, miss)) return 8;
+        }
+    if (mask & 256)  // MoreUpToDateCorrect raft.tla:1167-1172
+        for (int i = 0; i < S; ++i)
+            for (int j = 0; j < S; ++j) {
+                const int li = wlast_term(s, i), lj = wlast_term(s, j);
+                if ((li > lj || (li == lj && s.len[i] >= s.len[j])) && !wcommitted_prefix_of(s, j, i)) return 9;
+            }
+    if (mask & 512)  // LeaderCompleteness raft.tla:1176-1180
+        for (int i = 0; i < S; ++i) {
+            if (s.st[i] != LEADER) continue;
+            for (int j = 0; j < S; ++j)
+                if (!wcommitted_prefix_of(s, j, i)) return 10;
+        }
+    return 0;
+}
+
+// Fingerprint of a canonical record (every byte; salted like the packed one).
+RMC_HD u64 wfp(const WState& s, u64 salt) {
+    const u64* w = reinterpret_cast<const u64*>(&s);
+    u64 h = 0x6A09E667F3BCC909ull ^ salt;
+    for (int k = 0; k < WWORDS; ++k) h = mix64(h ^ (w[k] + (u64)k * 0x9E3779B97F4A7C15ull));
+    return h ? h : 1ull;
+}
+
+}  // namespace wide
+}  // namespace rmc

@@ -40,21 +40,24 @@ int validate(const rmc_config* c, std::string* why) {
     auto bad = [&](const char* s) { *why = s; return RMC_E_INVAL; };
     if (c->n_servers < 2 || c->n_servers > RMC_MAX_SERVERS) return bad("n_servers must be 2..5");
     if (c->n_values < 1 || c->n_values > RMC_MAX_VALUES) return bad("n_values must be 1..2");
+    if (c->invariants & ~1023u) return bad("unknown invariant bit");
+    if (c->flags & ~511u) return bad("unknown flag bit");
+    if ((c->flags & RMC_UNBOUNDED_ANY) && c->max_depth <= 0)
+        return bad("a model with unbounded fields (RMC_FLAG_UNBOUNDED_*) needs max_depth > 0 (TLC -depth)");
+    if (wide_wanted(*c)) return validate_wide(c, why);  // bounds beyond the packed capacity
     if (c->max_term < 1 || c->max_term > RMC_MAX_TERM) return bad("max_term must be 1..14");
     if (c->max_log_len < 0 || c->max_log_len > RMC_MAX_LOG) return bad("max_log_len must be 0..3");
     if (c->max_msgs < 0 || c->max_msgs > RMC_MAX_MSGS) return bad("max_msgs must be 0..8");
     if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
-    if (c->invariants & ~1023u) return bad("unknown invariant bit");
     if ((c->flags & RMC_FLAG_SPILL) && (c->flags & RMC_FLAG_VERIFY_STATES))
         return bad("RMC_FLAG_SPILL does not combine with RMC_FLAG_VERIFY_STATES");
-    if (c->flags & ~511u) return bad("unknown flag bit");
-    if ((c->flags & RMC_UNBOUNDED_ANY) && c->max_depth <= 0)
-        return bad("a model with unbounded fields (RMC_FLAG_UNBOUNDED_*) needs max_depth > 0 (TLC -depth)");
     return 0;
 }
 
 void fill_params(rmc_ctx* c) {
     const rmc_config& g = c->cfg;
+    c->wide = wide_wanted(g) ? 1 : 0;
+    if (c->wide) fill_wide_model(c);
     c->sh.S = g.n_servers;
     c->sh.K = kcap_for(g.max_msgs);
     c->sh.sym = (g.flags & RMC_FLAG_SYMMETRY) != 0;
@@ -295,8 +298,9 @@ std::string capacity_message(const rmc_ctx* c, u32 overflow, int depth) {
     if (f & 4) what += std::string(what.empty() ? "" : ", ") + "Cardinality(DOMAIN messages) > " +
                        std::to_string(c->cfg.max_msgs);
     if (f & 8) what += std::string(what.empty() ? "" : ", ") + "messages[m] > " + std::to_string(c->cfg.max_dup);
-    return "a successor of a level-" + std::to_string(depth) + " state needs " + what +
-           ": beyond the packed capacity of a field no CONSTRAINT bounds (lower the depth bound or add a CONSTRAINT)";
+    return "a successor of a level-" + std::to_string(depth) + " state needs " + what + ": beyond the " +
+           (c->wide ? "wide" : "packed") +
+           " layout's capacity of a field no CONSTRAINT bounds (lower the depth bound or add a CONSTRAINT)";
 }
 
 int read_counters(rmc_ctx* c) {
@@ -319,6 +323,7 @@ void spill_rebase(rmc_ctx* c, u64 base) {
     c->B.parent = (u64*)((uintptr_t)X.parent - (uintptr_t)base * 8);
     c->B.act = (uint8_t*)((uintptr_t)X.act - (uintptr_t)base);
     c->B.foot = (u64*)((uintptr_t)X.foot - (uintptr_t)base * 8);
+    c->B.cls = (uint8_t*)((uintptr_t)X.cls - (uintptr_t)base);
     c->B.cap = base + X.win;
 }
 
@@ -390,6 +395,7 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
         HIPCHK(c, hipMemcpyAsync(X.parent + off, X.parent + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.act + off, X.act + n + off, k, hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.foot + off, X.foot + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipMemcpyAsync(X.cls + off, X.cls + n + off, k, hipMemcpyDeviceToDevice, c->st));
     }
     HIPCHK(c, hipStreamSynchronize(c->st));
     spill_rebase(c, a);
@@ -434,6 +440,7 @@ const char* rmc_last_error(const rmc_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 size_t rmc_state_bytes(const rmc_config* cfg) {
     if (!cfg) return 0;
+    if (wide_wanted(*cfg)) return sizeof(rmc::wide::WState);
     return (size_t)(2 * cfg->n_servers + kcap_for(cfg->max_msgs)) * 4u;
 }
 
@@ -470,9 +477,19 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         c->err = "stream/event creation failed";
         return bail(RMC_E_HIP);
     }
+    if (hipHostMalloc(&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+        c->err = "pinned allocation failed";
+        return bail(RMC_E_NOMEM);
+    }
+    memset(c->h_ctr, 0, sizeof(Counters));
+    if (c->wide) {  // bounds beyond the packed capacity: the wide layout (rmc_wide.cpp)
+        if (int rc = create_wide(c)) return bail(rc);
+        *out = c;
+        return 0;
+    }
 
     // ---- capacity: state store + parents + lanes + fingerprint set (load <= 0.5)
-    const u64 per_state = (u64)c->NW * 4 + 8 + 1 + 8;  // state, parent, lane, footprint
+    const u64 per_state = (u64)c->NW * 4 + 8 + 1 + 8 + 1;  // state, parent, lane, footprint, class
     const bool spill = (cfg->flags & RMC_FLAG_SPILL) != 0;
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -498,8 +515,9 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     c->B.tmask = slots - 1;
     if (hipMalloc(&c->B.store, win * (u64)c->NW * 4) != hipSuccess ||
         hipMalloc(&c->B.parent, win * 8) != hipSuccess || hipMalloc(&c->B.act, win) != hipSuccess ||
-        hipMalloc(&c->B.foot, win * 8) != hipSuccess ||
+        hipMalloc(&c->B.foot, win * 8) != hipSuccess || hipMalloc(&c->B.cls, win) != hipSuccess ||
         hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
+        hipMalloc(&c->B.word, (1ull << 24) * 2) != hipSuccess ||  // presorted windows of one launch
         hipMalloc(&c->d_staged, (size_t)c->NW * 4 * 64) != hipSuccess) {
         c->err = "device allocation failed (capacity " + std::to_string(win) + " states)";
         return bail(RMC_E_NOMEM);
@@ -511,12 +529,14 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     c->spill.parent = c->B.parent;
     c->spill.act = c->B.act;
     c->spill.foot = c->B.foot;
-    if (spill && spill_reserve(c)) return bail(RMC_E_NOMEM);
-    if (hipHostMalloc(&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
-        c->err = "pinned allocation failed";
-        return bail(RMC_E_NOMEM);
+    c->spill.cls = c->B.cls;
+    // classes are a layout hint (any value is a valid class): zero them once so
+    // recovered or never-written states sort deterministically
+    if (hipMemset(c->B.cls, 0, win) != hipSuccess) {
+        c->err = "hipMemset failed";
+        return bail(RMC_E_HIP);
     }
-    memset(c->h_ctr, 0, sizeof(Counters));
+    if (spill && spill_reserve(c)) return bail(RMC_E_NOMEM);
     if (c->sh.sym) {  // successors with tied signatures, canonicalised by k_ties after each launch
         // a lane defers at most one tied successor, so launches of at most
         // tie_cap / lanes states cannot overflow it (run_bfs sizes them so):
@@ -550,14 +570,17 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
 void rmc_destroy(rmc_ctx* c) {
     if (!c) return;
     if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->wide) destroy_wide(c);
     spill_free(c);
     // the unbiased allocations (B.* may be rebased by a spill)
     (void)hipFree(c->spill.store ? c->spill.store : c->B.store);
     (void)hipFree(c->spill.parent ? c->spill.parent : c->B.parent);
     (void)hipFree(c->spill.act ? c->spill.act : c->B.act);
     (void)hipFree(c->spill.foot ? c->spill.foot : c->B.foot);
+    (void)hipFree(c->spill.cls ? c->spill.cls : c->B.cls);
     (void)hipFree(c->B.table);
     (void)hipFree(c->B.ctr);
+    (void)hipFree(c->B.word);
     (void)hipFree(c->d_staged);
     free_dist(c);
     (void)hipFree(c->B.sidx);
@@ -573,6 +596,7 @@ void rmc_destroy(rmc_ctx* c) {
 int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (!c) return RMC_E_INVAL;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->wide) return run_bfs_wide(c, cb, user);
     if (c->dist.on) return run_bfs_sharded(c, cb, user);
     const auto t0 = std::chrono::steady_clock::now();
     auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
@@ -827,6 +851,7 @@ int move_file(rmc_ctx* c, FILE* f, void* dev, u64 n, bool to_file) {
 // exist — the fingerprint set itself (TLC checkpoints its FPSet too).
 int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
+    if (c->wide) return fail(c, RMC_E_STATE, "checkpoint / recover: not supported on the wide layout");
     if (c->level_start.size() < 2 || c->have_target)
         return fail(c, RMC_E_STATE, "checkpoint: needs a BFS stopped at a level boundary without a violation");
     if (c->res.left_on_queue == 0) return fail(c, RMC_E_STATE, "checkpoint: the search is complete");
@@ -869,6 +894,7 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
 
 int rmc_recover(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
+    if (c->wide) return fail(c, RMC_E_STATE, "checkpoint / recover: not supported on the wide layout");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     const std::string file = shard_path(c, path);
     FILE* f = fopen(file.c_str(), "rb");
@@ -980,6 +1006,7 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
     if (!c || !len) return RMC_E_INVAL;
     if (!c->have_target) return fail(c, RMC_E_STATE, "no violation or deadlock to trace");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->wide) return trace_wide(c, states, families, instances, cap, len);
     if (c->dist.on) return trace_sharded(c, states, families, instances, cap, len);
     std::vector<u64> chain;
     std::vector<uint8_t> acts;
@@ -1130,11 +1157,17 @@ void msg_to_view(const std::vector<int>& v, rmc_msg_view* m) {
 // SmokeInit (Smokeraft.tla:64-76): k choices for each of the 9 per-server
 // variables, all k^9 combinations, each with the same bag of k messages drawn as
 // [RandomSubset(k, SmokeMessageType) -> {1}].
-int smoke_init(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<u32>* packed, std::string* why) {
-    const int S = c->sh.S, k = sc.smoke_k;
+}  // namespace
+
+namespace rmc_host {
+// SmokeInit (Smokeraft.tla:64-76) as k^9 views, in RandomSubset product order.
+int smoke_views(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<rmc_state_view>* views, std::string* why) {
+    const int S = c->cfg.n_servers, k = sc.smoke_k;
     SmokeDomains D{S, c->cfg.n_values, sc.smoke_nat > 0 ? sc.smoke_nat : 2};
-    if (D.nat > 3) { *why = "smoke_nat > 3 exceeds the packed index range"; return RMC_E_INVAL; }
-    if (k > c->sh.K) { *why = "smoke_k messages exceed the bag capacity (set MaxMsgs >= k)"; return RMC_E_INVAL; }
+    if (D.nat > 3 && !c->wide) { *why = "smoke_nat > 3 exceeds the packed index range"; return RMC_E_INVAL; }
+    if (D.nat > 100) { *why = "smoke_nat > 100"; return RMC_E_INVAL; }
+    const int bag = c->wide ? rmc::wide::KW : c->sh.K;
+    if (k > bag) { *why = "smoke_k messages exceed the bag capacity (set MaxMsgs >= k)"; return RMC_E_INVAL; }
     std::mt19937_64 g(sc.seed ^ 0x5350AC3ull);
     using V = std::vector<int>;
     auto fn = [&](auto elem) { return [&, elem](std::mt19937_64& gg) { V v; for (int i = 0; i < S; ++i) { auto e = elem(gg); v.insert(v.end(), e.begin(), e.end()); } return v; }; };
@@ -1159,7 +1192,7 @@ int smoke_init(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<u32>* pac
         if ((int)vec->size() != k) { *why = "RandomSubset could not draw k distinct elements"; return RMC_E_INVAL; }
     u64 n = 1;
     for (int x = 0; x < 9; ++x) n *= (u64)k;
-    packed->assign(n * (u64)c->NW, 0u);
+    views->assign(n, rmc_state_view{});
     for (u64 idx = 0; idx < n; ++idx) {
         int dg[9];
         u64 r = idx;
@@ -1187,16 +1220,31 @@ int smoke_init(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<u32>* pac
         }
         v.n_msgs = (int)msgs.size();
         for (size_t q = 0; q < msgs.size(); ++q) msg_to_view(msgs[q], &v.msgs[q]);
-        if (int rc = encode_view(c, v, packed->data() + idx * (u64)c->NW, why)) return rc;
+        (*views)[idx] = v;
     }
     return 0;
 }
+}  // namespace rmc_host
 
-int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_beh, std::vector<u32>* rec) {
+namespace {
+int smoke_init(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<u32>* packed, std::string* why) {
+    std::vector<rmc_state_view> views;
+    if (int rc = smoke_views(c, sc, &views, why)) return rc;
+    packed->assign(views.size() * (u64)c->NW, 0u);
+    for (size_t q = 0; q < views.size(); ++q)
+        if (int rc = encode_view(c, views[q], packed->data() + q * (u64)c->NW, why)) return rc;
+    return 0;
+}
+
+int run_sim(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, i64 rec_beh, std::vector<u32>* rec,
+            std::vector<rmc_state_view>* wrec = nullptr) {
     if (!c || !sc || !out || sc->behaviours == 0 || sc->depth < 1 ||
-        (sc->mode != RMC_SIM_WITHIN_CAPACITY && sc->mode != RMC_SIM_TRUNCATE))
+        (sc->mode != RMC_SIM_WITHIN_CAPACITY && sc->mode != RMC_SIM_TRUNCATE && sc->mode != RMC_SIM_TLC))
         return RMC_E_INVAL;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->wide) return sim_wide(c, sc, out, rec_beh, wrec);
+    if (sc->mode == RMC_SIM_TLC)
+        return fail(c, RMC_E_INVAL, "RMC_SIM_TLC draws on the wide layout only (bounds beyond the packed capacity)");
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<u32> inits;
     std::string why;
@@ -1267,6 +1315,13 @@ int rmc_smoke_init(const rmc_config* cfg, const rmc_sim_config* sc, rmc_state_vi
     rmc_ctx host;  // codec only: no device, no allocation
     host.cfg = *cfg;
     fill_params(&host);
+    if (host.wide) {
+        std::vector<rmc_state_view> views;
+        if (smoke_views(&host, *sc, &views, &why)) return RMC_E_INVAL;
+        *n = views.size();
+        for (size_t q = 0; q < *n && q < cap && states; ++q) states[q] = views[q];
+        return 0;
+    }
     std::vector<u32> packed;
     if (smoke_init(&host, *sc, &packed, &why)) return RMC_E_INVAL;
     *n = packed.size() / (size_t)host.NW;
@@ -1279,6 +1334,13 @@ int rmc_sim_replay(rmc_ctx* c, const rmc_sim_config* sc, uint64_t behaviour, rmc
     if (!c || !sc || !len || behaviour >= sc->behaviours) return RMC_E_INVAL;
     rmc_sim_result r;
     std::vector<u32> rec;
+    if (c->wide) {
+        std::vector<rmc_state_view> wrec;
+        if (int rc = run_sim(c, sc, &r, (i64)behaviour, nullptr, &wrec)) return rc;
+        *len = wrec.size();
+        for (size_t q = 0; q < *len && q < cap; ++q) states[q] = wrec[q];
+        return 0;
+    }
     if (int rc = run_sim(c, sc, &r, (i64)behaviour, &rec)) return rc;
     *len = rec.size() / (size_t)c->NW;
     for (size_t q = 0; q < *len && q < cap; ++q) decode_state(c, rec.data() + q * c->NW, &states[q]);
@@ -1328,6 +1390,7 @@ int rmc_expand(rmc_ctx* c, const rmc_state_view* states, size_t n, rmc_succ_view
     HIPCHK(c, hipSetDevice(c->cfg.device));
     *n_out = 0;
     if (n == 0) return 0;
+    if (c->wide) return expand_wide(c, states, n, out, cap, n_out);
     const int NW = c->NW, RW = 6 + NW;
     std::vector<u32> packed(n * (size_t)NW);
     std::string why;

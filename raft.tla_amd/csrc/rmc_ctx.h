@@ -37,6 +37,7 @@ struct DistState {
         int timed = 0, xtimed = 0;
     } set[2];
     hipEvent_t ev_cnt = nullptr, ev_acc = nullptr, ev_c = nullptr, ev_x = nullptr;
+    hipEvent_t ev_h = nullptr;      // host waits on xs (under the deadline)
     // single buffers (used on xs only, rounds in order)
     rmc::u64* key_in = nullptr;     // keys received, blocks by source
     uint8_t* rep_out = nullptr;     // replies to the keys received (same layout)
@@ -55,6 +56,20 @@ struct DistState {
     int overlap = 1;                // RMC_DIST_OVERLAP=0: the next expansion waits for the exchange
     double fill = 0.5;              // RMC_DIST_FILL: expected fill of the fullest outbox a round aims at
                                     // (> 1 forces parking: a test hook)
+    // replicated levels: a level of at most rep_max states in total is gathered
+    // whole (k_pack_rep records) into rep_buf on every rank and expanded there
+    rmc::u64 rep_max = 0;
+    rmc::u32* rep_send = nullptr;   // this rank's records of the level
+    rmc::u32* rep_buf = nullptr;    // every rank's, in rank order
+    rmc::u64 rep_levels = 0;        // replicated levels of the last run
+    // deadlines (RMC_DIST_TIMEOUT_S) and where the loop is, for error messages
+    double timeout_s = 300.0;
+    int nonblocking = 0;            // the RCCL communicator is non-blocking
+    int aborted = 0;                // a deadline aborted the communicator: the ctx is unusable
+    int lvl = 0, rnd = 0;
+    const char* phase = "";
+    int stall_rank = -1, stall_level = 2;  // test hook (RMC_DIST_STALL_*)
+    double stall_s = 0;
     // statistics of the last run
     rmc::u64 keys_sent = 0, states_sent = 0, chunks = 0, parked = 0;
     double xfer_seconds = 0;        // device time of the exchange rounds (xs), overlapped or not
@@ -77,6 +92,7 @@ struct SpillState {
     rmc::u64* parent = nullptr;
     uint8_t* act = nullptr;
     rmc::u64* foot = nullptr;
+    uint8_t* cls = nullptr;
     rmc::u64* h_parent = nullptr;  // host, [total_cap], reserved address space,
     uint8_t* h_act = nullptr;      // pages touched as levels spill
     size_t h_bytes = 0;
@@ -106,6 +122,11 @@ struct rmc_ctx {
     // recovery (rmc_recover): the next rmc_run_bfs continues from this level
     int resume = 0;
     int resume_depth = 0;
+    // the wide layout (raft_wide.h): bounds beyond the packed capacity
+    int wide = 0;
+    rmc::wide::WModel WM{};
+    rmc::wide::WideBufs WB{};
+    rmc::wide::WState* w_staged = nullptr;
 };
 
 #define HIPCHK(c, expr)                                                                              \
@@ -141,4 +162,16 @@ int spill_reserve(rmc_ctx* c);
 int spill_to(rmc_ctx* c, rmc::u64 a, rmc::u64 count);
 void spill_free(rmc_ctx* c);
 int read_link(rmc_ctx* c, rmc::u64 idx, rmc::u64* parent, uint8_t* act);
+// the wide layout (rmc_wide.cpp)
+bool wide_wanted(const rmc_config& g);
+int validate_wide(const rmc_config* c, std::string* why);
+int create_wide(rmc_ctx* c);
+void destroy_wide(rmc_ctx* c);
+int run_bfs_wide(rmc_ctx* c, rmc_progress_fn cb, void* user);
+int trace_wide(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* instances, size_t cap, size_t* len);
+int expand_wide(rmc_ctx* c, const rmc_state_view* states, size_t n, rmc_succ_view* out, size_t cap, size_t* n_out);
+int sim_wide(rmc_ctx* c, const rmc_sim_config* sc, rmc_sim_result* out, rmc::i64 rec_beh,
+             std::vector<rmc_state_view>* rec);
+void fill_wide_model(rmc_ctx* c);
+int smoke_views(const rmc_ctx* c, const rmc_sim_config& sc, std::vector<rmc_state_view>* views, std::string* why);
 }  // namespace rmc_host

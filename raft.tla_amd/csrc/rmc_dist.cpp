@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "rmc_ctx.h"
 
@@ -36,14 +37,92 @@ using namespace rmc_host;
 
 namespace {
 
-#define NCCLCHK(c, expr)                                                                         \
-    do {                                                                                         \
-        ncclResult_t r_ = (expr);                                                                \
-        if (r_ != ncclSuccess) return fail((c), RMC_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
-    } while (0)
-
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---- deadlines ---------------------------------------------------------------------
+// Every wait of the sharded loop on other ranks has a deadline
+// (RMC_DIST_TIMEOUT_S, default 300 s): a collective that has not completed in
+// time aborts the RCCL communicator (ncclCommAbort also ends the kernels
+// waiting inside it) and fails the call on this rank, naming the level, the
+// round and the phase, instead of hanging until an outer time limit.  The
+// communicator is non-blocking (ncclConfig_t.blocking = 0), so connection
+// set-up inside a group call is polled under the same deadline.  A host
+// transport applies its own deadline inside its callbacks (rmc.h).
+std::string where(const rmc_ctx* c) {
+    const DistState& D = c->dist;
+    return "rank " + std::to_string(D.rank) + " of " + std::to_string(D.world) + ", level " +
+           std::to_string(D.lvl) + ", round " + std::to_string(D.rnd) + ", phase " + D.phase;
+}
+
+int deadline_fail(rmc_ctx* c, const char* what) {
+    DistState& D = c->dist;
+    D.aborted = 1;
+    if (D.rccl && D.comm) {
+        (void)ncclCommAbort(D.comm);
+        D.comm = nullptr;
+    }
+    char t[32];
+    snprintf(t, sizeof t, "%g", D.timeout_s);
+    return fail(c, RMC_E_HIP, std::string("sharded search: ") + what + " did not complete within the " + t +
+                                  " s deadline (RMC_DIST_TIMEOUT_S) at " + where(c) +
+                                  (D.rccl ? "; the RCCL communicator was aborted" : ""));
+}
+
+// Wait for an event of the exchange path under the deadline: spin first (a
+// round's read-back is on the critical path), then back off.
+int xwait(rmc_ctx* c, hipEvent_t ev) {
+    DistState& D = c->dist;
+    const double t0 = now_s();
+    for (u64 spin = 0;; ++spin) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady)
+            return fail(c, RMC_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e) + " at " + where(c));
+        if ((spin & 63) == 0 && now_s() - t0 > D.timeout_s) return deadline_fail(c, "a wait on the exchange");
+        if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    D.wait_seconds += now_s() - t0;
+    return 0;
+}
+
+// The result of an RCCL call on the non-blocking communicator: ncclInProgress
+// is polled (ncclCommGetAsyncError) until the call is enqueued, under the deadline.
+int nccl_done(rmc_ctx* c, ncclResult_t r, const char* what) {
+    DistState& D = c->dist;
+    if (r == ncclInProgress || (r == ncclSuccess && D.nonblocking)) {
+        const double t0 = now_s();
+        for (u64 spin = 0;; ++spin) {
+            if (!D.comm) return fail(c, RMC_E_HIP, std::string(what) + ": no communicator at " + where(c));
+            if (ncclCommGetAsyncError(D.comm, &r) != ncclSuccess) break;
+            if (r != ncclInProgress) break;
+            if ((spin & 63) == 0 && now_s() - t0 > D.timeout_s) return deadline_fail(c, what);
+            if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    if (r != ncclSuccess) return fail(c, RMC_E_HIP, std::string(what) + ": " + ncclGetErrorString(r) + " at " + where(c));
+    return 0;
+}
+
+#define NCCLCHK(c, expr)                                              \
+    do {                                                              \
+        if (int rc_ = nccl_done((c), (expr), #expr)) return rc_;      \
+    } while (0)
+
+// The host transport's callbacks return non-zero on failure, their own
+// deadline included (rmc.h): the call fails naming where; a callback that
+// failed after the deadline had passed is reported as the deadline.
+int host_fail(rmc_ctx* c, const char* what, double t0) {
+    const DistState& D = c->dist;
+    if (now_s() - t0 >= 0.9 * D.timeout_s) {
+        char t[32];
+        snprintf(t, sizeof t, "%g", D.timeout_s);
+        return fail(c, RMC_E_HIP, std::string("sharded search: the host transport's ") + what +
+                                      " did not complete within the " + t + " s deadline (RMC_DIST_TIMEOUT_S) at " +
+                                      where(c));
+    }
+    return fail(c, RMC_E_HIP, std::string("host transport ") + what + " failed at " + where(c));
 }
 
 // All-to-all of per-peer byte blocks living on the device, on the exchange
@@ -59,8 +138,20 @@ int a2a(rmc_ctx* c, const void* sbuf, const u64* soff, const u64* scnt, void* rb
         if (!any) return 0;
         NCCLCHK(c, ncclGroupStart());
         for (int p = 0; p < W; ++p) {
-            if (scnt[p]) NCCLCHK(c, ncclSend((const char*)sbuf + soff[p], scnt[p], ncclUint8, p, D.comm, D.xs));
-            if (rcnt[p]) NCCLCHK(c, ncclRecv((char*)rbuf + roff[p], rcnt[p], ncclUint8, p, D.comm, D.xs));
+            if (scnt[p]) {
+                const ncclResult_t r = ncclSend((const char*)sbuf + soff[p], scnt[p], ncclUint8, p, D.comm, D.xs);
+                if (r != ncclSuccess && r != ncclInProgress) {
+                    (void)ncclGroupEnd();
+                    return nccl_done(c, r, "ncclSend");
+                }
+            }
+            if (rcnt[p]) {
+                const ncclResult_t r = ncclRecv((char*)rbuf + roff[p], rcnt[p], ncclUint8, p, D.comm, D.xs);
+                if (r != ncclSuccess && r != ncclInProgress) {
+                    (void)ncclGroupEnd();
+                    return nccl_done(c, r, "ncclRecv");
+                }
+            }
         }
         NCCLCHK(c, ncclGroupEnd());
         return 0;
@@ -76,17 +167,19 @@ int a2a(rmc_ctx* c, const void* sbuf, const u64* soff, const u64* scnt, void* rb
                                      D.xs));
         o += scnt[p];
     }
-    HIPCHK(c, hipStreamSynchronize(D.xs));
+    HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+    if (int rc = xwait(c, D.ev_h)) return rc;
+    const double th = now_s();
     if (D.host.alltoallv(D.host.user, D.stage_send.data(), scnt, D.stage_recv.data(), rcnt))
-        return fail(c, RMC_E_HIP, "host transport alltoallv failed");
+        return host_fail(c, "alltoallv", th);
     o = 0;
     for (int p = 0; p < W; ++p) {
         if (rcnt[p])
             HIPCHK(c, hipMemcpyAsync((char*)rbuf + roff[p], D.stage_recv.data() + o, rcnt[p], hipMemcpyHostToDevice, D.xs));
         o += rcnt[p];
     }
-    HIPCHK(c, hipStreamSynchronize(D.xs));
-    return 0;
+    HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+    return xwait(c, D.ev_h);
 }
 
 // All-to-all of `per` u64 per peer between device buffers (the count rows).
@@ -105,7 +198,8 @@ int a2a_u64(rmc_ctx* c, const u64* send, u64* recv, u64 per) {
 int allgather(rmc_ctx* c, const void* mine, u64 bytes, void* all) {
     DistState& D = c->dist;
     if (!D.rccl) {
-        if (D.host.allgather(D.host.user, mine, bytes, all)) return fail(c, RMC_E_HIP, "host transport allgather failed");
+        const double th = now_s();
+        if (D.host.allgather(D.host.user, mine, bytes, all)) return host_fail(c, "allgather", th);
         return 0;
     }
     const bool big = bytes > D.ag_cap;  // rows are small: the staging buffer is allocated once
@@ -116,8 +210,8 @@ int allgather(rmc_ctx* c, const void* mine, u64 bytes, void* all) {
     NCCLCHK(c, ncclAllGather(d_in, d_buf, bytes, ncclUint8, D.comm, D.xs));
     HIPCHK(c, hipMemcpyAsync(all, d_buf, bytes * (u64)D.world, hipMemcpyDeviceToHost, D.xs));
     if (big) HIPCHK(c, hipFreeAsync(d_buf, D.xs));
-    HIPCHK(c, hipStreamSynchronize(D.xs));
-    return 0;
+    HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+    return xwait(c, D.ev_h);
 }
 
 // All-gather of this rank's device counters (the level statistics), after
@@ -130,14 +224,74 @@ int allgather_counters(rmc_ctx* c, Counters* rows) {
     if (D.rccl) {
         NCCLCHK(c, ncclAllGather(c->B.ctr, D.ag_dev, bytes, ncclUint8, D.comm, D.xs));
         HIPCHK(c, hipMemcpyAsync(rows, D.ag_dev, bytes * (u64)D.world, hipMemcpyDeviceToHost, D.xs));
-        HIPCHK(c, hipStreamSynchronize(D.xs));
-        return 0;
+        HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+        return xwait(c, D.ev_h);
     }
     Counters mine;
     HIPCHK(c, hipMemcpyAsync(&mine, c->B.ctr, bytes, hipMemcpyDeviceToHost, D.xs));
-    HIPCHK(c, hipStreamSynchronize(D.xs));
-    if (D.host.allgather(D.host.user, &mine, bytes, rows)) return fail(c, RMC_E_HIP, "host transport allgather failed");
+    HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+    if (int rc = xwait(c, D.ev_h)) return rc;
+    const double th = now_s();
+    if (D.host.allgather(D.host.user, &mine, bytes, rows)) return host_fail(c, "allgather", th);
     return 0;
+}
+
+// Replicated level: every rank's records (n[p] of them, rb bytes each) into
+// D.rep_buf, contiguous in rank order; this rank's own block is copied locally.
+int gather_level(rmc_ctx* c, const std::vector<u64>& n, u64 rb) {
+    DistState& D = c->dist;
+    const int W = D.world, me = D.rank;
+    std::vector<u64> off((size_t)W + 1, 0);
+    for (int p = 0; p < W; ++p) off[(size_t)p + 1] = off[(size_t)p] + n[(size_t)p];
+    char* dst = (char*)D.rep_buf;
+    if (n[(size_t)me])
+        HIPCHK(c, hipMemcpyAsync(dst + off[(size_t)me] * rb, D.rep_send, n[(size_t)me] * rb, hipMemcpyDeviceToDevice,
+                                 D.xs));
+    if (W == 1) return 0;
+    if (D.rccl) {
+        bool any = false;
+        for (int p = 0; p < W; ++p) any |= p != me && (n[(size_t)p] || n[(size_t)me]);
+        if (!any) return 0;
+        NCCLCHK(c, ncclGroupStart());
+        for (int p = 0; p < W; ++p) {
+            if (p == me) continue;
+            ncclResult_t r = ncclSuccess;
+            if (n[(size_t)me]) r = ncclSend(D.rep_send, n[(size_t)me] * rb, ncclUint8, p, D.comm, D.xs);
+            if ((r == ncclSuccess || r == ncclInProgress) && n[(size_t)p])
+                r = ncclRecv(dst + off[(size_t)p] * rb, n[(size_t)p] * rb, ncclUint8, p, D.comm, D.xs);
+            if (r != ncclSuccess && r != ncclInProgress) {
+                (void)ncclGroupEnd();
+                return nccl_done(c, r, "ncclSend/ncclRecv (level all-gather)");
+            }
+        }
+        NCCLCHK(c, ncclGroupEnd());
+        return 0;
+    }
+    // host transport: this rank's block to every peer (the block repeated per destination)
+    const u64 mine = n[(size_t)me] * rb;
+    std::vector<u64> scnt((size_t)W), rcnt((size_t)W);
+    for (int p = 0; p < W; ++p) {
+        scnt[(size_t)p] = p == me ? 0 : mine;
+        rcnt[(size_t)p] = p == me ? 0 : n[(size_t)p] * rb;
+    }
+    D.stage_send.resize(std::max<u64>(mine * (u64)(W - 1), 1));
+    D.stage_recv.resize(std::max<u64>((off[(size_t)W] - n[(size_t)me]) * rb, 1));
+    if (mine) HIPCHK(c, hipMemcpyAsync(D.stage_send.data(), D.rep_send, mine, hipMemcpyDeviceToHost, D.xs));
+    HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+    if (int rc = xwait(c, D.ev_h)) return rc;
+    for (int q = 1; q < W - 1; ++q) memcpy(D.stage_send.data() + (u64)q * mine, D.stage_send.data(), mine);
+    const double th = now_s();
+    if (D.host.alltoallv(D.host.user, D.stage_send.data(), scnt.data(), D.stage_recv.data(), rcnt.data()))
+        return host_fail(c, "alltoallv (level all-gather)", th);
+    u64 o = 0;
+    for (int p = 0; p < W; ++p) {
+        if (rcnt[(size_t)p])
+            HIPCHK(c, hipMemcpyAsync(dst + off[(size_t)p] * rb, D.stage_recv.data() + o, rcnt[(size_t)p],
+                                     hipMemcpyHostToDevice, D.xs));
+        o += rcnt[(size_t)p];
+    }
+    HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+    return xwait(c, D.ev_h);
 }
 
 float elapsed_ms(hipEvent_t a, hipEvent_t b) {
@@ -164,8 +318,12 @@ void free_dist(rmc_ctx* c) {
             if (*e) (void)hipEventDestroy(*e);
         S = DistState::Set{};
     }
-    for (hipEvent_t* e : {&D.ev_cnt, &D.ev_acc, &D.ev_c, &D.ev_x})
+    for (hipEvent_t* e : {&D.ev_cnt, &D.ev_acc, &D.ev_c, &D.ev_x, &D.ev_h})
         if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
+    (void)hipFree(D.rep_send);
+    (void)hipFree(D.rep_buf);
+    D.rep_send = nullptr;
+    D.rep_buf = nullptr;
     (void)hipFree(D.key_in);
     (void)hipFree(D.rep_out);
     (void)hipFree(D.rep_in);
@@ -174,7 +332,16 @@ void free_dist(rmc_ctx* c) {
     (void)hipFree(D.sa);
     if (D.h_sa) (void)hipHostFree(D.h_sa);
     (void)hipFree(D.ag_dev);
-    if (D.comm) (void)ncclCommDestroy(D.comm);
+    if (D.comm) {  // finalize (polled and bounded on a non-blocking communicator), then destroy
+        ncclResult_t r = ncclCommFinalize(D.comm);
+        const double t0 = now_s();
+        while (r == ncclInProgress && now_s() - t0 < 10.0) {
+            if (ncclCommGetAsyncError(D.comm, &r) != ncclSuccess) break;
+            if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        if (r == ncclSuccess) (void)ncclCommDestroy(D.comm);
+        else (void)ncclCommAbort(D.comm);
+    }
     if (D.xs) (void)hipStreamDestroy(D.xs);
     c->B.sent = nullptr; c->B.key_out = nullptr; c->B.tick_out = nullptr; c->B.ocount = nullptr;
     c->B.st_out = nullptr; c->B.scount = nullptr; c->B.ovf = nullptr; c->B.ovf_cap = 0;
@@ -184,14 +351,20 @@ void free_dist(rmc_ctx* c) {
     D.comm = nullptr;
     D.xs = nullptr;
     D.on = 0;
+    D.aborted = 0;
 }
 
 int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     DistState& D = c->dist;
     const int W = D.world, me = D.rank;
     const u64 RB = (u64)(c->NW + 4) * 4;  // state record: packed state, global parent ref, footprint
+    const u64 RBR = (u64)(c->NW + 6) * 4;  // replicated-level record (RepRec)
     const u64 kcap = c->B.kcap;
     const double t0 = now_s();
+    if (D.aborted) return fail(c, RMC_E_STATE, "sharded search: the communicator was aborted by an earlier deadline");
+    D.lvl = 0;
+    D.rnd = 0;
+    D.phase = "start";
     // rmc_recover restored this rank's levels, parents and set (every rank of
     // the checkpoint's world, each from its own part)
     const bool resume = c->resume != 0;
@@ -202,6 +375,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->have_target = 0;
     D.keys_sent = D.states_sent = D.chunks = D.parked = 0;
     D.xfer_seconds = D.wait_seconds = 0;
+    D.rep_levels = 0;
     if (!resume) HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->B.sent) HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
     const bool verify = c->sh.verify;
@@ -220,17 +394,15 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         HIPCHK(c, launch(c->sh, 1, c->P, c->PT, c->B, 1, 0, c->d_staged, nullptr, 0, nullptr, c->st));
     }
     std::vector<Counters> rows((size_t)W);
-    int lvl_now = 1;  // the level being expanded (error messages)
     // level end: the all-gathered device counters; errors stop every rank alike
     auto level_end = [&]() -> int {
-        const double tw = now_s();
+        D.phase = "level end (counter all-gather)";
         if (int rc = allgather_counters(c, rows.data())) return rc;
-        D.wait_seconds += now_s() - tw;
         *c->h_ctr = rows[(size_t)me];
         for (int r = 0; r < W; ++r) {
             const Counters& k = rows[(size_t)r];
             if (k.table_full) return fail(c, RMC_E_CAPACITY, "fingerprint set full on rank " + std::to_string(r));
-            if (k.overflow >> 8) return fail(c, RMC_E_CAPACITY, capacity_message(c, k.overflow, lvl_now));
+            if (k.overflow >> 8) return fail(c, RMC_E_CAPACITY, capacity_message(c, k.overflow, D.lvl));
             if (k.overflow & 4u) return fail(c, RMC_E_CAPACITY, "verification buffer full on rank " + std::to_string(r));
             if (k.overflow & 8u)
                 return fail(c, RMC_E_HIP, "verification: a fingerprint without a published state on rank " +
@@ -252,7 +424,11 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (verify && !resume && c->h_ctr->count)  // slot -> store index of the initial state(s)
         HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, 0, c->h_ctr->count, nullptr, nullptr, 0, nullptr, c->st));
     u64 total_prev = 0;
-    for (const auto& k : rows) total_prev += k.count;
+    std::vector<u64> count_before((size_t)W);  // every rank's store count when the current level began
+    for (int r = 0; r < W; ++r) {
+        total_prev += rows[(size_t)r].count;
+        count_before[(size_t)r] = rows[(size_t)r].count;
+    }
     if (resume && total_prev != saved.distinct)
         return fail(c, RMC_E_IO, "recover: the ranks' parts hold " + std::to_string(total_prev) +
                                      " states, the checkpoint " + std::to_string(saved.distinct));
@@ -263,16 +439,26 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             c->have_target = 1;
             c->target_idx = ((u64)r << 48) | (rows[(size_t)r].viol >> 4);
         }
-    // the per-level stop vote runs only when some rank passed a progress callback
+    // every rank's frontier size (replicated levels need them all), and
+    // whether some rank passed a progress callback (the per-level stop vote
+    // runs only then)
+    std::vector<u64> fsz((size_t)W);
     int any_cb = 0;
     {
-        const int mine = cb ? 1 : 0;
-        std::vector<int> all((size_t)W);
-        if (int rc = allgather(c, &mine, sizeof mine, all.data())) return rc;
-        for (int x : all) any_cb |= x;
+        D.phase = "start (frontier sizes)";
+        const u64 mine[2] = {c->level_start.back() - c->level_start[c->level_start.size() - 2], cb ? 1ull : 0ull};
+        std::vector<u64> all(2 * (size_t)W);
+        if (int rc = allgather(c, mine, sizeof mine, all.data())) return rc;
+        for (int r = 0; r < W; ++r) {
+            fsz[(size_t)r] = all[2 * (size_t)r];
+            any_cb |= all[2 * (size_t)r + 1] ? 1 : 0;
+        }
     }
     u64 generated = resume ? saved.generated : 1, probes = resume ? saved.probes : 0;
     int depth = resume ? c->resume_depth : 1;
+    // Replicated levels: the plain kernel on shapes of <= 64 lanes, models
+    // with a CONSTRAINT on every field (the capacity pass reads the store)
+    const bool rep_ok = !verify && !c->sh.sym && c->P.off[10] <= 64 && !c->P.unbounded && D.rep_max > 0;
     // Round sizing: rho = most keys one round sends one owner, per expanded
     // state, from the previous rounds (it varies along a frontier: states
     // received from other ranks are appended after the local ones).  A round
@@ -282,16 +468,44 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     const u64 row_len = 4 * (u64)W + 1;  // cx: [2W] sent pairs, [1] novf, [2W] received pairs
     while (!c->have_target) {
         const u64 lo = c->level_start[(size_t)depth - 1], hi = c->level_start[(size_t)depth];
+        D.lvl = depth;
+        D.rnd = 0;
         if (c->cfg.max_depth > 0 && depth >= c->cfg.max_depth) {
-            u64 f = hi - lo;
-            std::vector<u64> all((size_t)W);
-            if (int rc = allgather(c, &f, 8, all.data())) return rc;
             c->res.left_on_queue = 0;
-            for (u64 x : all) c->res.left_on_queue += x;
+            for (u64 x : fsz) c->res.left_on_queue += x;
             break;
         }
+        if (D.stall_rank == me && D.stall_level == depth) {  // test hook: this rank stops answering
+            fprintf(stderr, "[rmc rank %d] RMC_DIST_STALL_RANK: stalling %.1f s at level %d\n", me, D.stall_s, depth);
+            std::this_thread::sleep_for(std::chrono::duration<double>(D.stall_s));
+        }
         if (int rc = reset_counters(c, true)) return rc;
-        lvl_now = depth;
+        bool rep_timed = false;
+        u64 ftot = 0;
+        for (u64 x : fsz) ftot += x;
+        if (rep_ok && ftot <= D.rep_max) {
+            // ---- a replicated level: every rank gathers the whole frontier,
+            // expands all of it and keeps the successors it owns; no key or
+            // state exchange, one all-gather of the level's records
+            D.phase = "replicated level (frontier all-gather)";
+            if (hi > lo) HIPCHK(c, launch(c->sh, 13, c->P, c->PT, c->B, lo, hi, nullptr, D.rep_send, 0, nullptr, c->st));
+            HIPCHK(c, hipEventRecord(D.ev_c, c->st));
+            HIPCHK(c, hipStreamWaitEvent(D.xs, D.ev_c, 0));
+            if (int rc = gather_level(c, fsz, RBR)) return rc;
+            HIPCHK(c, hipEventRecord(D.ev_x, D.xs));
+            HIPCHK(c, hipStreamWaitEvent(c->st, D.ev_x, 0));
+            D.phase = "replicated level (expansion)";
+            DevBufs Bb = c->B;
+            Bb.rep = D.rep_buf;
+            // one launch (rep_max <= 2^24 records); timed by events read after the level end
+            HIPCHK(c, hipEventRecord(D.set[0].k0, c->st));
+            HIPCHK(c, launch(c->sh, 12, c->P, c->PT, Bb, 0, ftot, nullptr, nullptr, 0, nullptr, c->st));
+            HIPCHK(c, hipEventRecord(D.set[0].k1, c->st));
+            rep_timed = ftot != 0;
+            c->res.expand_launches += 1;
+            D.rep_levels += 1;
+            D.chunks += 1;
+        } else {
         u64 cursor = lo, ovf_known = 0, ovf_done = 0;
         const u64 frontier = hi - lo;
         // at least D.split rounds for a large level, so one round's count
@@ -349,8 +563,10 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         for (u64 k = 0;; ++k) {
             const int b = (int)(k & 1);
             DistState::Set& S = D.set[b];
+            D.rnd = (int)k;
             const bool host_more = cursor < hi || ovf_done < ovf_known;
             // ---- count row of round k (after its expansion), on xs
+            D.phase = "count all-to-all";
             HIPCHK(c, hipStreamWaitEvent(D.xs, S.ev_exp, 0));
             HIPCHK(c, hipEventRecord(S.x0, D.xs));
             {
@@ -368,16 +584,15 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 if (int rc = enqueue_A(k + 1)) return rc;
                 next_queued = true;
             }
-            {
-                const double tw = now_s();
-                HIPCHK(c, hipEventSynchronize(D.ev_cnt));
-                D.wait_seconds += now_s() - tw;
-            }
+            if (int rc = xwait(c, D.ev_cnt)) return rc;
             const u64* cx = S.h_cx;
-            const u64 novf = cx[2 * W];
-            if (novf > c->B.ovf_cap)
-                return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(me) +
-                                                   " (raise keys_per_dest)");
+            // a rank whose parking buffer overflowed says so in its flags (bit 1):
+            // every rank sees every row and stops here alike
+            for (int p = 0; p < W; ++p)
+                if (cx[2 * W + 1 + 2 * p + 1] & 2u)
+                    return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(p) +
+                                                       " (raise keys_per_dest) at " + where(c));
+            const u64 novf = std::min(cx[2 * W], c->B.ovf_cap);  // never drain past the buffer
             const u64 newly_parked = novf - std::min(novf, ovf_known);
             D.parked += newly_parked;
             ovf_known = std::max(ovf_known, novf);
@@ -409,7 +624,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                         me, depth, (unsigned long long)k, round_kind[b], (unsigned long long)round_states[b],
                         (unsigned long long)mx, (unsigned long long)kcap, (unsigned long long)ovf_done,
                         (unsigned long long)ovf_known, (unsigned long long)tot_in, rho, (int)global_more);
-            if (tot_in > D.in_cap) return fail(c, RMC_E_CAPACITY, "phase-1 inbox full");
+            if (tot_in > D.in_cap) return fail(c, RMC_E_CAPACITY, "phase-1 inbox full at " + where(c));
             if (global_more && !next_queued) {
                 if (int rc = enqueue_A(k + 1)) return rc;
                 next_queued = true;
@@ -430,6 +645,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 continue;
             }
             // ---- phase 1: keys to their owners, replies back; phase 2 sizes
+            D.phase = "phase 1 (keys to owners)";
             HIPCHK(c, hipMemsetAsync(D.sa, 0, 16 * (u64)W, D.xs));
             if (int rc = a2a(c, S.key_out, soff.data(), scnt.data(), D.key_in, roff.data(), rcnt.data())) return rc;
             SrcOff so{};
@@ -442,6 +658,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 r2[(size_t)p] = scnt[(size_t)p] / 8;
                 q2[(size_t)p] = (u64)p * kcap;
             }
+            D.phase = "phase 1 (replies)";
             if (int rc = a2a(c, D.rep_out, o2.data(), s2.data(), D.rep_in, q2.data(), r2.data())) return rc;
             if (mx) {
                 DevBufs Bb = c->B;
@@ -454,12 +671,9 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             HIPCHK(c, hipEventRecord(S.ev_free, D.xs));  // the set's keys and tickets are consumed
             HIPCHK(c, hipMemcpyAsync(D.h_sa, D.sa, 16 * (u64)W, hipMemcpyDeviceToHost, D.xs));
             HIPCHK(c, hipEventRecord(D.ev_acc, D.xs));
-            {
-                const double tw = now_s();
-                HIPCHK(c, hipEventSynchronize(D.ev_acc));
-                D.wait_seconds += now_s() - tw;
-            }
+            if (int rc = xwait(c, D.ev_acc)) return rc;
             // ---- phase 2: the accepted states
+            D.phase = "phase 2 (states to owners)";
             u64 tot_st = 0;
             for (int p = 0; p < W; ++p) {
                 // verification ships every key's state (the seen ones to be compared)
@@ -472,19 +686,21 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 tot_st += rcnt[(size_t)p] / RB;
                 if (p != me) D.states_sent += ns;
             }
-            if (tot_st > (u64)W * kcap) return fail(c, RMC_E_CAPACITY, "phase-2 inbox full");
+            if (tot_st > (u64)W * kcap) return fail(c, RMC_E_CAPACITY, "phase-2 inbox full at " + where(c));
             if (int rc = a2a(c, c->B.st_out, soff.data(), scnt.data(), D.st_in, roff.data(), rcnt.data())) return rc;
             if (tot_st)
                 HIPCHK(c, launch(c->sh, 9, c->P, c->PT, c->B, tot_st, 0, D.st_in, nullptr, 0, nullptr, D.xs));
             if (verify && tot_st) {  // publish the received new states, then compare the seen ones
-                HIPCHK(c, hipStreamSynchronize(D.xs));
+                HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+                if (int rc = xwait(c, D.ev_h)) return rc;
                 if (int rc = read_counters(c)) return rc;
                 const u64 c2 = c->h_ctr->count;
                 if (c2 > vpub)
                     HIPCHK(c, launch(c->sh, 5, c->P, c->PT, c->B, vpub, c2, nullptr, nullptr, 0, nullptr, D.xs));
                 vpub = c2;
                 HIPCHK(c, launch(c->sh, 11, c->P, c->PT, c->B, tot_st, 0, D.st_in, nullptr, 0, nullptr, D.xs));
-                HIPCHK(c, hipStreamSynchronize(D.xs));
+                HIPCHK(c, hipEventRecord(D.ev_h, D.xs));
+                if (int rc = xwait(c, D.ev_h)) return rc;
             }
             HIPCHK(c, hipEventRecord(S.x1, D.xs));
             S.xtimed = 1;
@@ -494,22 +710,35 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         // expansion of the next level reads what xs stored: the ctx stream waits for it
         HIPCHK(c, hipEventRecord(D.ev_x, D.xs));
         HIPCHK(c, hipStreamWaitEvent(c->st, D.ev_x, 0));
+        }
         if (int rc = level_end()) return rc;
+        if (rep_timed) {  // a replicated level's launch (complete: the counters were gathered after it)
+            c->res.expand_kernel_seconds += 1e-3 * elapsed_ms(D.set[0].k0, D.set[0].k1);
+            rep_timed = false;
+        }
         for (auto& S2 : D.set)  // exchange device time of the level's last round
             if (S2.xtimed) {
                 D.xfer_seconds += 1e-3 * elapsed_ms(S2.x0, S2.x1);
                 S2.xtimed = 0;
             }
         u64 tot = 0, gen = 0, pr = 0;
-        for (const auto& r : rows) {
-            tot += r.count; gen += r.generated; pr += r.probes;
-            c->res.collisions += r.collisions;
-            c->res.verified += r.vchecked;
+        for (int r = 0; r < W; ++r) {
+            const Counters& k = rows[(size_t)r];
+            tot += k.count;
+            gen += k.generated;
+            pr += k.probes;
+            c->res.collisions += k.collisions;
+            c->res.verified += k.vchecked;
         }
         const u64 nnew = tot - total_prev;
         total_prev = tot;
         generated += gen;
         probes += pr;
+        // the next level's frontier on every rank: the states it stored in this one
+        for (int r = 0; r < W; ++r) {
+            fsz[(size_t)r] = rows[(size_t)r].count - count_before[(size_t)r];
+            count_before[(size_t)r] = rows[(size_t)r].count;
+        }
         c->level_start.push_back(c->h_ctr->count);
         if (nnew) ++depth;
         for (int r = 0; r < W && !c->have_target; ++r)  // the lowest rank's least violating index
@@ -535,6 +764,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             ls.seconds = now_s() - t0;
             const int stop = (cb && cb(&ls, user)) ? 1 : 0;
             std::vector<int> votes((size_t)W);
+            D.phase = "progress vote";
             if (int rc = allgather(c, &stop, sizeof stop, votes.data())) return rc;
             if (votes[0]) {
                 c->res.left_on_queue = nnew;
@@ -558,6 +788,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     const double Dd = (double)total_prev, G = (double)generated;
     c->res.collision_probability = Dd * (G - Dd) / 18446744073709551616.0;
     c->res.seconds = now_s() - t0;
+    D.phase = "done";
     return 0;
 }
 
@@ -629,6 +860,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     if (!rccl_id && !(host && host->alltoallv && host->allgather))
         return fail(c, RMC_E_INVAL, "rmc_shard needs an RCCL id or a host transport");
     if (c->spill.on) return fail(c, RMC_E_INVAL, "sharded mode does not support RMC_FLAG_SPILL");
+    if (c->wide) return fail(c, RMC_E_INVAL, "sharded mode runs the packed layout only (bounds within its capacity)");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     free_dist(c);
     DistState& D = c->dist;
@@ -653,7 +885,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
               hipSuccess;
     // full-state verification ships every remote successor: no sent-cache
     // (the default kernel keeps send markers in the fingerprint set instead)
-    if (!c->sh.verify && (c->sh.sym || dist_uses_sent_cache())) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
+    if (!c->sh.verify && c->sh.sym) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
     const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
     ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
     for (auto& S : D.set) {
@@ -664,8 +896,17 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
             ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
         for (hipEvent_t* e : {&S.k0, &S.k1, &S.x0, &S.x1}) ok = ok && hipEventCreate(e) == hipSuccess;
     }
-    for (hipEvent_t* e : {&D.ev_cnt, &D.ev_acc, &D.ev_c, &D.ev_x})
+    for (hipEvent_t* e : {&D.ev_cnt, &D.ev_acc, &D.ev_c, &D.ev_x, &D.ev_h})
         ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    // replicated levels: levels of at most rep_max states in total are gathered
+    // whole on every rank (RMC_DIST_REP states; 0 turns them off)
+    D.rep_max = 1ull << 20;
+    if (const char* e = getenv("RMC_DIST_REP")) D.rep_max = std::min<u64>((u64)atoll(e), 1ull << 24);
+    if (D.rep_max) {
+        const u64 rbr = (u64)(c->NW + 6) * 4;
+        ok = ok && hipMalloc(&D.rep_send, D.rep_max * rbr) == hipSuccess &&
+             hipMalloc(&D.rep_buf, D.rep_max * rbr) == hipSuccess;
+    }
     ok = ok && hipMalloc(&D.key_in, W * kcap * 8) == hipSuccess && hipMalloc(&D.rep_out, W * kcap) == hipSuccess &&
          hipMalloc(&D.rep_in, W * kcap) == hipSuccess && hipMalloc(&c->B.st_out, W * kcap * RB) == hipSuccess &&
          hipMalloc(&D.st_in, W * kcap * RB) == hipSuccess && hipMalloc(&D.sa, 16 * W) == hipSuccess &&
@@ -678,7 +919,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     // send markers share the fingerprint set with this rank's states: twice the
     // slots keeps the load of linear probing near the single-GPU one (when
     // HBM allows; otherwise the set stays as rmc_create sized it)
-    if (world > 1 && !c->sh.verify && !c->sh.sym && !dist_uses_sent_cache() && !D.table_grown) {
+    if (world > 1 && !c->sh.verify && !c->sh.sym && !D.table_grown) {
         u64* t2 = nullptr;
         if (hipMalloc(&t2, c->table_slots * 16) == hipSuccess) {
             (void)hipFree(c->B.table);
@@ -707,13 +948,39 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     // SYMMETRY: the states of one orbit must meet at one owner, so the owner is
     // a function of the canonical fingerprint (server words differ across the orbit)
     if (c->sh.sym) c->B.owner_mode = 0;
+    D.timeout_s = 300.0;
+    if (const char* e = getenv("RMC_DIST_TIMEOUT_S")) D.timeout_s = std::max(0.1, atof(e));
+    // test hook: rank RMC_DIST_STALL_RANK sleeps RMC_DIST_STALL_S (default twice
+    // the deadline) before level RMC_DIST_STALL_LEVEL (default 2)
+    D.stall_rank = -1;
+    if (const char* e = getenv("RMC_DIST_STALL_RANK")) D.stall_rank = atoi(e);
+    D.stall_level = 2;
+    if (const char* e = getenv("RMC_DIST_STALL_LEVEL")) D.stall_level = atoi(e);
+    D.stall_s = 2 * D.timeout_s;
+    if (const char* e = getenv("RMC_DIST_STALL_S")) D.stall_s = atof(e);
+    D.lvl = 0;
+    D.rnd = 0;
+    D.phase = "communicator init";
     if (D.rccl) {
         ncclUniqueId u;
         memcpy(&u, rccl_id, sizeof u);
-        ncclResult_t r = ncclCommInitRank(&D.comm, world, u, rank);
-        if (r != ncclSuccess) {
+        // non-blocking (RMC_DIST_NCCL_BLOCKING=1: the blocking mode, A/B): every
+        // call is polled under the deadline, connection set-up included
+        D.nonblocking = 1;
+        if (const char* e = getenv("RMC_DIST_NCCL_BLOCKING")) D.nonblocking = atoi(e) ? 0 : 1;
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = D.nonblocking ? 0 : 1;
+        ncclResult_t r = ncclCommInitRankConfig(&D.comm, world, u, rank, &cfg);
+        if (r != ncclSuccess && r != ncclInProgress) {
+            D.comm = nullptr;
             free_dist(c);
-            return fail(c, RMC_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+            return fail(c, RMC_E_HIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+        }
+        if (int rc = nccl_done(c, r, "ncclCommInitRankConfig (waiting for every rank)")) {
+            const std::string msg = c->err;
+            free_dist(c);
+            c->err = msg;
+            return rc;
         }
     }
     D.on = 1;

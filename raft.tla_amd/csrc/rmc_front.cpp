@@ -886,22 +886,22 @@ static int parse_model(const char* cfg_path, const char* tla_path, const char* r
     g.max_log_len = bd.log;
     g.max_msgs = bd.msgs;
     g.max_dup = bd.dup;
-    if (simulate) {  // unbounded fields: the packed capacity (rmc_simulate truncates beyond it)
-        if (g.max_term < 0) g.max_term = RMC_MAX_TERM;
-        if (g.max_log_len < 0) g.max_log_len = RMC_MAX_LOG;
-        if (g.max_msgs < 0) g.max_msgs = RMC_MAX_MSGS;
-        if (g.max_dup < 0) g.max_dup = RMC_MAX_DUP;
+    if (simulate) {  // unbounded fields: the wide layout's capacity (rmc_simulate truncates beyond it)
+        if (g.max_term < 0) g.max_term = RMC_WIDE_MAX_TERM;
+        if (g.max_log_len < 0) g.max_log_len = RMC_WIDE_MAX_LOG;
+        if (g.max_msgs < 0) g.max_msgs = RMC_WIDE_MAX_MSGS;
+        if (g.max_dup < 0) g.max_dup = RMC_WIDE_MAX_DUP;
     } else if (options & RMC_FRONT_DEPTH_BOUNDED) {
         // TLC -depth on a model that leaves fields unbounded (MCraft.cfg as
-        // shipped): the packed capacity, and a successor beyond it is an error
-        if (g.max_term < 0) { g.max_term = RMC_MAX_TERM; flags |= RMC_FLAG_UNBOUNDED_TERM; }
-        if (g.max_log_len < 0) { g.max_log_len = RMC_MAX_LOG; flags |= RMC_FLAG_UNBOUNDED_LOG; }
-        if (g.max_msgs < 0) { g.max_msgs = RMC_MAX_MSGS; flags |= RMC_FLAG_UNBOUNDED_MSGS; }
-        if (g.max_dup < 0) { g.max_dup = RMC_MAX_DUP; flags |= RMC_FLAG_UNBOUNDED_DUP; }
+        // shipped): the wide layout's capacity, and a successor beyond it is an error
+        if (g.max_term < 0) { g.max_term = RMC_WIDE_MAX_TERM; flags |= RMC_FLAG_UNBOUNDED_TERM; }
+        if (g.max_log_len < 0) { g.max_log_len = RMC_WIDE_MAX_LOG; flags |= RMC_FLAG_UNBOUNDED_LOG; }
+        if (g.max_msgs < 0) { g.max_msgs = RMC_WIDE_MAX_MSGS; flags |= RMC_FLAG_UNBOUNDED_MSGS; }
+        if (g.max_dup < 0) { g.max_dup = RMC_WIDE_MAX_DUP; flags |= RMC_FLAG_UNBOUNDED_DUP; }
         if (flags & (RMC_FLAG_UNBOUNDED_TERM | RMC_FLAG_UNBOUNDED_LOG | RMC_FLAG_UNBOUNDED_MSGS | RMC_FLAG_UNBOUNDED_DUP))
-            notes.push_back("no CONSTRAINT bounds every field: the search runs under the depth bound and stops with a "
-                            "capacity error if a successor exceeds the packed capacity (currentTerm 14, Len(log) 3, "
-                            "8 messages, count 3)");
+            notes.push_back("no CONSTRAINT bounds every field: the search runs under the depth bound on the wide "
+                            "layout and stops with a capacity error if a successor exceeds it (currentTerm 255, "
+                            "Len(log) 8, 16 messages, count 255)");
     }
     if (g.max_term < 0 || g.max_log_len < 0 || g.max_msgs < 0 || g.max_dup < 0)
         return fail("the model is infinite without a CONSTRAINT bounding currentTerm, Len(log), "

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "raft_packed.h"
+#include "raft_wide.h"
 
 namespace rmc {
 
@@ -29,6 +30,8 @@ struct DevBufs {
     u64* parent;     // parent index per state (~0 for initial states)
     uint8_t* act;    // lane that produced the state (255 for initial states)
     u64* foot;       // messages the producing lane acted on / added (make_foot; 0 = unknown)
+    uint8_t* cls;    // window-sort class of each state (state_class_fine; a layout hint)
+    uint16_t* word;  // presorted windows (k_window_order): the launch's window positions in class order
     u64* table;      // fingerprint set, power-of-two slots, 0 = empty
     u64 tmask;       // slots - 1
     u64 cap;         // state store capacity
@@ -51,6 +54,9 @@ struct DevBufs {
     // sent in later exchange rounds of the same level (never dropped)
     u64* ovf;
     u64 ovf_cap;               // records in ovf
+    // replicated levels (small levels of a sharded search): the whole level's
+    // records, gathered from every rank (RepRec: state, global ref, footprint, lane | class)
+    const u32* rep;
     // full-state verification mode: store index of the state owning each
     // fingerprint-set slot (~0 = not yet published; published between launches
     // by k_publish) and the deferred hits {parent index, slot | lane << 56}
@@ -83,7 +89,9 @@ struct Shape {
 //        5 = k_publish over store[a, b) (verification: slot -> store index);
 //        6 = k_verify of `a` deferred hits in B.vbuf;
 //        7 = k_rehash of the stored states [a, b) (recovery).
-//       11 = k_compare_remote of `a` received state records `in` (sharded verification).
+//       11 = k_compare_remote of `a` received state records `in` (sharded verification);
+//       12 = k_expand_dist<REP> over the replicated level's records B.rep[a, b);
+//       13 = k_pack_rep of this rank's stored states [a, b) into records at `out`.
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 
@@ -106,14 +114,14 @@ hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply
                                unsigned long long* acc, hipStream_t st);
 // Sharded mode: the exchange-count row of one round, out[2p] = keys for rank p
 // (min(ocount[p], kcap), 0 for p = rank), out[2p + 1] = flags (bit 0: this rank
-// has more to send: host_more, or parked keys beyond ovf_done), out[2W] = novf.
+// has more to send: host_more, or parked keys beyond ovf_done; bit 1: its
+// parking buffer overflowed), out[2W] = novf.
 hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st);
+// Presorted windows: k_window_order over the launch [lo, hi) for an expansion
+// grid of `grid` blocks and windows of at most wt_max tiles (B.word).
+hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st);
 // Sharded mode: move parked keys ovf[a, a + n) into the (emptied) outbox; n <= kcap.
 hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st);
-
-// Sharded expansion: does the selected kernel (RMC_DIST_VARIANT) use the lossy
-// sent-cache B.sent, or send markers in the fingerprint set?
-bool dist_uses_sent_cache();
 
 // Fingerprint salt for the kernels of shape sh on this device (0 = default
 // hash); returns after the copy (the staging value lives on the caller's stack).
@@ -121,5 +129,31 @@ hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st);
 
 // Random-probe microbenchmark over table[mask + 1] (mode 0 loads, 1 CAS).
 hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st);
+
+// ---- the wide layout (raft_wide.h, rmc_wide.hip) ------------------------------------
+namespace wide {
+struct WideBufs {
+    WState* store;    // wide records; levels are contiguous ranges
+    u64* parent;      // parent index per state (~0 for initial states)
+    uint8_t* act;     // lane that produced the state (255 for initial states)
+    u64* table;       // fingerprint set (wfp keys), power-of-two slots
+    u64 tmask, cap;
+    Counters* ctr;
+    u64 salt;         // fingerprint salt (rmc_config.seed)
+};
+// One successor listed by k_wlist (rmc_expand on the wide layout).
+struct WSucc {
+    u64 parent;
+    int lane, code, in_model, pad;
+    u64 fp;
+    WState state;
+};
+hipError_t launch_wseed(const WModel& M, const WideBufs& B, const WState* staged, u64 n, hipStream_t st);
+hipError_t launch_wexpand(const WModel& M, const WideBufs& B, u64 lo, u64 hi, hipStream_t st);
+hipError_t launch_wlist(const WModel& M, const WState* in, u64 n, WSucc* out, u64 cap, unsigned long long* count,
+                        u64 salt, hipStream_t st);
+hipError_t launch_wsimulate(const WModel& M, const WState* inits, u64 n_init, u64 n_beh, int depth, u64 seed, int mode,
+                            SimCounters* out, i64 rec_beh, WState* rec, hipStream_t st);
+}  // namespace wide
 
 }  // namespace rmc

@@ -107,6 +107,23 @@ __device__ __forceinline__ void store_state(u32* __restrict__ base, const u64 (&
     for (int q = 0; q < K; ++q) base[2 * S + q] = m[q];
 }
 
+// Store one new state at index ni: the packed state, its trace link (global
+// parent ref, lane), the footprint of its discovering lane (commuting
+// diamonds; only shapes whose kernels skip diamonds keep them), its
+// window-sort class (B.cls: a layout hint, read 1 B per state by the next
+// level's window sort) and the fused invariant check.
+template <int S, int K>
+__device__ __forceinline__ void store_new(const Params& P, const DevBufs& B, u64 ni, const u64 (&wo)[S],
+                                          const u32 (&mo)[K], u64 parent, int lane, u64 foot) {
+    store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
+    B.parent[ni] = parent;
+    B.act[ni] = (uint8_t)lane;
+    if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = foot;
+    B.cls[ni] = (uint8_t)state_class_fine<S, K>(wo, mo);
+    const int v = check_invariants<S, K>(wo, mo, P);
+    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
+}
+
 // Wave-aggregated allocation of store slots for the lanes with is_new set,
 // then materialise + store + parent + invariants.  Must be reached by every
 // lane of the wave (it contains a ballot).
@@ -129,12 +146,8 @@ __device__ __forceinline__ void commit_new(int is_new, const u64 (&w)[S], const 
     u64 wo[S];
     u32 mo[K];
     materialise<S, K>(w, m, d, wo, mo);
-    store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
-    B.parent[ni] = parent_idx;
-    B.act[ni] = (uint8_t)lane;
-    B.foot[ni] = 0;  // initial states and deferred SYMMETRY ties: no diamond skipping from them
-    const int v = check_invariants<S, K>(wo, mo, P);
-    if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
+    // initial states and deferred SYMMETRY ties: no diamond skipping from them
+    store_new<S, K>(P, B, ni, wo, mo, parent_idx, lane, 0ull);
 }
 
 // Per-wave list of new states, kept in LDS until a flush materialises them.
@@ -145,16 +158,28 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Replicated levels (sharded mode): one record per frontier state of the
+// whole level, gathered from every rank — the packed state, its global ref
+// (rank << 48 | index), its footprint and lane | class << 8 (k_pack_rep).
+template <int S, int K>
+struct RepRec {
+    static constexpr int NW = 2 * S + K;
+    static constexpr int REF = NW, FOOT = NW + 2, ACT = NW + 4;
+    static constexpr int RR = NW + 6;  // words per record (8-byte aligned: NW is even)
+};
+
 // Materialise the wave's n listed new states: ONE global allocation atomic per
 // flush, then each lane re-derives one listed successor from its parent
 // (same lane_delta code, deterministic), stores it, its parent pointer and
 // lane, and runs the fused invariant checks.  Convergent: the whole wave
 // runs it together, so the rare new-state path does not serialise the
-// per-lane expansion loop.
-template <int S, int K>
+// per-lane expansion loop.  REP: the parents are replicated-level records
+// (B.rep), their refs global.
+template <int S, int K, bool REP = false>
 __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
                                           const uint8_t* l_lane, u32 n) {
     constexpr int NW = 2 * S + K;
+    typedef RepRec<S, K> RR;
     wave_sync_lds();
     const int me = (int)__lane_id();
     u64 base = 0;
@@ -170,85 +195,23 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         }
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        const u32* pr = REP ? B.rep + (lo + rel) * (u64)RR::RR : B.store + (lo + rel) * (u64)NW;
+        load_state<S, K>(pr, w, m);
         Delta d;
-        lane_delta<S, K>(w, m, lane, P, d);
-        u64 wo[S];
-        u32 mo[K];
-        materialise<S, K>(w, m, d, wo, mo);
-        store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
-        B.parent[ni] = B.ref_tag | (lo + rel);
-        B.act[ni] = (uint8_t)lane;
-        if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = make_foot<S, K>(m, lane, d, P);  // diamonds: sorted kernels only
-        const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
-    }
-    wave_sync_lds();
-}
-
-// flush_new with the batch written in succ_class order (a counting sort over
-// 256 classes in LDS, two 16-bit counters per word): consecutive new states
-// then share their roles and message count, so the waves that expand them at
-// the next level walk fewer lanes (lane_superset).  The class of each listed
-// successor rides in the top byte of its l_rel entry (launches are at most
-// 2^24 states).  Positions inside a class follow LDS atomic order; the search
-// does not depend on the layout.
-template <int S, int K>
-__device__ __forceinline__ void flush_new_sorted(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
-                                                 const uint8_t* l_lane, u32* bins, u32 n) {
-    constexpr int NW = 2 * S + K;
-    wave_sync_lds();
-    const int me = (int)__lane_id();
-    bins[me] = 0;
-    bins[me + 64] = 0;
-    wave_sync_lds();
-    for (u32 e = (u32)me; e < n; e += 64) {
-        const u32 c = l_rel[e] >> 24;
-        atomicAdd(&bins[c >> 1], 1u << (16 * (c & 1u)));
-    }
-    wave_sync_lds();
-    // exclusive scan: lane me owns counters 4me .. 4me+3 (words 2me, 2me+1)
-    const u32 wa = bins[2 * me], wb = bins[2 * me + 1];
-    const u32 c0 = wa & 0xFFFFu, c1 = wa >> 16, c2 = wb & 0xFFFFu, c3 = wb >> 16;
-    const u32 tot = c0 + c1 + c2 + c3;
-    u32 incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const u32 v = (u32)__shfl_up((int)incl, off);
-        if (me >= off) incl += v;
-    }
-    const u32 ex = incl - tot;
-    bins[2 * me] = ex | ((ex + c0) << 16);
-    bins[2 * me + 1] = (ex + c0 + c1) | ((ex + c0 + c1 + c2) << 16);
-    wave_sync_lds();
-    u64 base = 0;
-    if (me == 0) base = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)n);
-    base = bcast64(base, 0);
-    for (u32 e = (u32)me; e < n; e += 64) {
-        const u32 rc = l_rel[e];
-        const u32 c = rc >> 24, sh = 16 * (c & 1u);
-        const u32 pos = (atomicAdd(&bins[c >> 1], 1u << sh) >> sh) & 0xFFFFu;
-        const u64 rel = rc & 0xFFFFFFu;
-        const int lane = l_lane[e];
-        const u64 ni = base + pos;
-        if (ni >= B.cap) {
-            atomicOr(&B.ctr->overflow, 1u);
-            continue;
+        u64 foot;
+        if constexpr (Lanes<S, K>::N <= 64) {  // the lane's descriptor: no family-offset compares
+            const u32 desc = P.ldesc[lane];
+            lane_delta_desc<S, K>(w, m, desc, P, d);
+            foot = make_foot_desc<S, K>(m, desc, d);
+        } else {
+            lane_delta<S, K>(w, m, lane, P, d);
+            foot = 0;
         }
-        u64 w[S];
-        u32 m[K];
-        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
-        Delta d;
-        lane_delta<S, K>(w, m, lane, P, d);
         u64 wo[S];
         u32 mo[K];
         materialise<S, K>(w, m, d, wo, mo);
-        store_state<S, K>(B.store + ni * (u64)NW, wo, mo);
-        B.parent[ni] = B.ref_tag | (lo + rel);
-        B.act[ni] = (uint8_t)lane;
-        if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = make_foot<S, K>(m, lane, d, P);  // diamonds: sorted kernels only
-        const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
+        const u64 parent = REP ? ((u64)pr[RR::REF] | ((u64)pr[RR::REF + 1] << 32)) : B.ref_tag | (lo + rel);
+        store_new<S, K>(P, B, ni, wo, mo, parent, lane, foot);
     }
     wave_sync_lds();
 }
@@ -439,16 +402,16 @@ __device__ __forceinline__ u32 owner_succ_w(u64 key, const Delta& d, const u64 (
     return owner_state<S>(key, ws, B);
 }
 // Owner of a successor from the parent's word mixes (pm.hw) and the new word's
-// mix hn (delta_fp_pre / delta_hash_pre): a lane that leaves the hashed words
-// alone keeps its parent's owner — this rank, since a state is stored by its
-// owner.
+// mix hn (delta_fp_pre): a lane that leaves the hashed words alone keeps its
+// parent's owner `powner` — this rank in the sharded kernel (a state is
+// expanded by its owner), the record's rank in a replicated level.
 template <int S, int K>
 __device__ __forceinline__ u32 owner_succ(u64 key, const Delta& d, const ParentMix<S, K>& pm, u64 hn,
-                                          const DevBufs& B) {
+                                          const DevBufs& B, u32 powner) {
     if (B.world == 1) return 0;
     if (B.owner_mode == 0) return owner_of(key, B.world);
     const int nw = owner_words<S>(B);
-    if (d.srv < 0 || d.srv >= nw) return B.rank;
+    if (d.srv < 0 || d.srv >= nw) return powner;
     u64 h = 0;
 #pragma unroll
     for (int i = 0; i < S; ++i) h += i < nw ? (i == d.srv ? hn : pm.hw[i]) : 0ull;
@@ -536,12 +499,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         u64 wo[S];
         u32 mo[K];
         materialise<S, K>(w, m, d, wo, mo);
-        store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
-        B.parent[slot] = B.ref_tag | (lo + rel);
-        B.act[slot] = (uint8_t)lane;
-        if constexpr (Lanes<S, K>::N <= 64) B.foot[slot] = make_foot<S, K>(m, lane, d, P);
-        const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
+        store_new<S, K>(P, B, slot, wo, mo, B.ref_tag | (lo + rel), lane, make_foot<S, K>(m, lane, d, P));
     }
     wave_sync_lds();
 }
@@ -599,7 +557,15 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
         u32 m[K];
         load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
         Delta d;
-        lane_delta<S, K>(w, m, lane, P, d);
+        u64 foot;
+        if constexpr (Lanes<S, K>::N <= 64) {  // the lane's descriptor: no family-offset compares
+            const u32 desc = P.ldesc[lane];
+            lane_delta_desc<S, K>(w, m, desc, P, d);
+            foot = make_foot_desc<S, K>(m, desc, d);
+        } else {
+            lane_delta<S, K>(w, m, lane, P, d);
+            foot = 0;
+        }
         u64 wo[S];
         u32 mo[K];
         materialise<S, K>(w, m, d, wo, mo);
@@ -619,12 +585,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
             B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
             continue;
         }
-        store_state<S, K>(B.store + slot * (u64)NW, wo, mo);
-        B.parent[slot] = B.ref_tag | (lo + rel);
-        B.act[slot] = (uint8_t)lane;
-        if constexpr (Lanes<S, K>::N <= 64) B.foot[slot] = make_foot<S, K>(m, lane, d, P);
-        const int v = check_invariants<S, K>(wo, mo, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((slot << 4) | (u64)(v - 1)));
+        store_new<S, K>(P, B, slot, wo, mo, B.ref_tag | (lo + rel), lane, foot);
     }
     wave_sync_lds();
 }
@@ -632,43 +593,49 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 // Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
 // processed BATCH at a time so BATCH fingerprint probes per thread are in
 // flight together (the kernel is bound by probe latency, not bandwidth).
-// DIST: sharded mode — successors owned by another rank are looked up in the
-// local sent-cache instead of the set and, if not sent before, shipped
-// through the outbox (flush_dist).
+// SORT: the lane-superset walk — each block takes windows of WTILES tiles and
+//   walks their states in class order (a counting sort in LDS over the 1-byte
+//   classes B.cls), so its waves hold states of one kind and walk only the
+//   lanes some state of the wave can enable (lane_superset, a scalar).
+// DIST: sharded mode — successors owned by another rank go to that owner's
+//   key outbox: with MARK (the default) after a CAS into the local set (send
+//   markers: a lossless sent-cache), else through the lossy sent-cache B.sent
+//   (SYMMETRY and verification).
 // DIA: commuting-diamond successors are not probed (raft_packed.h "commuting
-// diamonds"; P.diamond = 0 turns it off at run time).
-template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SYMINC = false,
-          bool SORT = false, bool WSORT = false, bool FSORT = true, bool DIA = false, bool EARLY = false,
-          bool MARK = false, int WTILES = 8, bool UPROBE = false, bool WFINE = true, int PIPE = 0>
+//   diamonds"; P.diamond = 0 turns it off at run time).
+// PIPE: a probe's load is issued as soon as its key is known, so the loads
+//   overlap the lane code of the batch's later lanes (266-272 vs 271-279 ms
+//   per bench BFS, profiles/r03/ab/probe_issue_r03pipe*.jsonl).
+// REP: a replicated level of the sharded search — [lo, hi) indexes the whole
+//   level's records in B.rep (gathered from every rank); every rank expands
+//   all of them and probes, stores and counts only the successors it owns.
+template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
+          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
     static_assert(!DIA || (!SYM && !VERIFY), "diamond skipping: not under SYMMETRY or verification");
-    // EARLY: the stutter / CONSTRAINT / diamond decisions come before the hash,
-    // so a lane that does not probe never hashes (needs the parent's mixes)
-    static_assert(!EARLY || (DIA && PRE), "EARLY needs DIA and PRE");
-    constexpr int NW = 2 * S + K;
-    constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
-    // SORT: class-sorted flushes + the wave walks only lane_superset's lanes
-    // WSORT: each block takes windows of 8 tiles and walks their states in
-    // state_class order (a counting sort in LDS), so its waves hold states of
-    // one kind; FSORT: flushes write new states class-sorted (flush_new_sorted)
     static_assert(!SORT || !VERIFY, "SORT: not with verification");
     static_assert(!SORT || BATCH * 7 <= 64, "SORT packs a batch's lanes 7 bits each into one u64");
-    static_assert(!(SORT && FSORT && (SYM || DIST)), "class-sorted flushes are built for the plain kernel only");
-    static_assert(!WSORT || SORT, "WSORT needs SORT");
-    // PIPE: a probe's load is issued as soon as its key is known, so the loads
-    // overlap the lane code of the batch's later lanes (266-272 vs 271-279 ms
-    // per bench BFS, profiles/r03/ab/probe_issue_r03pipe*.jsonl).  Measured and
-    // removed: issuing per half batch (268-274 ms), and the window's next state
-    // prefetched into registers as well (269-272 ms, 2 VGPRs spilled).
-    static_assert(PIPE == 0 || (!SYM && !VERIFY && !SENTC && !UPROBE), "PIPE: the plain and marker kernels");
-    // (the marker kernel measured no gain from it at one rank: 308.7-309.7 vs 307.4-308.7 ms)
-    constexpr int WT = WSORT ? WTILES : 1;  // tiles per window
-    __shared__ uint16_t s_ord[WSORT ? 256 * WT : 1];  // WSORT: window positions in class order
-    __shared__ uint8_t s_wcls[WSORT ? 256 * WT : 1];  // WSORT: class of each window position
-    constexpr int NBIN = WFINE ? 256 : 64;            // WFINE (default): roles x message-count classes
-    __shared__ u32 s_wbin[WSORT ? NBIN : 1];          // WSORT: class counters / cursors
+    static_assert(PIPE == 0 || (!SYM && !VERIFY && !SENTC), "PIPE: the plain and marker kernels");
+    static_assert(!REP || (MARK && SORT && PRE), "replicated levels: the plain sharded kernel");
+    // PRESORT: the windows were counting-sorted by class before the launch
+    // (k_window_order writes each window's positions in class order to B.word),
+    // so the kernel carries no sort: no LDS bins, scan or block barriers
+    static_assert(!PRESORT || (SORT && !REP), "presorted windows: the sorted kernels");
+    constexpr bool INSORT = SORT && !PRESORT;
+    // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
+    constexpr int NW = 2 * S + K;
+    typedef RepRec<S, K> RR;
+    constexpr int FW = REP ? RR::RR : NW;  // words per frontier record
+    const u32* const fr = REP ? B.rep : B.store;
+    constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
+    constexpr bool LISTOWN = DIST && !REP;  // list entries carry their owner
+    constexpr int WT = SORT ? WTILES : 1;   // tiles per window
+    __shared__ uint16_t s_ord[INSORT ? 256 * WT : 1];  // window positions in class order
+    __shared__ uint8_t s_wcls[INSORT ? 256 * WT : 1];  // class of each window position
+    constexpr int NBIN = 256;                           // roles x message-count classes
+    __shared__ u32 s_wbin[INSORT ? NBIN : 1];           // class counters / cursors
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
@@ -678,8 +645,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     __shared__ uint8_t s_dest[SENTC ? 4 : 1][SENTC ? LCAP : 1];
     __shared__ u64 s_lkey[SENTC ? 4 : 1][SENTC ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
-    __shared__ uint8_t s_own[DIST ? BATCH : 1][DIST ? 256 : 1];  // owner rank per probe
-    __shared__ u32 s_bins[SORT && FSORT ? 4 : 1][SORT && FSORT ? 128 : 1];  // FSORT: 256 16-bit class counters
+    __shared__ uint8_t s_own[LISTOWN ? BATCH : 1][LISTOWN ? 256 : 1];  // owner rank per probe
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
     const u64 lt_mask = (1ull << me) - 1ull;
@@ -693,25 +659,25 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
     const u64 nf = hi - lo;
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
-    // WSORT: tiles per window, fewer when the launch has too few states to
-    // give every block a full window (small levels would idle most blocks)
+    // tiles per window, fewer when the launch has too few states to give every
+    // block a full window (small levels would idle most blocks)
     u64 wt = WT;
-    if constexpr (WSORT) {
+    if constexpr (SORT) {
         const u64 per_block = (nf + (u64)gridDim.x * 256ull - 1) / ((u64)gridDim.x * 256ull);
         wt = per_block < (u64)WT ? (per_block ? per_block : 1ull) : (u64)WT;
     }
     for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {  // block-uniform
-    u32 wn = 0;  // WSORT: states in this window
-    if constexpr (WSORT) {
-        wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
+    u32 wn = 0;  // SORT: states in this window
+    if constexpr (SORT) wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
+    if constexpr (INSORT) {
         __syncthreads();  // the previous window's s_ord is consumed
         if (threadIdx.x < NBIN) s_wbin[threadIdx.x] = 0;
         __syncthreads();
         for (int k = 0; k < (int)wt; ++k) {
             const u32 p = (u32)k * 256u + threadIdx.x;
             if (p < wn) {
-                const u64* st = reinterpret_cast<const u64*>(B.store + (lo + win + p) * (u64)NW);
-                const u32 c = WFINE ? state_class_fine<S, K>(st) : state_class<S>(st);
+                // the stored 1-byte class (B.cls / the record's class byte), not the state
+                const u32 c = REP ? (fr[(lo + win + p) * (u64)FW + RR::ACT] >> 8) & 0xFFu : (u32)B.cls[lo + win + p];
                 s_wcls[p] = (uint8_t)c;
                 atomicAdd(&s_wbin[c], 1u);
             }
@@ -742,23 +708,33 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     for (int wk = 0; wk < (int)wt; ++wk) {
         u64 rel;
         bool live;
-        if constexpr (WSORT) {
+        if constexpr (SORT) {
             const u32 p = (u32)wk * 256u + threadIdx.x;
             live = p < wn;
-            rel = win + (live ? s_ord[p] : 0u);
+            if constexpr (PRESORT) rel = win + (live ? (u32)B.word[win + p] : 0u);
+            else rel = win + (live ? s_ord[p] : 0u);
         } else {
             rel = win + threadIdx.x;
             live = rel < nf;
         }
         u64 w[S];
         u32 m[K];
+        const u32* rec = fr + (lo + rel) * (u64)FW;
         if (live) {
-            load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+            load_state<S, K>(rec, w, m);
         } else {
 #pragma unroll
             for (int i = 0; i < S; ++i) w[i] = 0;
 #pragma unroll
             for (int q = 0; q < K; ++q) m[q] = 0;
+        }
+        // REP: the record's rank; only this rank's own states count as generated
+        // (every rank expands every state) and as deadlocks
+        u32 powner = B.rank;
+        bool mine = true;
+        if constexpr (REP) {
+            powner = live ? (rec[RR::REF + 1] >> 16) & 0xFFu : B.rank;
+            mine = powner == B.rank;
         }
         ParentMix<S, K> pmx;
         u64 h0;
@@ -774,12 +750,21 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
 #pragma unroll
             for (int i = 0; i < S; ++i) sbase[i] = sig_base<S>(w[i], (u32)i);
         }
-        SymParent<S, K> spar;  // SYMMETRY, incremental keys: the parent's frame
-        if constexpr (SYMINC) sym_parent<S, K>(w, m, sbase, spar);
         Diamond dm;  // DIA: how this state was discovered (lane + footprint), once per state
         if constexpr (DIA) {
             const bool on = live && P.diamond;
-            diamond_of<S, K>(m, on ? (int)B.act[lo + rel] : 255, on ? B.foot[lo + rel] : 0ull, P, dm);
+            int act = 255;
+            u64 foot = 0;
+            if (on) {
+                if constexpr (REP) {
+                    act = (int)(rec[RR::ACT] & 0xFFu);
+                    foot = (u64)rec[RR::FOOT] | ((u64)rec[RR::FOOT + 1] << 32);
+                } else {
+                    act = (int)B.act[lo + rel];
+                    foot = B.foot[lo + rel];
+                }
+            }
+            diamond_of<S, K>(m, act, foot, P, dm);
         }
         u32 g = 0;
         // SORT: the lanes some state of this wave can enable (wave-uniform, scalar)
@@ -787,7 +772,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         if constexpr (SORT) wm = wave_or64(live ? lane_superset<S, K>(w, m, P.V) : 0ull);
         for (int lane0 = 0; SORT ? (wm != 0) : (lane0 < nl); lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
             u64 lp = 0;  // SORT: this batch's lanes, 7 bits each (127 = none), a scalar
-            u64 cp = 0;  // SORT: the succ_class of each lane's successor, 8 bits each
             if constexpr (SORT) {
 #pragma unroll
                 for (int b = 0; b < BATCH; ++b) {
@@ -801,7 +785,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             // Rolled under SYMMETRY: one copy of the canonicalisation in flight.
             // (Rolling the plain kernel too, one copy of the lane code instead of
             // 8, measured no difference: instruction-cache misses are ~1e-5.)
-#pragma unroll(SYM ? 1 : BATCH)
+#ifndef RMC_LANE_UNROLL
+#define RMC_LANE_UNROLL BATCH
+#endif
+            constexpr int UNROLL = SYM ? 1 : RMC_LANE_UNROLL;
+#pragma unroll UNROLL
             for (int b = 0; b < BATCH; ++b) {
                 const int lane = SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b;
                 u64 key = 0;
@@ -811,7 +799,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     if constexpr (SORT) lane_delta_desc<S, K>(w, m, P.ldesc[SORT ? lane : 0], P, d);  // scalar descriptor
                     else lane_delta<S, K>(w, m, lane, P, d);
                     const int en = d.en && live;
-                    g += (u32)en;
+                    g += (u32)(en && mine);
                     u64 h = 0;
                     u64 hwn = 0;  // DIST: the mix of the changed server word (owner routing)
                     int in_model = 0;
@@ -821,10 +809,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         if (en && !stutter && delta_in_model<S, K>(m, d, P)) {
                             in_model = 1;
                             if constexpr (TIEDEFER) {  // tied signatures: k_ties canonicalises it after this launch
-                                if constexpr (SYMINC)
-                                    h = canon_delta_inc<S, K>(w, m, sbase, spar, d, PT.code, PT.np, &tied);
-                                else
-                                    h = canon_delta<S, K, true>(w, m, sbase, d, PT.code, PT.np, &tied);
+                                h = canon_delta<S, K, true>(w, m, sbase, d, PT.code, PT.np, &tied);
                                 if (tied) in_model = 0;
                             } else {
                                 h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
@@ -832,31 +817,25 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         }
                     } else if (en) {
                         int nmb = 0;
-                        if constexpr (EARLY) {
-                            const bool stutter = d.rm < 0 && !d.has_add && (d.srv < 0 || d.w_new == selw<S>(w, d.srv));
-                            in_model = !stutter && delta_bounds_pre<S, K>(m, pmx, d, P, &nmb) &&
-                                       !(SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d, nmb, dm)
-                                              : diamond_skip<S, K>(m, lane, d, nmb, dm, P));
-                            h = in_model ? delta_hash_pre<S, K>(w, m, pmx, d, DIST ? &hwn : nullptr) : h0;
-                        } else {
-                            if constexpr (PRE)
-                                in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr,
-                                                              DIST ? &hwn : nullptr);
-                            else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
-                            if constexpr (DIA)
-                                if (in_model && h != h0 &&
-                                    (SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d, nmb, dm)
-                                          : diamond_skip<S, K>(m, lane, d, nmb, dm, P)))
-                                    in_model = 0;
-                        }
-                        if constexpr (SORT && FSORT) cp |= (u64)succ_class<S, K>(w, m, d) << (8 * b);
+                        if constexpr (PRE)
+                            in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr,
+                                                          DIST ? &hwn : nullptr);
+                        else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
+                        if constexpr (DIA)
+                            if (in_model && h != h0 &&
+                                (SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d, nmb, dm)
+                                      : diamond_skip<S, K>(m, lane, d, nmb, dm, P)))
+                                in_model = 0;
                     }
                     if (in_model && (SYM || h != h0)) {
                         key = h;
                         if constexpr (VERIFY) key &= P.fp_mask;
                         key = key ? key : 1ull;
-                        if constexpr (DIST) {
-                            if constexpr (PRE) s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(key, d, pmx, hwn, B);
+                        if constexpr (REP) {  // a replicated level: only the owner probes
+                            if (owner_succ<S, K>(key, d, pmx, hwn, B, powner) != B.rank) key = 0;
+                        } else if constexpr (DIST) {
+                            if constexpr (PRE)
+                                s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(key, d, pmx, hwn, B, B.rank);
                             else  // no parent mixes: the successor's words 0 and 1 when it changes one
                                 s_own[b][threadIdx.x] = (uint8_t)(
                                     B.world == 1 ? 0u
@@ -893,11 +872,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     cur[b] = !key[b] ? 0ull
                            : remote ? (B.sent ? B.sent[(key[b] >> 8) & B.smask] : 0ull)
                                     : B.table[key[b] & B.tmask];
+                } else if constexpr (PIPE != 0) {
+                    cur[b] = cur_p[PIPE ? b : 0];
                 } else {
-                    // UPROBE: every lane loads (a lane without a key reads slot 0, a
-                    // valid address), so the loads need no exec-mask branches
-                    if constexpr (PIPE != 0) cur[b] = cur_p[PIPE ? b : 0];
-                    else cur[b] = (UPROBE || key[b]) ? B.table[key[b] & B.tmask] : 0ull;
+                    cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
                 }
             }
 #pragma unroll
@@ -907,17 +885,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             u32 hitbits = 0;  // verification: probes that found their key (slot parked in s_key)
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
-                if constexpr (UPROBE && !VERIFY && !SENTC) {  // one branch per probe: around its CAS
-                    const bool live = key[b] != 0;
-                    slowbits |= (u32)(live && cur[b] != 0 && cur[b] != key[b]) << b;
-                    if (live && cur[b] == 0) {
-                        const u64 prev = atomicCAS((unsigned long long*)&B.table[key[b] & B.tmask], 0ull,
-                                                   (unsigned long long)key[b]);
-                        newbits |= (u32)(prev == 0) << b;
-                        slowbits |= (u32)(prev != 0 && prev != key[b]) << b;
-                    }
-                    continue;
-                }
                 if (!key[b]) continue;
                 if (cur[b] == key[b]) {
                     if constexpr (VERIFY) {
@@ -998,8 +965,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 if (bal) {
                     if (is_new) {
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
-                        l_rel[pos] = (SORT && FSORT) ? (u32)rel | ((u32)(cp >> (8 * b)) << 24)
-                                   : MARK ? (u32)rel | ((u32)s_own[DIST ? b : 0][threadIdx.x] << 24) : (u32)rel;
+                        l_rel[pos] = (MARK && !REP) ? (u32)rel | ((u32)s_own[LISTOWN ? b : 0][threadIdx.x] << 24)
+                                                    : (u32)rel;
                         l_lane[pos] = (uint8_t)(SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b);
                         if constexpr (SENTC) {
                             l_dest[pos] = s_own[b][threadIdx.x];
@@ -1008,23 +975,26 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     }
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
-                        if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+                        if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
+                        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
                         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
-                        else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
                     }
                 }
             }
         }
-        if (live && g == 0) atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)(lo + rel));
+        if (live && mine && g == 0) {  // deadlock: the state's index on its own rank
+            const u64 ix = REP ? (((u64)rec[RR::REF] | ((u64)rec[RR::REF + 1] << 32)) & ((1ull << 48) - 1)) : lo + rel;
+            atomicMin((unsigned long long*)&B.ctr->deadlock, (unsigned long long)ix);
+        }
         gen += g;
     }
     }
     if (n) {
-        if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+        if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
+        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
-        else if constexpr (SORT && FSORT) flush_new_sorted<S, K>(P, B, lo, l_rel, l_lane, s_bins[wv], n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
     // wave reductions of the generated and probe counts, one atomic each per wave
@@ -1065,49 +1035,47 @@ __global__ __launch_bounds__(256) void k_capacity_check(const Params P, const De
     if (bad) atomicOr(&B.ctr->overflow, bad << 8);
 }
 
+// Every lane of every state (shapes with more than 64 lanes; verification).
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false>
 __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     expand_body<S, K, SYM, BATCH, DIST, VERIFY, PRE>(P, PT, B, lo, hi);
 }
 
-// Precomputed parent mixes + the lane-superset walk (needs <= 64 lanes), with
-// class-sorted flushes (FS) and/or class-sorted windows (WS).  WPE: waves/SIMD cap (0 = none).
-template <int S, int K, int BATCH, int WPE, bool WS = false, bool FS = true, bool EARLY = false, int WT = 8,
-          bool UP = false, bool WF = true, int PI = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1))) void k_expand_sort(
+// The single-GPU expansion kernel: the lane-superset walk over class-sorted
+// windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
+// loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
+template <int S, int K, int BATCH, int PI, bool PS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, false, true, WS, FS, true, EARLY, false, WT, UP, WF, PI>(
-            P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, true, true, false, 16, PI, false, PS>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
 // permutation that sorts the servers by signature, all S! only on ties
-// (deferred to k_ties).  INC: keys from the parent's frame (canon_delta_inc);
-// otherwise every lane hashes its whole permuted successor (canon_delta).
-// WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
-template <int S, int K, int BATCH, bool INC, int WPE = 5, bool WS = false, int WT = 8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? WPE : 1))) void k_expand_sym(
-    const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
+// (deferred to k_ties).  WS: the lane-superset walk over class-sorted windows
+// of 16 tiles, 4 waves/SIMD (72.1-72.7 vs 75.0-75.3 ms for 8 tiles on the
+// MCraftBench bounds); otherwise (more than 64 lanes) every lane, 5 waves/SIMD.
+template <int S, int K, int BATCH, bool WS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
+k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, true, BATCH, false, false, false, INC, true, true, false, false, false, false, WT>(P, PT, B, lo,
-                                                                                                          hi);
+        expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16>(P, PT, B, lo, hi);
     else
-        expand_body<S, K, true, BATCH, false, false, false, INC>(P, PT, B, lo, hi);
+        expand_body<S, K, true, BATCH, false, false, false>(P, PT, B, lo, hi);
 }
 
-// The sharded expansion (owner routing, sent-cache, per-wave key lists).
-// WS: the lane-superset walk over class-sorted windows (as k_expand_sort).
-// 4 waves/SIMD like k_expand_sort (uncapped it takes 131 VGPRs: 3 waves).
-template <int S, int K, int BATCH, bool WS, int WPE = 4, bool DIA = true, bool EARLY = true, bool MARK = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WS ? WPE : 1))) void k_expand_dist(
+// The sharded expansion: send markers in the local set, diamond skipping and
+// the lane-superset walk over class-sorted windows of 8 tiles (4 waves/SIMD;
+// uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
+// REP: a replicated level (the whole level's records in B.rep).
+template <int S, int K, int BATCH, bool REP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, true, false, true, false, true, true, false, DIA, DIA && EARLY, MARK>(P, PT, B,
-                                                                                                          lo, hi);
-    else  // more than 64 lanes: every lane of every state
-        expand_body<S, K, false, BATCH, true, false, false, false, false, false, true, false, false, MARK>(P, PT, B, lo,
-                                                                                                       hi);
+    if constexpr (Lanes<S, K>::N <= 64)
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
+    else if constexpr (!REP)
+        expand_body<S, K, false, BATCH, true, false, false, false, false, true>(P, PT, B, lo, hi);
 }
 
 #ifndef RMC_SHAPE_S  // non-template kernels: in the common object only
@@ -1145,11 +1113,65 @@ __global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64
     if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
 }
 
+// Presorted windows (k_expand_sort<PS>): the frontier [lo, lo + nf) cut into
+// the windows the expansion kernel will take (256 * wt states, wt from the
+// launch size and the expansion grid exactly as the kernel computes it), each
+// counting-sorted by the states' 1-byte classes: word[win + i] = the i-th
+// position of window win in class order.
+__global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo, u64 nf, u64 wt, uint16_t* word) {
+    __shared__ u32 bins[256];
+    __shared__ uint8_t cs[256 * 16];
+    const u32 tid = threadIdx.x;
+    for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {
+        const u32 wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
+        __syncthreads();
+        bins[tid] = 0;
+        __syncthreads();
+        for (u32 p = tid; p < wn; p += 256) {
+            const u32 c = cls[lo + win + p];
+            cs[p] = (uint8_t)c;
+            atomicAdd(&bins[c], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {  // exclusive scan of the 256 counters: 4 per lane, then across the wave
+            u32 v[4], tot = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[q] = bins[tid * 4 + q]; tot += v[q]; }
+            u32 incl = tot;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const u32 t = (u32)__shfl_up((int)incl, off);
+                if ((int)tid >= off) incl += t;
+            }
+            u32 ex = incl - tot;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { bins[tid * 4 + q] = ex; ex += v[q]; }
+        }
+        __syncthreads();
+        for (u32 p = tid; p < wn; p += 256) word[win + atomicAdd(&bins[cs[p]], 1u)] = (uint16_t)p;
+    }
+}
+
+hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st) {
+    const u64 nf = hi - lo;
+    if (nf == 0) return hipSuccess;
+    if (wt_max > 16) return hipErrorInvalidValue;
+    // the expansion kernel's window size for this launch (expand_body: per_block)
+    const u64 per_block = (nf + grid * 256ull - 1) / (grid * 256ull);
+    const u64 wt = per_block < wt_max ? (per_block ? per_block : 1ull) : wt_max;
+    const u64 nwin = (nf + 256ull * wt - 1) / (256ull * wt);
+    hipLaunchKernelGGL(k_window_order, dim3((unsigned)(nwin < grid ? nwin : grid)), dim3(256), 0, st, B.cls, lo, nf,
+                       wt, B.word);
+    return hipGetLastError();
+}
+
 // Sharded mode: the count row of one exchange round (launch_pack_counts).
 __global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64* out) {
     const u32 p = threadIdx.x;
     const u64 novf = B.ctr->novf;
-    const u64 flags = host_more | (novf > ovf_done ? 1ull : 0ull);
+    // bit 0: more to send this level; bit 1: the parking buffer overflowed (every
+    // rank reads every row and fails alike)
+    const u64 flags = host_more | (novf > ovf_done ? 1ull : 0ull) | (novf > B.ovf_cap ? 2ull : 0ull);
     if (p < B.world) {
         const u64 c = B.ocount[p];
         out[2 * p] = p == B.rank ? 0ull : (c < B.kcap ? c : B.kcap);
@@ -1249,13 +1271,9 @@ __global__ __launch_bounds__(256) void k_store_remote(const Params P, const DevB
         u64 w[S];
         u32 m[K];
         load_state<S, K>(r, w, m);
-        store_state<S, K>(B.store + ni * (u64)NW, w, m);
         const u64 ref = (u64)r[NW] | ((u64)r[NW + 1] << 32);
-        B.parent[ni] = ref & ~((0xFFull << 40) | REF_SEEN);
-        B.act[ni] = (uint8_t)(ref >> 40);
-        B.foot[ni] = (u64)r[NW + 2] | ((u64)r[NW + 3] << 32);
-        const int v = check_invariants<S, K>(w, m, P);
-        if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
+        store_new<S, K>(P, B, ni, w, m, ref & ~((0xFFull << 40) | REF_SEEN), (int)((ref >> 40) & 0xFFu),
+                        (u64)r[NW + 2] | ((u64)r[NW + 3] << 32));
     }
 }
 
@@ -1434,6 +1452,30 @@ __global__ __launch_bounds__(256) void k_rehash(const Params P, const PermTable 
     }
 }
 
+// Replicated level (sharded mode): this rank's frontier states [lo, hi) as
+// records for the level's all-gather (RepRec: state, global ref, footprint,
+// lane | class << 8).
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_pack_rep(const DevBufs B, u64 lo, u64 hi, u32* out) {
+    constexpr int NW = 2 * S + K;
+    typedef RepRec<S, K> RR;
+    for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
+        u32* r = out + (i - lo) * (u64)RR::RR;
+        const uint2* src = reinterpret_cast<const uint2*>(B.store + i * (u64)NW);
+        uint2* dst = reinterpret_cast<uint2*>(r);
+#pragma unroll
+        for (int q = 0; q < NW / 2; ++q) dst[q] = src[q];
+        const u64 ref = B.ref_tag | i;
+        const u64 f = Lanes<S, K>::N <= 64 ? B.foot[i] : 0ull;
+        r[RR::REF] = (u32)ref;
+        r[RR::REF + 1] = (u32)(ref >> 32);
+        r[RR::FOOT] = (u32)f;
+        r[RR::FOOT + 1] = (u32)(f >> 32);
+        r[RR::ACT] = (u32)B.act[i] | ((u32)B.cls[i] << 8);
+        r[RR::ACT + 1] = 0;
+    }
+}
+
 // Every enabled lane of n given states, written out without dedup.
 template <int S, int K, bool SYM>
 __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT, const u32* in, u64 n, u32* out,
@@ -1599,25 +1641,14 @@ static u64 resident_grid(const void* k) {
     return v;
 }
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, for same-box A/B runs;
-// profiles/r02/ab/, profiles/r03/ab/): 6 (default) = commuting-diamond
-// skipping (7.18 G instead of 10.41 G probes per MCraftBench BFS: 315 vs
-// 337-340 ms) on the lane-superset walk over class-sorted windows of 16 tiles
-// (308.2-309.3 vs 310.9-312.4 ms for 8 tiles, variant 8, same box), classes by
-// roles x message count (270.8-279.6 vs 279.4-286.0 ms by roles only, variant
-// 10; profiles/r03/ab/window_classes_r03ab2.jsonl);
-// 7 = 6 with the stutter, CONSTRAINT and commuting-diamond decisions taken
-// before the lane hashes (317-322 ms: the split costs more than the hashes
-// it saves); without the diamond, 6 is the round-2 kernel: the lane-superset walk over class-sorted
-// windows of up to 2048 states (k_expand_sort, 4 waves/SIMD; 317 vs 343 ms per
-// MCraftBench BFS against 1; shapes with > 64 lanes run 1), 1 = every lane of
-// every state, the parent's per-component mixes precomputed (k_expand, 95
-// VGPRs, 5 waves/SIMD), 4 = the lane-superset walk with class-sorted flushes
-// instead of windows (322 ms).  Measured and removed: mixes recomputed per lane
-// (−2.5 %), 6 waves/SIMD, the delta loop rolled, 5-wave caps of 4 and 6 (spills),
-// flushes and windows both sorted.
-// Round 3, last: 6 issues each probe's load as soon as its key is known (PIPE);
-// 14 is the same kernel issuing the batch's 8 loads after its lane code.
+// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 6 (default) =
+// k_expand_sort (the lane-superset walk over class-sorted windows of 16
+// tiles, commuting-diamond skipping, probe loads issued during the lane code;
+// profiles/r03/ab/), 1 = every lane of every state (k_expand with the
+// parent's mixes precomputed; also what shapes with more than 64 lanes run).
+// The variants measured and rejected in rounds 2-3 (EARLY, UPROBE, class-sorted
+// flushes, 8-tile windows, role-only classes, probes after the lane code) are
+// in git history, not in the build.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
@@ -1626,48 +1657,13 @@ static int expand_variant() {
     return v;
 }
 
-// SYMMETRY expansion variant (RMC_SYM_VARIANT, same-box A/B): 4 (default) =
-// whole permuted successor keys, the lane-superset walk over class-sorted
-// windows, 4 waves/SIMD (86 vs 93.5 ms on the MCraftBench bounds against 0);
-// 0 = whole permuted successor keys, every lane (5 waves/SIMD); 1 = incremental
-// keys from the parent's frame (canon_delta_inc; 97 ms: its registers cost more
-// than the mixes it saves).
-static int sym_variant() {
-    static int v = [] {
-        const char* e = getenv("RMC_SYM_VARIANT");
-        return e ? atoi(e) : 4;
-    }();
-    return v;
-}
-
-// Sharded expansion variant (RMC_DIST_VARIANT; same-box A/B at one rank on
-// RCCL, profiles/r03/ab/dist_* and final_lane_code_r03u.jsonl): 6 (default) =
-// send markers in the local set (a lossless sent-cache; the probe loop is the
-// single-GPU loop) with diamond skipping: 322.7-323.9 ms per MCraftBench BFS
-// against 290.9-294.0 unsharded, once the per-lane descriptors freed the
-// registers (before them: 341 ms, and 7 was best); 7 = markers without
-// diamonds (357.7-360.3 ms now, 329-333 before the descriptors); 4 = the
-// lossy sent-cache, no diamonds (bench shape); 1 = the sent-cache with
-// diamonds decided before hashing (round-3 start, 366 ms); 0 = every lane.
-// Measured and removed: 3 waves/SIMD, 6 probes in flight, the owner decided
-// in the flush (390 ms: a reservation atomic per 64 entries).
-// Measured and removed: 6 with the probe loads issued during the lane code
-// (PIPE; 308.7-309.7 vs 307.4-308.7 ms at one rank, no gain).
-static int dist_variant() {
-    static int v = [] {
-        const char* e = getenv("RMC_DIST_VARIANT");
-        return e ? atoi(e) : 6;
-    }();
-    return v;
-}
-
-// Probes in flight per thread: 8 (measured best of 4/8 on MI355X).
+// Probes in flight per thread: 8 (measured best of 4/8/16 on MI355X).
 constexpr int kBatch = 8;
 
 template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, bool verify, const Params& P, const PermTable& PT, const DevBufs& B, u64 a,
                            u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
-    const u64 n = (which == 0 || which == 3 || which == 5 || which == 7) ? (b - a)
+    const u64 n = (which == 0 || which == 3 || which == 5 || which == 7 || which == 12 || which == 13) ? (b - a)
                 : which == 8 ? a * (u64)B.world : which == 10 ? 1 : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
@@ -1682,99 +1678,41 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(k);
         return (unsigned)(blocks < want ? blocks : want);
     };
+#define RMC_EXPAND_LAUNCH(KERNEL)                                                                              \
+    hipLaunchKernelGGL(KERNEL, dim3(eg(reinterpret_cast<const void*>(&(KERNEL)))), dim3(256), 0, st, P, PT, B, a, b)
+    constexpr bool SORTED = Lanes<S, K>::N <= 64;  // the lane-superset walk needs a 64-bit lane mask
     if (which == 0) {
         if constexpr (SYM) {
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else if (sym_variant() == 1)
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, true>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
-                                   a, b);
-            else if (sym_variant() == 4)  // default: windows of 16 tiles (72.1-72.7 vs 75.0-75.3 ms for 8)
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true, 16>), dim3((unsigned)g), dim3(256), 0, st,
-                                   P, PT, B, a, b);
-            else if (sym_variant() == 5)  // windows of 8 tiles
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false, 4, true>), dim3((unsigned)g), dim3(256), 0, st, P,
-                                   PT, B, a, b);
             else
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, false>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
         } else if (verify) {
-            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, false, kBatch, false, true>)))), dim3(256), 0, st, P, PT,
-                               B, a, b);
-        } else if (expand_variant() == 4 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 0>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 0>)))), dim3(256), 0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 7 && Lanes<S, K>::N <= 64) {
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, true>)))), dim3(256), 0, st, P,
-                               PT, B, a, b);
-        } else if (S == 3 && K == 4 && expand_variant() == 10) {  // A/B (bench shape): window classes by roles only
-            if constexpr (S == 3 && K == 4)
-                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, false>),
-                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false,
-                                                                                         false, 16, false, false>)))),
-                                   dim3(256), 0, st, P, PT, B, a, b);
-        } else if (S == 3 && K == 4 && expand_variant() == 9) {  // A/B (bench shape): unconditional probe loads
-            if constexpr (S == 3 && K == 4)
-                hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, true>),
-                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false,
-                                                                                         false, 16, true>)))),
-                                   dim3(256), 0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 8 && Lanes<S, K>::N <= 64) {  // windows of 8 tiles (round-2 size)
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false>)))), dim3(256), 0, st, P, PT,
-                               B, a, b);
-        } else if (expand_variant() == 6 && Lanes<S, K>::N <= 64) {
-            // default: windows of 16 tiles (4096 states), probe loads issued during the
-            // lane code where the registers allow it (K = 8 shapes would spill 10-13 VGPRs)
-            constexpr int PI = K <= 4 ? 1 : 0;
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, true, PI>),
-                               dim3(eg(reinterpret_cast<const void*>(
-                                   &(k_expand_sort<S, K, kBatch, 4, true, false, false, 16, false, true, PI>)))),
-                               dim3(256), 0, st, P, PT, B, a, b);
-        } else if (expand_variant() == 14 && Lanes<S, K>::N <= 64) {  // A/B: 6 with the probes issued after the batch
-            hipLaunchKernelGGL((k_expand_sort<S, K, kBatch, 4, true, false, false, 16>), dim3(eg(reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, 4, true, false, false, 16>)))), dim3(256), 0,
-                               st, P, PT, B, a, b);
+            RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
+        } else if (expand_variant() == 6 && SORTED) {
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
+        } else if (expand_variant() == 7 && SORTED && B.word) {  // windows presorted by k_window_order
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true>));
         } else {  // 1, and shapes with more than 64 lanes
-            hipLaunchKernelGGL((k_expand<S, K, false, kBatch, false, false, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, false, kBatch, false, false, true>)))), dim3(256), 0, st,
-                               P, PT, B, a, b);
+            RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
         }
     } else if (which == 3 && verify) {  // sharded full-state verification: every lane, hits compared
-        hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, SYM, kBatch, true, true>)))), dim3(256), 0, st, P, PT, B, a,
-                           b);
+        RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
+    } else if (which == 3) {
+        if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
+        else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
+    } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
+        if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
+        else return hipErrorInvalidValue;
+    } else if (which == 13) {
+        hipLaunchKernelGGL((k_pack_rep<S, K>), dim3((unsigned)g), dim3(256), 0, st, B, a, b, out);
     } else if (which == 11) {
         hipLaunchKernelGGL((k_compare_remote<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a);
-    } else if (which == 3) {
-        if constexpr (SYM)
-            hipLaunchKernelGGL((k_expand<S, K, SYM, kBatch, true>), dim3(eg(reinterpret_cast<const void*>(&(k_expand<S, K, SYM, kBatch, true>)))), dim3(256), 0, st, P, PT, B, a, b);
-        else if (dist_variant() == 6) {  // default: send markers with diamond skipping
-            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, true, false, true>),
-                               dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, true, false, true>)))),
-                               dim3(256), 0, st, P, PT, B, a, b);
-        } else if (dist_variant() == 7) {  // send markers, no diamond skipping
-            hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false, false, true>),
-                               dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false, false, true>)))),
-                               dim3(256), 0, st, P, PT, B, a, b);
-        } else {
-            bool ab = false;
-            if constexpr (S == 3 && K == 4) {  // A/B variant, bench shape only: 4 = sent-cache, no diamonds
-                ab = true;
-                if (dist_variant() == 4)
-                    hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true, 4, false>),
-                                       dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true, 4, false>)))),
-                                       dim3(256), 0, st, P, PT, B, a, b);
-                else
-                    ab = false;
-            }
-            if (ab) {
-            } else if (dist_variant() == 1) {  // sent-cache, diamond skipping decided before hashing
-                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, true>),
-                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, true>)))), dim3(256), 0,
-                                   st, P, PT, B, a, b);
-            } else {  // 0: sent-cache, every lane
-                hipLaunchKernelGGL((k_expand_dist<S, K, kBatch, false>),
-                                   dim3(eg(reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, false>)))), dim3(256), 0,
-                                   st, P, PT, B, a, b);
-            }
-        }
     } else if (which == 8) {  // a = keys per destination block (max); out = replies
         hipLaunchKernelGGL((k_materialize_remote<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B,
                            reinterpret_cast<const uint8_t*>(in), a, b);
@@ -1794,6 +1732,7 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         hipLaunchKernelGGL((k_list<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, in, a, out, cap,
                            count);
     }
+#undef RMC_EXPAND_LAUNCH
     if ((which == 0 || which == 3) && P.unbounded)  // depth-bounded unconstrained model: the capacity pass
         hipLaunchKernelGGL((k_capacity_check<S, K>), dim3((unsigned)g), dim3(256), 0, st, P, B, a, b);
     return hipGetLastError();
@@ -1844,10 +1783,7 @@ RMC_SHAPES(RMC_SHAPE_DECLS)
 #define RMC_DEFINE_SHAPE_(SS, KK) RMC_DEFINE_SHAPE(SS, KK)
 RMC_DEFINE_SHAPE_(RMC_SHAPE_S, RMC_SHAPE_K)
 #else
-bool dist_uses_sent_cache() {
-    const int v = dist_variant();
-    return !(v == 6 || v == 7);  // markers live in the fingerprint set
-}
+
 
 hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st) {
     const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;

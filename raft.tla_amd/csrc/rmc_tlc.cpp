@@ -187,6 +187,10 @@ int run_simulation(const std::string& cfg, const std::string& tla, const std::st
     if (depth > 0) sc.depth = depth;
     if (num > 0) sc.behaviours = num;
     sc.seed = seed;
+    // a model that bounds no field (Smokeraft.cfg) walks on the wide layout with
+    // TLC's draw (an action, then a successor); a bounded one within its bounds
+    const bool wide = rmc_state_bytes(&c) > 64 * 4;
+    if (wide) sc.mode = RMC_SIM_TLC;
     printf("Running Random Simulation with seed %llu: %llu behaviours of up to %d states, %s.\n",
            (unsigned long long)seed, (unsigned long long)sc.behaviours, sc.depth,
            sc.smoke_k ? "initial states from SmokeInit" : "initial state from Init");
@@ -213,10 +217,10 @@ int run_simulation(const std::string& cfg, const std::string& tla, const std::st
     } else {
         printf("No error has been found in %llu behaviours.\n", (unsigned long long)r.behaviours);
     }
-    printf("%llu states generated (%llu steps), %llu behaviours truncated at the packed capacity, "
+    printf("%llu states generated (%llu steps), %llu behaviours truncated at the %s layout's capacity, "
            "%llu deadlocked (no successor within the capacity).\n",
            (unsigned long long)(r.steps + r.behaviours), (unsigned long long)r.steps,
-           (unsigned long long)r.truncated, (unsigned long long)r.deadlocked);
+           (unsigned long long)r.truncated, wide ? "wide" : "packed", (unsigned long long)r.deadlocked);
     printf("Finished in %.0fms (%.3g behaviours/s, %.3g steps/s on the device)\n", r.seconds * 1e3,
            r.behaviours / (r.kernel_seconds > 0 ? r.kernel_seconds : 1), r.steps / (r.kernel_seconds > 0 ? r.kernel_seconds : 1));
     rmc_destroy(ctx);

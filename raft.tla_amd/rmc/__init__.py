@@ -16,7 +16,10 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
 
-MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8
+MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8  # the packed layout's capacity
+WIDE_MAX_TERM, WIDE_MAX_LOG, WIDE_MAX_MSGS, WIDE_MAX_DUP = 255, 8, 16, 255  # the wide layout's
+VIEW_LOG, VIEW_MSGS = 8, 16  # rmc_state_view sizes (RMC_VIEW_LOG, RMC_VIEW_MSGS)
+SIM_WITHIN_CAPACITY, SIM_TRUNCATE, SIM_TLC = 0, 1, 2
 FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES, FLAG_SPILL = 1, 2, 4, 8, 16
 INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING, INV_MESSAGES = 1, 2, 4, 8
 INV_LEADER_VOTES, INV_CAND_TERM = 16, 32
@@ -68,7 +71,7 @@ class Entry(C.Structure):
 class MsgView(C.Structure):
     _fields_ = [("mtype", C.c_int32), ("mterm", C.c_int32), ("msource", C.c_int32),
                 ("mdest", C.c_int32), ("mlastLogTerm", C.c_int32), ("mlastLogIndex", C.c_int32),
-                ("mvoteGranted", C.c_int32), ("mlog_len", C.c_int32), ("mlog", Entry * MAX_LOG),
+                ("mvoteGranted", C.c_int32), ("mlog_len", C.c_int32), ("mlog", Entry * VIEW_LOG),
                 ("mprevLogIndex", C.c_int32), ("mprevLogTerm", C.c_int32),
                 ("mentries_len", C.c_int32), ("mentries", Entry * 1), ("mcommitIndex", C.c_int32),
                 ("msuccess", C.c_int32), ("mmatchIndex", C.c_int32), ("count", C.c_int32)]
@@ -79,12 +82,12 @@ class StateView(C.Structure):
                 ("currentTerm", C.c_int32 * MAX_SERVERS), ("state", C.c_int32 * MAX_SERVERS),
                 ("votedFor", C.c_int32 * MAX_SERVERS), ("commitIndex", C.c_int32 * MAX_SERVERS),
                 ("log_len", C.c_int32 * MAX_SERVERS),
-                ("log", (Entry * MAX_LOG) * MAX_SERVERS),
+                ("log", (Entry * VIEW_LOG) * MAX_SERVERS),
                 ("votesResponded", C.c_uint32 * MAX_SERVERS),
                 ("votesGranted", C.c_uint32 * MAX_SERVERS),
                 ("nextIndex", (C.c_int32 * MAX_SERVERS) * MAX_SERVERS),
                 ("matchIndex", (C.c_int32 * MAX_SERVERS) * MAX_SERVERS),
-                ("msgs", MsgView * MAX_MSGS)]
+                ("msgs", MsgView * VIEW_MSGS)]
 
 
 class SuccView(C.Structure):
@@ -326,7 +329,8 @@ class Checker:
 
     def simulate(self, behaviours=1 << 20, depth=100, smoke_k=2, smoke_nat=2, seed=0, mode=0) -> SimResult:
         """TLC -simulate over Smokeraft-style initial states (rmc_simulate);
-        mode 0 = RMC_SIM_WITHIN_CAPACITY, 1 = RMC_SIM_TRUNCATE."""
+        mode 0 = RMC_SIM_WITHIN_CAPACITY, 1 = RMC_SIM_TRUNCATE, 2 = RMC_SIM_TLC (TLC's
+        draw: an action, then a successor; the wide layout only)."""
         sc = SimConfig(behaviours, depth, smoke_k, smoke_nat, mode, seed)
         out = SimResult()
         self._check(self.lib.rmc_simulate(self.ctx, C.byref(sc), C.byref(out)))
@@ -383,7 +387,7 @@ class Checker:
 
     def expand(self, views):
         arr = (StateView * len(views))(*views)
-        lanes_max = 5 + 5 + 25 + 5 + 10 + 5 + 25 + 3 * 8
+        lanes_max = 5 + 5 + 25 + 5 + 10 + 5 + 25 + 3 * VIEW_MSGS
         cap = max(1, len(views) * lanes_max)
         out = (SuccView * cap)()
         n = C.c_size_t()

@@ -14,7 +14,9 @@ Replaces TLC's distributed mode (partitioned FPSet).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -22,14 +24,30 @@ import torch.distributed as dist
 from . import ALLGATHER_FN, ALLTOALLV_FN, Checker, Transport
 
 
+def dist_timeout_s() -> float:
+    """The sharded search's deadline for one collective (RMC_DIST_TIMEOUT_S,
+    the same variable librmc reads for its RCCL waits; default 300 s)."""
+    try:
+        return max(0.1, float(os.environ.get("RMC_DIST_TIMEOUT_S", "300")))
+    except ValueError:
+        return 300.0
+
+
 class GlooTransport:
     """rmc_transport over torch.distributed (a backend that moves CPU tensors:
-    gloo).  Keep the object alive while the ctx uses it."""
+    gloo).  Keep the object alive while the ctx uses it.  Every collective
+    waits at most dist_timeout_s(); past it the callback fails, librmc reports
+    where (level, round, phase) and the run stops instead of hanging."""
 
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.errors = []
+        self.timeout = timedelta(seconds=dist_timeout_s())
+
+        def finish(work):
+            if not work.wait(self.timeout):
+                raise TimeoutError(f"collective not complete within {self.timeout.total_seconds()} s")
 
         def alltoallv(_user, send, send_bytes, recv, recv_bytes):
             try:
@@ -39,7 +57,8 @@ class GlooTransport:
                 if sum(sb):
                     C.memmove(src.data_ptr(), send, sum(sb))
                 out = torch.empty(sum(rb), dtype=torch.uint8)
-                dist.all_to_all_single(out, src, output_split_sizes=rb, input_split_sizes=sb, group=self.group)
+                finish(dist.all_to_all_single(out, src, output_split_sizes=rb, input_split_sizes=sb,
+                                              group=self.group, async_op=True))
                 if sum(rb):
                     C.memmove(recv, out.data_ptr(), sum(rb))
                 return 0
@@ -53,7 +72,7 @@ class GlooTransport:
                 mine = torch.empty(n, dtype=torch.uint8)
                 C.memmove(mine.data_ptr(), send, n)
                 parts = [torch.empty(n, dtype=torch.uint8) for _ in range(self.world)]
-                dist.all_gather(parts, mine, group=self.group)
+                finish(dist.all_gather(parts, mine, group=self.group, async_op=True))
                 for r, p in enumerate(parts):
                     C.memmove(recv + r * n, p.data_ptr(), n)
                 return 0

@@ -104,4 +104,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # noqa: BLE001 — a failed rank exits at once: a collective
+        # still pending in the process group must not keep it alive
+        sys.stderr.write(f"dist_worker rank {os.environ.get('RANK')}: {type(e).__name__}: {e}\n")
+        sys.stderr.flush()
+        os._exit(1)

@@ -64,6 +64,10 @@ CONFIGS = {
     # (bit 29), which a sharded record once shared with its "seen" flag
     "tiny2_log3": (2, 2, 3, 3, 2, 1, 0, 1, 0, 0),
     "s3_log3_prefix14": (3, 2, 3, 3, 2, 1, 0, 1, 0, 14),
+    # the bench model (specs/MCraftBench.cfg) itself: its first 22 and 24 levels (31 M, 76 M
+    # states; the whole 1.23 G-state model exceeds the oracle's memory)
+    "bench_prefix22": (3, 2, 2, 1, 3, 1, 0, 1, 0, 22),
+    "bench_prefix24": (3, 2, 2, 1, 3, 1, 0, 1, 0, 24),
     # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
     "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }

@@ -2,7 +2,7 @@
 // the mask must contain every lane that lane_delta enables, on every state of
 // random walks from Init, for every shape the sorted kernels run (<= 64 lanes);
 // a missing lane would silently drop successors.  Also checks that
-// state_class / succ_class stay inside their bin ranges.
+// state_class / state_class_fine stay inside their bin ranges.
 // Build: g++ -O2 -std=c++17 -I raft.tla_amd/csrc lane_mask_check.cpp
 // Run:   ./a.out <walks> <depth> <seed>   (prints "ok ..." or the first failure)
 #include <cstdio>
@@ -32,6 +32,7 @@ static int run(u64 walks, int depth, u64 seed, int V, u64* checked, u64* lanes_o
         for (int dd = 0; dd < depth; ++dd) {
             const u64 mk = lane_superset<S, K>(w, m, V);
             if (state_class<S>(w) >= 64) { printf("state_class out of range\n"); return 1; }
+            if (state_class_fine<S, K>(w, m) > 255) { printf("state_class_fine out of range\n"); return 1; }
             int cand[64], nc = 0;
             for (int lane = 0; lane < nl; ++lane) {
                 Delta d;
@@ -44,7 +45,6 @@ static int run(u64 walks, int depth, u64 seed, int V, u64* checked, u64* lanes_o
                            (unsigned long long)wk, dd, lane, (unsigned long long)mk);
                     return 1;
                 }
-                if (succ_class<S, K>(w, m, d) > 255) { printf("succ_class out of range\n"); return 1; }
                 if (delta_in_model<S, K>(m, d, P)) cand[nc++] = lane;
             }
             if (!nc) break;

@@ -20,10 +20,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))
 
 
-def _torchrun(nproc, args, port, timeout=150):
+def _torchrun(nproc, args, port, timeout=150, rep="4096"):
+    """rep: RMC_DIST_REP, the largest level (states, all ranks) searched as a
+    replicated level.  The tests' default, 4096, mixes both kinds in one search:
+    the first levels replicated, the larger ones with the key/state exchange."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMC_DIST_REP=rep)
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
 
@@ -64,24 +67,28 @@ def test_host_transport_gloo(nproc, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,nproc,backend", [("tiny2_v2", 2, "gloo"), ("small", 2, "gloo"),
-                                                ("small", 4, "gloo"), ("s5_prefix9", 2, "gloo"),
-                                                ("small_sym", 2, "gloo"), ("bounded_sym_prefix16", 3, "gloo"),
-                                                ("msgs5_dup2_prefix9", 2, "gloo"), ("s4_prefix10", 3, "gloo"),
-                                                ("tiny2_log3", 2, "gloo"), ("s3_log3_prefix14", 2, "gloo"),
-                                                ("small", 1, "nccl")])
-def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
+@pytest.mark.parametrize("case,nproc,backend,rep", [
+    ("tiny2_v2", 2, "gloo", "4096"), ("small", 2, "gloo", "4096"), ("small", 4, "gloo", "4096"),
+    ("small", 3, "gloo", "0"), ("small", 3, "gloo", "1048576"), ("s5_prefix9", 2, "gloo", "4096"),
+    ("small_sym", 2, "gloo", "4096"), ("bounded_sym_prefix16", 3, "gloo", "4096"),
+    ("msgs5_dup2_prefix9", 2, "gloo", "4096"), ("s4_prefix10", 3, "gloo", "4096"),
+    ("tiny2_log3", 2, "gloo", "4096"), ("s3_log3_prefix14", 2, "gloo", "4096"),
+    ("tiny2_log3", 3, "gloo", "1048576"), ("small", 1, "nccl", "4096"), ("small", 1, "nccl", "0")])
+def test_sharded_bfs_matches_oracle(case, nproc, backend, rep, tmp_path):
     """The sharded BFS inside librmc (rmc_shard + rmc_run_bfs), through the C
     ABI.  gloo: N ranks share the box's one GPU over the host transport.
     nccl: one rank on librmc's own RCCL communicator, the code path of the
     driver's multi-GPU bench.  SYMMETRY cases route by the canonical
     fingerprint; depth-bounded cases stop with the last level unexpanded, as
     the single-GPU search.  A small key outbox forces several chunks per
-    level and several phase-2 rounds."""
+    level and several phase-2 rounds.  rep (RMC_DIST_REP): "4096" mixes
+    replicated small levels with exchanged large ones in one search, "0"
+    exchanges every level, "1048576" replicates every level of these models
+    (no key leaves its rank; SYMMETRY never replicates)."""
     g = GOLDEN[case]
     out = tmp_path / "r.json"
     r = _torchrun(nproc, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out",
-                          str(out), "--device", "0", "--backend", backend], 29620 + nproc)
+                          str(out), "--device", "0", "--backend", backend], 29620 + nproc, rep=rep)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     res = json.load(open(out))
     assert res["distinct"] == g["distinct"]
@@ -90,8 +97,10 @@ def test_sharded_bfs_matches_oracle(case, nproc, backend, tmp_path):
     assert res["left_on_queue"] == g["left_on_queue"]
     assert res["levels"] == g["level_new"]
     assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]]
-    assert res["keys_sent"] > 0 or nproc == 1
-    assert res["states_sent"] > 0 or nproc == 1
+    all_rep = rep == "1048576" and not g["params"]["symmetry"]
+    if nproc > 1:
+        assert (res["keys_sent"] > 0) != all_rep
+        assert (res["states_sent"] > 0) != all_rep
     assert sum(p["stored"] for p in res["per_rank"]) == g["distinct"]
     assert all(p["summary"]["distinct"] == g["distinct"] for p in res["per_rank"])  # global on every rank
 
@@ -133,7 +142,7 @@ def test_sharded_full_bench_model_equals_single_gpu(tmp_path):
     r = _torchrun(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--cfg",
                       os.path.join(ROOT, "specs", "MCraftBench.cfg"), "--out", str(out), "--device", "0",
                       "--backend", "gloo", "--capacity", "800000000", "--keys-per-dest", str(1 << 24),
-                      "--rerun", "0", "--sent-cache", str(1 << 28)], 29660, timeout=220)
+                      "--rerun", "0", "--sent-cache", str(1 << 28)], 29660, timeout=220, rep="1048576")
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     res = json.load(open(out))
     assert (res["distinct"], res["generated"], res["depth"]) == (1_227_465_177, 21_130_972_267, 56)
@@ -152,7 +161,7 @@ def test_sharded_outbox_overflow_is_recovered(case, nproc, overlap, tmp_path):
     (RMC_DIST_OVERLAP=0): same counts."""
     g = GOLDEN[case]
     out = tmp_path / "r.json"
-    env_over = dict(os.environ, RMC_DIST_OVERLAP=overlap, RMC_DIST_FILL="3")
+    env_over = dict(os.environ, RMC_DIST_OVERLAP=overlap, RMC_DIST_FILL="3", RMC_DIST_REP="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(29680 + nproc),
            os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out", str(out), "--device", "0",
@@ -231,3 +240,79 @@ def test_sharded_checkpoint_and_recover(case, nproc, stop, tmp_path):
     res = json.load(open(out2))
     assert (res["distinct"], res["generated"], res["depth"]) == (g["distinct"], g["generated"], g["depth"])
     assert sum(p["stored"] for p in res["per_rank"]) == g["distinct"]
+
+
+def _launch_ranks(nproc, args, port, env_extra, timeout):
+    """Every rank as its own process (no torchrun: it would end the others at the
+    first failure, hiding how each rank ends).  Returns [(rc, stderr, seconds)]."""
+    import time
+    procs = []
+    t0 = time.time()
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="1", **env_extra)
+        procs.append(subprocess.Popen([sys.executable] + args, env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    out = []
+    for p in procs:
+        try:
+            _, err = p.communicate(timeout=max(1.0, timeout - (time.time() - t0)))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            _, err = p.communicate()
+            out.append((None, err, time.time() - t0))
+            continue
+        out.append((p.returncode, err, time.time() - t0))
+    return out
+
+
+@pytest.mark.gpu
+def test_stalled_rank_ends_every_rank_within_the_deadline(tmp_path):
+    """a rank that stops answering (RMC_DIST_STALL_RANK=1
+    sleeps at level 2) must not hang the others.  With RMC_DIST_TIMEOUT_S=5
+    every rank exits non-zero well before an outer limit, and the waiting rank
+    names the deadline, the level and the phase it was in."""
+    env = {"RMC_DIST_TIMEOUT_S": "5", "RMC_DIST_STALL_RANK": "1", "RMC_DIST_STALL_LEVEL": "2",
+           "RMC_DIST_STALL_S": "12"}
+    res = _launch_ranks(2, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", "small", "--out",
+                            str(tmp_path / "r.json"), "--device", "0", "--backend", "gloo"], 29790, env, 90)
+    for rc, err, secs in res:
+        assert rc is not None, "a rank hung past the test's limit:\n" + err[-2000:]
+        assert rc != 0, err[-2000:]
+        assert secs < 60, (secs, err[-2000:])
+    err0 = res[0][1]
+    assert "deadline (RMC_DIST_TIMEOUT_S)" in err0 and "level 2" in err0 and "phase" in err0, err0[-2000:]
+    assert "RMC_DIST_STALL_RANK" in res[1][1], res[1][1][-2000:]
+    assert not (tmp_path / "r.json").exists()
+
+
+RCCL_INIT_ALONE = r"""
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], 'raft.tla_amd'))
+import rmc
+cfg = rmc.make_config(n_servers=2, n_values=1, max_term=2, max_log_len=1, max_msgs=2, max_dup=1,
+                      device=0, state_capacity=1 << 16)
+with rmc.Checker(cfg) as ck:
+    try:
+        ck.shard(0, 2, rccl_id=rmc.rccl_unique_id())  # rank 1 never comes
+    except rmc.RmcError as e:
+        print("REFUSED", e, flush=True)
+        os._exit(0)
+print("JOINED", flush=True)
+os._exit(1)
+"""
+
+
+@pytest.mark.gpu
+def test_rccl_communicator_init_has_a_deadline(tmp_path):
+    """The RCCL path itself (one GPU on the box): a world-2 communicator whose
+    second rank never arrives.  The non-blocking init is polled under
+    RMC_DIST_TIMEOUT_S and aborted; rmc_shard fails naming the deadline
+    instead of blocking forever."""
+    script = tmp_path / "alone.py"
+    script.write_text(RCCL_INIT_ALONE)
+    env = dict(os.environ, RMC_DIST_TIMEOUT_S="4")
+    r = subprocess.run([sys.executable, str(script), ROOT], capture_output=True, text=True, timeout=100, env=env,
+                       cwd=ROOT)
+    assert "REFUSED" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "deadline" in r.stdout and "communicator init" in r.stdout, r.stdout

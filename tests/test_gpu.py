@@ -67,6 +67,30 @@ def test_bfs_matches_oracle(name):
     assert res.violated_inv == 0 and res.deadlock == 0
 
 
+@pytest.mark.parametrize("prefix", ["bench_prefix22", "bench_prefix24"])
+def test_bench_model_prefix_equals_oracle(prefix):
+    """The bench workload itself (specs/MCraftBench.cfg through the front-end,
+    as bench.py loads it), searched to its fixpoint: its first levels equal the
+    C oracle's level by level (new states per level, and the distinct and
+    generated counts once those levels exist), and the whole search ends with
+    the bench line's counts (1.23 G states: beyond the oracle's memory)."""
+    g = GOLDEN[prefix]
+    cfg = rmc.config_from_files(os.path.join(ROOT, "specs", "MCraftBench.cfg"), builtin_raft=True)
+    p = g["params"]
+    assert (cfg.n_servers, cfg.n_values, cfg.max_term, cfg.max_log_len, cfg.max_msgs, cfg.max_dup) == \
+        (p["n_servers"], p["n_values"], p["max_term"], p["max_log_len"], p["max_msgs"], p["max_dup"])
+    cfg.state_capacity = 1_300_000_000
+    with rmc.Checker(cfg) as ck:
+        res = ck.run()
+        lv = list(ck.levels)
+    levels = [1] + [x[3] for x in lv if x[3]]
+    d = len(g["level_new"])
+    assert levels[:d] == g["level_new"]
+    at = [x for x in lv if x[2] == g["distinct"]]  # the callback of the level that completed level d
+    assert at and at[0][1] == g["generated"]
+    assert (res.distinct, res.generated, res.depth) == (1_227_465_177, 21_130_972_267, 56)
+
+
 def test_fingerprint_salt_does_not_change_counts():
     """Another member of the fingerprint family (rmc_config.seed) must give the
     same exact counts: evidence against fingerprint collisions at full size."""
@@ -510,9 +534,10 @@ def test_unconstrained_model_under_a_depth_bound():
     """MCraft.cfg as shipped has no CONSTRAINT; under -depth
     it runs level by level.  Fixture in its layout:
     depth 3 gives the survey's KAT (1 + 3 + 18 = 22 distinct, 1 + 6 + 27 = 34
-    generated); depths 4-5 equal the C oracle with every bound at the packed
-    capacity; depth 6 needs a 4th copy of a message (Duplicate), beyond the
-    capacity: RMC_E_CAPACITY naming messages[m], not a silent filter.  The CLI
+    generated); depths 4-5 equal the C oracle.  Its unbounded fields run on the
+    wide layout (depth 6 needed a 4th copy of a message, beyond the packed
+    layout: tests/test_wide.py takes it to depth 8); a field that outgrows the
+    wide layout is RMC_E_CAPACITY naming it, never a silent filter.  The CLI
     prints TLC's lines for the depth-3 run."""
     import subprocess
     from tests import oracle_c
@@ -528,13 +553,6 @@ def test_unconstrained_model_under_a_depth_bound():
         assert (r.distinct, r.generated, r.depth) == (ref.distinct, ref.generated, ref.depth), depth
         if depth == 3:
             assert (r.distinct, r.generated, r.left_on_queue) == (22, 34, 18)
-    c = rmc.Config.from_buffer_copy(base)
-    c.max_depth = 6
-    c.state_capacity = 1 << 22
-    with rmc.Checker(c) as ck:
-        with pytest.raises(rmc.RmcError, match=r"messages\[m\] > 3") as e:
-            ck.run()
-    assert e.value.code == -28
     exe = os.path.join(ROOT, "raft.tla_amd", "bin", "rmc-tlc")
     out = subprocess.run([exe, "-depth", "3", "-builtin-raft", "-config", cfgp,
                           os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.tla")],

@@ -1,0 +1,193 @@
+"""The wide layout (raft.tla_amd/csrc/raft_wide.h): models whose fields
+outgrow the packed layout — the reference's own MCraft.cfg (no CONSTRAINT)
+under a depth bound, Smokeraft's unbounded depth-100 walks, bounds beyond
+MaxTerm 14 / MaxLogLen 3 / 8 messages / count 3.
+
+Parity: the same per-level counts as the C oracle (oracle/rmc_oracle.c), the
+same successor sets as the Python restatement (oracle/raft_spec.py) on states
+far beyond the packed capacity, and replayed walks that are behaviours of
+the spec.  RMC_FORCE_WIDE=1 puts packed-size golden models on the wide layout
+to compare the two layouts on the same search."""
+import json
+import os
+import random
+from collections import Counter
+
+import pytest
+
+import rmc
+from oracle import raft_spec as R
+from tests import oracle_c
+from tests.convert import check_trace, from_view, to_view
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_levels.json")))
+
+
+@pytest.fixture
+def force_wide(monkeypatch):
+    monkeypatch.setenv("RMC_FORCE_WIDE", "1")
+
+
+def cfg_from(p, capacity=1 << 24):
+    return rmc.make_config(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
+                           max_log_len=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
+                           bug_quorum=bool(p["bug_quorum"]), invariants=p["invariants"],
+                           max_depth=p["max_depth"], state_capacity=capacity)
+
+
+@pytest.mark.parametrize("name", ["tiny2", "tiny2_v2", "small", "s4_prefix10", "msgs5_dup2_prefix9"])
+def test_wide_layout_matches_oracle_levels(name, force_wide):
+    """The wide layout on packed-size golden models: every per-level count,
+    distinct, generated and depth equal the oracle's."""
+    g = GOLDEN[name]
+    with rmc.Checker(cfg_from(g["params"], capacity=max(1 << 20, int(g["distinct"] * 1.25)))) as ck:
+        assert rmc.native().rmc_state_bytes(ck.cfg) == 568
+        r = ck.run()
+        levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+    assert levels == g["level_new"]
+    assert (r.distinct, r.generated, r.depth, r.left_on_queue) == (g["distinct"], g["generated"], g["depth"],
+                                                                  g["left_on_queue"])
+
+
+@pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "messages_small"])
+def test_wide_layout_violation_and_trace(name, force_wide):
+    g = GOLDEN[name]
+    p = g["params"]
+    with rmc.Checker(cfg_from(p)) as ck:
+        r = ck.run()
+        trace = ck.trace()
+    assert r.violated_inv == g["violated_inv"] and r.violation_depth == g["violation_depth"]
+    assert (r.distinct, r.generated) == (g["distinct"], g["generated"])
+    model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"], max_log=p["max_log_len"],
+                    max_msgs=p["max_msgs"], max_dup=p["max_dup"], bug_quorum=bool(p["bug_quorum"]))
+    check_trace(model, trace, r.violated_inv, r.violation_depth)
+
+
+def test_reference_mcraft_cfg_under_a_depth_bound():
+    """the reference's MCraft.cfg layout (no CONSTRAINT,
+    tests/golden/models/MCunbounded) runs past the packed capacity — depth 6
+    needed a 4th copy of a message (Duplicate) — to depth 8 on the wide
+    layout, level by level equal to the C oracle run with bounds no state of
+    those depths reaches."""
+    cfgp = os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg")
+    base, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, depth_bounded=True)
+    assert (base.max_term, base.max_log_len, base.max_msgs, base.max_dup) == (255, 8, 16, 255)
+    for depth in (6, 7, 8):
+        c = rmc.Config.from_buffer_copy(base)
+        c.max_depth = depth
+        c.state_capacity = 1 << 24
+        with rmc.Checker(c) as ck:
+            r = ck.run()
+            levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+        ref, ln, _ = oracle_c.bfs(3, 2, 127, 4, 8, 127, threads=8, max_levels=depth, capacity=1 << 25)
+        assert (r.distinct, r.generated, r.depth, r.left_on_queue) == (ref.distinct, ref.generated, ref.depth,
+                                                                      ref.left_on_queue), depth
+        assert levels == ln, depth
+
+
+def _walk_states(model, n, depth, seed):
+    """Random walks from Init of the unconstrained spec (Python restatement)."""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        s = R.init_state(model)
+        for _ in range(rng.randint(1, depth)):
+            succ = R.successors(model, s)
+            s = rng.choice(succ)[2]
+        out.append(s)
+    return out
+
+
+def _fits_wide(s):
+    return (all(t <= 250 for t in s.currentTerm) and all(len(lg) <= 7 for lg in s.log) and len(s.messages) <= 15
+            and all(c <= 250 for _, c in s.messages))
+
+
+def test_wide_successors_equal_the_python_restatement_beyond_the_packed_capacity():
+    """Every lane of the wide layout (rmc_expand) on states of long random walks
+    — terms, logs, bag sizes and counts far past the packed capacity — gives
+    exactly the successor multiset of Next in the Python restatement."""
+    model = R.Model()
+    states = [s for s in _walk_states(model, 300, 60, 7) if _fits_wide(s)]
+    beyond = sum(1 for s in states if max(s.currentTerm) > 15 or max(len(x) for x in s.log) > 3
+                 or len(s.messages) > 8 or any(c > 3 for _, c in s.messages))
+    assert beyond > 30
+    cfg = rmc.make_config(max_term=255, max_log_len=8, max_msgs=16, max_dup=255, max_depth=1, state_capacity=1 << 12)
+    with rmc.Checker(cfg) as ck:
+        got = ck.expand([to_view(model, s) for s in states])
+    by_parent = {}
+    for sv in got:
+        assert sv.in_constraint
+        by_parent.setdefault(sv.parent, []).append((rmc.FAMILIES[sv.family], from_view(sv.state)))
+    for k, s in enumerate(states):
+        want = Counter((f, t) for f, _p, t in R.successors(model, s))
+        have = Counter(by_parent.get(k, []))
+        assert have == want, k
+
+
+def _smoke_cfg(mode_tlc=False):
+    cfgp = os.path.join(ROOT, "tests", "golden", "models", "SmokeFixture.cfg")
+    c, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, simulate=True)
+    c.state_capacity = 1 << 12
+    return c
+
+
+@pytest.mark.parametrize("mode", [rmc.SIM_TRUNCATE, rmc.SIM_TLC])
+def test_smokeraft_walks_to_depth_100_without_truncation(mode):
+    """Smokeraft's walks (no bounds, Smokeraft.cfg:46-48) at
+    TLC -simulate's depth 100 on the wide layout: with every enabled successor
+    drawn (TLC's distribution; RMC_SIM_TLC also TLC's action-then-successor
+    draw) no behaviour leaves the layout, and TypeOK holds on every state."""
+    c = _smoke_cfg()
+    assert (c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (255, 8, 16, 255)
+    with rmc.Checker(c) as ck:
+        r = ck.simulate(behaviours=1 << 16, depth=100, smoke_k=2, seed=3, mode=mode)
+    assert r.init_states == 512
+    assert r.violated_inv == 0
+    assert r.truncated == 0, r.truncated
+    assert r.steps + 100 * r.deadlocked >= (1 << 16) * 99
+
+
+def test_smokeraft_wide_replays_are_behaviours_of_the_spec():
+    model = R.Model()
+    c = _smoke_cfg()
+    with rmc.Checker(c) as ck:
+        for b, mode in ((0, rmc.SIM_TRUNCATE), (5, rmc.SIM_TLC), (777, rmc.SIM_TLC)):
+            views = ck.sim_replay(b, behaviours=1024, depth=100, smoke_k=2, seed=11, mode=mode)
+            states = [from_view(v) for v in views]
+            assert len(states) == 100
+            for a, nxt in zip(states, states[1:]):
+                assert nxt in {t for _f, _p, t in R.successors(model, a)}
+            assert all(R.type_ok(model, s) for s in states)
+
+
+def test_wide_capacity_edges_are_never_silently_in_the_model():
+    """A lane whose successor outgrows the wide layout — a 9th log entry, a 17th
+    distinct message, a count or a term past 255 — is listed as outside the
+    model (the BFS stops with RMC_E_CAPACITY on it when the field has no
+    CONSTRAINT, k_wexpand); every other lane of the same state is in it."""
+    model = R.Model()
+    s = R.init_state(model)
+    e = [R.entry(1, 0)] * 8
+    s = s._replace(state=(R.LEADER, R.CANDIDATE, R.FOLLOWER), currentTerm=(1, 255, 1),
+                   log=(tuple(e), (), ()))
+    msgs = {}
+    for k in range(16):
+        m = R.rec(mtype=R.AEP, mterm=1, msuccess=False, mmatchIndex=k, msource=k % 3, mdest=(k + 1) % 3)
+        msgs[m] = 255 if k == 0 else 1
+    s = s._replace(messages=frozenset(msgs.items()))
+    cfg = rmc.make_config(max_term=255, max_log_len=8, max_msgs=16, max_dup=255, max_depth=1, state_capacity=1 << 12)
+    with rmc.Checker(cfg) as ck:
+        got = ck.expand([to_view(model, s)])
+    out = [(rmc.FAMILIES[sv.family], sv.instance) for sv in got if not sv.in_constraint]
+    fams = Counter(f for f, _ in out)
+    assert fams["ClientRequest"] == 2          # leader 0: log full (8 entries)
+    assert fams["Timeout"] == 1                # candidate 1 at term 255
+    assert fams["RequestVote"] == 3            # candidate 1: a 17th message
+    assert fams["AppendEntries"] == 2          # leader 0: a 17th message
+    assert fams["DuplicateMessage"] == 1       # the message held 255 times
+    want = Counter(f for f, _p, t in R.successors(model, s))
+    assert sum(want.values()) == len(got)
