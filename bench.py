@@ -38,7 +38,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBench.cfg"))
     ap.add_argument("--capacity", type=int, default=0,
-                    help="state capacity per GPU (0 = 1.5e9 / world * 1.3 for the bench model)")
+                    help="state capacity per GPU (0: 1.5e9 / world * 1.3 for MCraftBench.cfg, the table size every "
+                         "round measured; any other model: librmc's own sizing, 80%% of free HBM)")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK modulo the visible GPUs")
     ap.add_argument("--keys-per-dest", type=int, default=0,
                     help="sharded mode: phase-1 keys one chunk may send one owner (0 = librmc's choice)")
@@ -310,7 +311,12 @@ def main(argv=None):
     cfg = rmc.config_from_files(a.config, builtin_raft=True)
     cfg.device = dev
     ranks_per_gpu = max(1, -(-world // ndev)) if sharded else 1
-    cfg.state_capacity = a.capacity or int(1.5e9 / world * (1.3 if sharded else 1.0))
+    if a.capacity:
+        cfg.state_capacity = a.capacity
+    elif os.path.basename(a.config) == "MCraftBench.cfg":
+        cfg.state_capacity = int(1.5e9 / world * (1.3 if sharded else 1.0))
+    else:  # e.g. specs/MCraftBench8.cfg (2.56 G states per rank at 288 GB)
+        cfg.state_capacity = 0
     W = rmc.native().rmc_state_bytes(cfg)
     # roofline ceiling of the fingerprint set: random 8-B probes over 64 GB
     r_max = None

@@ -345,6 +345,15 @@ int rmc_sim_replay(rmc_ctx* ctx, const rmc_sim_config* sc, uint64_t behaviour, r
  * the host reads back two small count rows; one all-gather of the device
  * counters per level combines the level statistics.  A key whose owner's
  * outbox is full is parked and sent in a further round of the same level.
+ * Replicated levels: a level of at most RMC_DIST_REP states (default 2^20) is
+ * gathered whole on every rank (one all-gather of state records) and every
+ * rank expands all of it, probing and storing only the successors it owns —
+ * no key or state exchange for the small levels at either end of the search.
+ * Deadlines: every collective and the communicator set-up run under
+ * RMC_DIST_TIMEOUT_S (default 300 s; the RCCL communicator is non-blocking and
+ * aborted on expiry, host-transport callbacks are expected to honour it too):
+ * a stalled rank makes every other rank's rmc_run_bfs return RMC_E_HIP naming
+ * the level, round and phase.
  * Transport: RCCL over xGMI (rccl_id = an id from rmc_rccl_unique_id on rank
  * 0, given to every rank; host = NULL), or a caller-supplied host transport
  * (rccl_id = NULL) whose callbacks move host buffers: alltoallv sends

@@ -2,7 +2,7 @@
 one JSON line per level — level, frontier expanded, new states, generated,
 seconds since the start — for a TLC model file.  Measurement tool.
 
-    python tools/level_times.py specs/MCraftBench.cfg > levels.jsonl
+    python tools/level_times.py specs/MCraftBench.cfg [capacity [max_depth]] > levels.jsonl
 """
 import json
 import os
@@ -14,6 +14,8 @@ import rmc  # noqa: E402
 
 cfg = rmc.config_from_files(sys.argv[1], builtin_raft=True)
 cfg.state_capacity = int(sys.argv[2]) if len(sys.argv) > 2 else 1_500_000_000
+if len(sys.argv) > 3:
+    cfg.max_depth = int(sys.argv[3])  # a prefix of a model larger than one GPU
 with rmc.Checker(cfg) as ck:
     ck.run()  # warm
     r = ck.run()
