@@ -66,6 +66,7 @@ struct DistState {
     double timeout_s = 300.0;
     int nonblocking = 0;            // the RCCL communicator is non-blocking
     int aborted = 0;                // a deadline aborted the communicator: the ctx is unusable
+    int abort_pending = 0;          // ... and the abort has not returned: device buffers are leaked, not freed
     int lvl = 0, rnd = 0;
     const char* phase = "";
     int stall_rank = -1, stall_level = 2;  // test hook (RMC_DIST_STALL_*)

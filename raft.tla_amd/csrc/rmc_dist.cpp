@@ -24,7 +24,9 @@
 // caller-supplied host transport (gloo in the tests, where several ranks share
 // one GPU; every collective is then a synchronous host round trip).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -56,18 +58,39 @@ std::string where(const rmc_ctx* c) {
            std::to_string(D.lvl) + ", round " + std::to_string(D.rnd) + ", phase " + D.phase;
 }
 
+// ncclCommAbort of a communicator whose peers never connected can itself wait
+// on them (the bootstrap of an unfinished init): it runs on a helper thread,
+// waited for at most kAbortWait s; past that the call returns and the helper
+// is left to the process exit (after a deadline the caller ends the process,
+// rmc.h).  Returns whether the abort completed.
+constexpr double kAbortWait = 10.0;
+bool abort_bounded(ncclComm_t comm) {
+    auto done = std::make_shared<std::atomic<int>>(0);
+    std::thread([comm, done] {
+        (void)ncclCommAbort(comm);
+        done->store(1);
+    }).detach();
+    const double t0 = now_s();
+    while (!done->load() && now_s() - t0 < kAbortWait) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    return done->load() != 0;
+}
+
 int deadline_fail(rmc_ctx* c, const char* what) {
     DistState& D = c->dist;
     D.aborted = 1;
+    bool aborted = true;
     if (D.rccl && D.comm) {
-        (void)ncclCommAbort(D.comm);
+        aborted = abort_bounded(D.comm);
         D.comm = nullptr;
+        D.abort_pending = aborted ? 0 : 1;
     }
     char t[32];
     snprintf(t, sizeof t, "%g", D.timeout_s);
     return fail(c, RMC_E_HIP, std::string("sharded search: ") + what + " did not complete within the " + t +
                                   " s deadline (RMC_DIST_TIMEOUT_S) at " + where(c) +
-                                  (D.rccl ? "; the RCCL communicator was aborted" : ""));
+                                  (!D.rccl ? "" : aborted ? "; the RCCL communicator was aborted"
+                                                          : "; the RCCL communicator's abort is still pending "
+                                                            "(end the process)"));
 }
 
 // Wait for an event of the exchange path under the deadline: spin first (a
@@ -305,6 +328,12 @@ namespace rmc_host {
 
 void free_dist(rmc_ctx* c) {
     DistState& D = c->dist;
+    if (D.abort_pending) {  // RCCL kernels may still wait on these buffers: leave them to the process exit
+        D = DistState{};
+        D.aborted = 1;
+        D.abort_pending = 1;
+        return;
+    }
     if (D.xs) (void)hipStreamSynchronize(D.xs);
     (void)hipFree(c->B.sent);
     (void)hipFree(c->B.ovf);
@@ -970,7 +999,35 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
         if (const char* e = getenv("RMC_DIST_NCCL_BLOCKING")) D.nonblocking = atoi(e) ? 0 : 1;
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = D.nonblocking ? 0 : 1;
-        ncclResult_t r = ncclCommInitRankConfig(&D.comm, world, u, rank, &cfg);
+        // the init call itself on a helper thread, waited for under the
+        // deadline: a non-blocking init returns at once, but the call does not
+        // promise so for every bootstrap state (a peer that never connects)
+        struct Init {
+            std::atomic<int> done{0};
+            ncclComm_t comm = nullptr;
+            ncclResult_t r = ncclSuccess;
+        };
+        auto in = std::make_shared<Init>();
+        std::thread([in, world, u, rank, cfg]() mutable {
+            in->r = ncclCommInitRankConfig(&in->comm, world, u, rank, &cfg);
+            in->done.store(1);
+        }).detach();
+        const double t_init = now_s();
+        while (!in->done.load()) {
+            if (now_s() - t_init > D.timeout_s) {
+                // the helper still owns the call: left to the process exit
+                D.comm = nullptr;
+                D.rccl = 0;
+                const int rc = deadline_fail(c, "ncclCommInitRankConfig (the init call; it has not returned)");
+                const std::string msg = c->err;
+                free_dist(c);
+                c->err = msg;
+                return rc;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+        D.comm = in->comm;
+        ncclResult_t r = in->r;
         if (r != ncclSuccess && r != ncclInProgress) {
             D.comm = nullptr;
             free_dist(c);

@@ -1044,8 +1044,8 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // The single-GPU expansion kernel: the lane-superset walk over class-sorted
 // windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
 // loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_sort(
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, false, false, true, true, true, false, 16, PI, false, PS>(P, PT, B, lo, hi);
@@ -1069,10 +1069,13 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // the lane-superset walk over class-sorted windows of 8 tiles (4 waves/SIMD;
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
-template <int S, int K, int BATCH, bool REP>
+// PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
+template <int S, int K, int BATCH, bool REP, bool PS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (Lanes<S, K>::N <= 64)
+    if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
+    else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
         expand_body<S, K, false, BATCH, true, false, false, false, false, true>(P, PT, B, lo, hi);
@@ -1657,6 +1660,16 @@ static int expand_variant() {
     return v;
 }
 
+// Sharded expansion kernel (RMC_DIST_KVARIANT, A/B): 0 (default) windows of 8
+// tiles sorted in LDS; 1 windows of 16 tiles presorted by k_window_order.
+static int dist_kvariant() {
+    static int v = [] {
+        const char* e = getenv("RMC_DIST_KVARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 // Probes in flight per thread: 8 (measured best of 4/8/16 on MI355X).
 constexpr int kBatch = 8;
 
@@ -1693,11 +1706,19 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
         } else if (expand_variant() == 6 && SORTED) {
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if (expand_variant() == 7 && SORTED && B.word) {  // windows presorted by k_window_order
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true>));
+        } else if (expand_variant() >= 7 && expand_variant() <= 9 && SORTED && B.word) {
+            // windows presorted by k_window_order (no sort in LDS): 4, 5 or 6 waves/SIMD
+#define RMC_PRESORT(WPE)                                                                                       \
+    {                                                                                                          \
+        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, WPE>)); \
+        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                            \
+        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                               \
+        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, WPE>));                           \
+    }
+            if (expand_variant() == 7) RMC_PRESORT(4)
+            else if (expand_variant() == 8) RMC_PRESORT(5)
+            else RMC_PRESORT(6)
+#undef RMC_PRESORT
         } else {  // 1, and shapes with more than 64 lanes
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
         }
@@ -1705,7 +1726,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
     } else if (which == 3) {
         if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
-        else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
+        else if (dist_kvariant() == 1 && SORTED && B.word) {                      // presorted windows (A/B)
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, false, true>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
+        } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
         else return hipErrorInvalidValue;

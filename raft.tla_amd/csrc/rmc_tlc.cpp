@@ -286,8 +286,9 @@ int main(int argc, char** argv) {
     if (nodeadlock) c.flags &= ~RMC_FLAG_CHECK_DEADLOCK;
     if (verify) c.flags |= RMC_FLAG_VERIFY_STATES;
     // like TLC's states/ directory, expanded levels leave the device when it fills
-    // (single GPU; full-state verification keeps every state resident)
-    if (!nospill && !verify && gpus == 1) c.flags |= RMC_FLAG_SPILL;
+    // (single GPU, packed layout; full-state verification keeps every state
+    // resident, and the wide layout of -depth runs of unbounded models has no spill)
+    if (!nospill && !verify && gpus == 1 && rmc_state_bytes(&c) <= 64 * 4) c.flags |= RMC_FLAG_SPILL;
     c.device_window = window;
     c.seed = fpseed;
     printf("Model: %d servers, %d values, CONSTRAINT MaxTerm=%d MaxLogLen=%d MaxMsgs=%d MaxDup=%d%s%s\n",
