@@ -613,6 +613,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         depth = c->resume_depth;
     } else {
     c->res = rmc_result{};
+    c->walked = 0;
     c->level_start.clear();
     if (c->spill.on) {
         spill_rebase(c, 0);
@@ -737,6 +738,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         }
         c->res.generated += k.generated;
         c->res.probes += k.probes;
+        c->walked += k.walked;
         const u64 nnew = k.count - hi;
         if (nnew) {
             ++depth;
@@ -773,6 +775,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     // TLC's "calculated (optimistic)" fingerprint-collision estimate
     c->res.collision_probability = D * (G - D) / 18446744073709551616.0;
     c->res.seconds = secs();
+    if (getenv("RMC_WALK_STATS"))  // lane efficiency of the walk: enabled lanes / visited slots
+        fprintf(stderr, "[rmc] lane walk: %llu slots visited, %llu generated, %llu probes: efficiency %.4f\n",
+                (unsigned long long)c->walked, (unsigned long long)c->res.generated,
+                (unsigned long long)c->res.probes, c->walked ? G / (double)c->walked : 0.0);
     return 0;
 }
 

@@ -113,6 +113,7 @@ struct rmc_ctx {
     rmc::Counters* h_ctr = nullptr;  // pinned
     rmc::u32* d_staged = nullptr;
     rmc::u64 table_slots = 0;
+    rmc::u64 walked = 0;  // (state, lane) slots of the lane walk in the last run (RMC_WALK_STATS)
     rmc_result res{};
     std::string err;
     std::vector<rmc::u64> level_start;  // level d (1-based) = [level_start[d-1], level_start[d])

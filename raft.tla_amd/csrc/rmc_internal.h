@@ -23,6 +23,7 @@ struct Counters {
     u64 vcount;     // deferred hits in vbuf (stored twin not yet published)
     u64 nties;      // SYMMETRY: successors with tied signatures deferred to k_ties
     u64 novf;       // sharded: keys that did not fit their owner's outbox (parked in B.ovf)
+    u64 walked;     // (state, lane) slots the lane walk visited (RMC_WALK_STATS: lane efficiency = generated / walked)
 };
 
 struct DevBufs {

@@ -657,6 +657,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u64 gen = 0;
     u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
+    u64 walked = 0;  // (live state, lane) slots visited by the wave (wave-uniform)
     const u64 nf = hi - lo;
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
     // tiles per window, fewer when the launch has too few states to give every
@@ -779,6 +780,16 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     wm &= wm - 1;
                     lp |= ln << (7 * b);
                 }
+            }
+            {
+                int nb = 0;  // lanes of this batch
+                if constexpr (SORT) {
+#pragma unroll
+                    for (int b = 0; b < BATCH; ++b) nb += ((lp >> (7 * b)) & 127u) != 127u;
+                } else {
+                    nb = nl - lane0 < BATCH ? nl - lane0 : BATCH;
+                }
+                walked += (u64)nb * (u64)__popcll(__ballot(live));
             }
             u64 cur_p[PIPE ? BATCH : 1];  // PIPE: the probes issued during (a)
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
@@ -1004,6 +1015,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         gs += (u64)(u32)__shfl_xor((int)(u32)gs, off) | ((u64)(u32)__shfl_xor((int)(u32)(gs >> 32), off) << 32);
     if (me == 0 && gs) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)gs);
     if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
+    if (me == 0 && walked) atomicAdd((unsigned long long*)&B.ctr->walked, (unsigned long long)walked);
     if constexpr (VERIFY) {
         vchk = wave_sum64(vchk);
         vcol = wave_sum64(vcol);
