@@ -610,7 +610,8 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 //   level's records in B.rep (gathered from every rank); every rank expands
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
-          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false>
+          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
+          int PF = 0>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -624,6 +625,12 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // so the kernel carries no sort: no LDS bins, scan or block barriers
     static_assert(!PRESORT || (SORT && !REP), "presorted windows: the sorted kernels");
     constexpr bool INSORT = SORT && !PRESORT;
+    // PF: the next tile's state (and its lane + footprint) is loaded while this
+    // one's lanes are walked (presorted windows: its position is one load away);
+    // PF = 1 into registers, PF = 2 by LDS-DMA (global_load_lds: no registers
+    // held across the walk; per wave [word][lane] images, read back at the tile)
+    static_assert(!PF || (PRESORT && DIA && !REP), "prefetch: the presorted single-GPU kernel");
+    constexpr bool PFR = PF == 1, PFD = PF == 2;
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
     typedef RepRec<S, K> RR;
@@ -657,7 +664,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u64 gen = 0;
     u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
-    u64 walked = 0;  // (live state, lane) slots visited by the wave (wave-uniform)
+    u32 walked = 0;  // (live state, lane) slots this thread's waves visited for it
     const u64 nf = hi - lo;
     const int nl = P.off[10];  // == Lanes<S,K>::N; runtime on purpose (see lane_delta)
     // tiles per window, fewer when the launch has too few states to give every
@@ -706,10 +713,64 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         }
         __syncthreads();
     }
+    u64 pf_w[PFR ? S : 1], pf_foot = 0, pf_rel = 0;
+    u32 pf_m[PFR ? K : 1], pf_act = 255;
+    bool pf_live = false;
+    __shared__ u32 s_pfw[PFD ? 4 : 1][PFD ? NW + 2 : 1][64];  // PFD: state words, footprint lo/hi
+    __shared__ uint8_t s_pfa[PFD ? 4 : 1][64];               // PFD: lane byte
+    u32 pf_word = 0;  // PFD: the position (B.word) of the tile after the prefetched one
+    auto pf_rel_of = [&](int k, u32 word, bool& lv) -> u64 {
+        const u32 p = (u32)k * 256u + threadIdx.x;
+        lv = p < wn;
+        return win + (lv ? word : 0u);
+    };
+    auto pf_issue = [&](int k) {  // PF: start tile k's state on its way
+        if constexpr (PFR) {
+            const u32 p = (u32)k * 256u + threadIdx.x;
+            pf_rel = pf_rel_of(k, p < wn ? (u32)B.word[win + p] : 0u, pf_live);
+            if (pf_live) {
+                load_state<S, K>(fr + (lo + pf_rel) * (u64)FW, pf_w, pf_m);
+                pf_act = B.act[lo + pf_rel];
+                pf_foot = B.foot[lo + pf_rel];
+            } else {
+#pragma unroll
+                for (int i = 0; i < S; ++i) pf_w[i] = 0;
+#pragma unroll
+                for (int q = 0; q < K; ++q) pf_m[q] = 0;
+                pf_act = 255;
+                pf_foot = 0;
+            }
+        } else if constexpr (PFD) {
+            // the DMA writes lane l's 4 bytes at base + 4 l: one instruction per
+            // word of the record; a dead lane reads the frontier's first record
+            const u64 ix = lo + (pf_live ? pf_rel : 0ull);
+            const u32* src = fr + ix * (u64)FW;
+            const int wvs = __builtin_amdgcn_readfirstlane(wv);  // scalar: the image bases stay in SGPRs
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the previous image was read out
+#pragma unroll
+            for (int c = 0; c < NW; ++c)
+                __builtin_amdgcn_global_load_lds(src + c, &s_pfw[wvs][c][0], 4, 0, 0);
+            const u32* fw = reinterpret_cast<const u32*>(B.foot + ix);
+            __builtin_amdgcn_global_load_lds(fw, &s_pfw[wvs][NW][0], 4, 0, 0);
+            __builtin_amdgcn_global_load_lds(fw + 1, &s_pfw[wvs][NW + 1][0], 4, 0, 0);
+            __builtin_amdgcn_global_load_lds(B.act + ix, &s_pfa[wvs][0], 1, 0, 0);
+            (void)k;
+        }
+    };
+    if constexpr (PFR) pf_issue(0);
+    if constexpr (PFD) {
+        const u32 p0 = threadIdx.x, p1 = 256u + threadIdx.x;
+        pf_rel = pf_rel_of(0, p0 < wn ? (u32)B.word[win + p0] : 0u, pf_live);
+        pf_word = (wt > 1 && p1 < wn) ? (u32)B.word[win + p1] : 0u;
+        pf_issue(0);
+    }
     for (int wk = 0; wk < (int)wt; ++wk) {
         u64 rel;
         bool live;
-        if constexpr (SORT) {
+        if constexpr (PF) {
+            rel = pf_rel;
+            live = pf_live;
+        } else if constexpr (SORT) {
             const u32 p = (u32)wk * 256u + threadIdx.x;
             live = p < wn;
             if constexpr (PRESORT) rel = win + (live ? (u32)B.word[win + p] : 0u);
@@ -721,7 +782,40 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         u64 w[S];
         u32 m[K];
         const u32* rec = fr + (lo + rel) * (u64)FW;
-        if (live) {
+        int pf_a = 255;
+        u64 pf_f = 0;
+        if constexpr (PFR) {
+#pragma unroll
+            for (int i = 0; i < S; ++i) w[i] = pf_w[i];
+#pragma unroll
+            for (int q = 0; q < K; ++q) m[q] = pf_m[q];
+            pf_a = (int)pf_act;
+            pf_f = pf_foot;
+            if (wk + 1 < (int)wt) pf_issue(wk + 1);
+        } else if constexpr (PFD) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this tile's image has landed
+            const int ln = me;
+#pragma unroll
+            for (int i = 0; i < S; ++i) w[i] = (u64)s_pfw[wv][2 * i][ln] | ((u64)s_pfw[wv][2 * i + 1][ln] << 32);
+#pragma unroll
+            for (int q = 0; q < K; ++q) m[q] = s_pfw[wv][2 * S + q][ln];
+            pf_f = (u64)s_pfw[wv][NW][ln] | ((u64)s_pfw[wv][NW + 1][ln] << 32);
+            pf_a = (int)s_pfa[wv][ln];
+            if (!live) {
+#pragma unroll
+                for (int i = 0; i < S; ++i) w[i] = 0;
+#pragma unroll
+                for (int q = 0; q < K; ++q) m[q] = 0;
+                pf_a = 255;
+                pf_f = 0;
+            }
+            if (wk + 1 < (int)wt) {  // the next tile: its position was loaded a tile ago
+                pf_rel = pf_rel_of(wk + 1, pf_word, pf_live);
+                const u32 p2 = (u32)(wk + 2) * 256u + threadIdx.x;
+                pf_word = (wk + 2 < (int)wt && p2 < wn) ? (u32)B.word[win + p2] : 0u;
+                pf_issue(wk + 1);
+            }
+        } else if (live) {
             load_state<S, K>(rec, w, m);
         } else {
 #pragma unroll
@@ -757,7 +851,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             int act = 255;
             u64 foot = 0;
             if (on) {
-                if constexpr (REP) {
+                if constexpr (PF) {
+                    act = pf_a;
+                    foot = pf_f;
+                } else if constexpr (REP) {
                     act = (int)(rec[RR::ACT] & 0xFFu);
                     foot = (u64)rec[RR::FOOT] | ((u64)rec[RR::FOOT + 1] << 32);
                 } else {
@@ -771,6 +868,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         // SORT: the lanes some state of this wave can enable (wave-uniform, scalar)
         u64 wm = 0;
         if constexpr (SORT) wm = wave_or64(live ? lane_superset<S, K>(w, m, P.V) : 0ull);
+        walked += live ? (u32)(SORT ? __popcll(wm) : nl) : 0u;  // per thread (a VGPR: no scalar register held)
         for (int lane0 = 0; SORT ? (wm != 0) : (lane0 < nl); lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
             u64 lp = 0;  // SORT: this batch's lanes, 7 bits each (127 = none), a scalar
             if constexpr (SORT) {
@@ -780,16 +878,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     wm &= wm - 1;
                     lp |= ln << (7 * b);
                 }
-            }
-            {
-                int nb = 0;  // lanes of this batch
-                if constexpr (SORT) {
-#pragma unroll
-                    for (int b = 0; b < BATCH; ++b) nb += ((lp >> (7 * b)) & 127u) != 127u;
-                } else {
-                    nb = nl - lane0 < BATCH ? nl - lane0 : BATCH;
-                }
-                walked += (u64)nb * (u64)__popcll(__ballot(live));
             }
             u64 cur_p[PIPE ? BATCH : 1];  // PIPE: the probes issued during (a)
             // (a) deltas + fingerprints of BATCH lanes; keys parked in LDS (0 = no probe).
@@ -1015,7 +1103,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         gs += (u64)(u32)__shfl_xor((int)(u32)gs, off) | ((u64)(u32)__shfl_xor((int)(u32)(gs >> 32), off) << 32);
     if (me == 0 && gs) atomicAdd((unsigned long long*)&B.ctr->generated, (unsigned long long)gs);
     if (me == 0 && pr) atomicAdd((unsigned long long*)&B.ctr->probes, (unsigned long long)pr);
-    if (me == 0 && walked) atomicAdd((unsigned long long*)&B.ctr->walked, (unsigned long long)walked);
+    const u64 wk_sum = wave_sum64((u64)walked);
+    if (me == 0 && wk_sum) atomicAdd((unsigned long long*)&B.ctr->walked, (unsigned long long)wk_sum);
     if constexpr (VERIFY) {
         vchk = wave_sum64(vchk);
         vcol = wave_sum64(vcol);
@@ -1056,11 +1145,11 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // The single-GPU expansion kernel: the lane-superset walk over class-sorted
 // windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
 // loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4>
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, int PF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, true, true, false, 16, PI, false, PS>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, true, true, true, false, 16, PI, false, PS, PF>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1082,8 +1171,8 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_expand_dist(
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
@@ -1673,7 +1762,8 @@ static int expand_variant() {
 }
 
 // Sharded expansion kernel (RMC_DIST_KVARIANT, A/B): 0 (default) windows of 8
-// tiles sorted in LDS; 1 windows of 16 tiles presorted by k_window_order.
+// tiles sorted in LDS; 1 windows of 16 tiles presorted by k_window_order; 2 the
+// same with 6 probes in flight per thread at 5 waves/SIMD.
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
@@ -1718,18 +1808,37 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
         } else if (expand_variant() == 6 && SORTED) {
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if (expand_variant() >= 7 && expand_variant() <= 9 && SORTED && B.word) {
-            // windows presorted by k_window_order (no sort in LDS): 4, 5 or 6 waves/SIMD
-#define RMC_PRESORT(WPE)                                                                                       \
-    {                                                                                                          \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, WPE>)); \
-        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                            \
-        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                               \
-        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, WPE>));                           \
+        } else if (expand_variant() == 12 && SORTED && B.word) {  // presorted + next-state prefetch
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 1>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 1>));
+        } else if (expand_variant() == 13 && SORTED && B.word) {  // presorted + next-state LDS-DMA
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 2>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 2>));
+        } else if (((expand_variant() >= 7 && expand_variant() <= 11) || (expand_variant() >= 14 && expand_variant() <= 17)) &&
+                   SORTED && B.word) {
+            // windows presorted by k_window_order (no sort in LDS): probes in flight
+            // per thread x waves/SIMD: 7 (8, 4), 8 (8, 5), 9 (8, 6), 10 (6, 5), 11 (4, 6),
+            // 14 (6, 6), 15 (5, 5), 16 (4, 5), 17 (7, 5)
+#define RMC_PRESORT(BT, WPE)                                                                                 \
+    {                                                                                                        \
+        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE>)); \
+        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
+        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
+        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE>));                             \
     }
-            if (expand_variant() == 7) RMC_PRESORT(4)
-            else if (expand_variant() == 8) RMC_PRESORT(5)
-            else RMC_PRESORT(6)
+            if (expand_variant() == 7) RMC_PRESORT(kBatch, 4)
+            else if (expand_variant() == 8) RMC_PRESORT(kBatch, 5)
+            else if (expand_variant() == 9) RMC_PRESORT(kBatch, 6)
+            else if (expand_variant() == 10) RMC_PRESORT(6, 5)
+            else if (expand_variant() == 11) RMC_PRESORT(4, 6)
+            else if (expand_variant() == 14) RMC_PRESORT(6, 6)
+            else if (expand_variant() == 15) RMC_PRESORT(5, 5)
+            else if (expand_variant() == 16) RMC_PRESORT(4, 5)
+            else RMC_PRESORT(7, 5)
 #undef RMC_PRESORT
         } else {  // 1, and shapes with more than 64 lanes
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
@@ -1743,6 +1852,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
+        } else if (dist_kvariant() == 2 && SORTED && B.word) {  // presorted, 6 probes in flight, 5 waves/SIMD
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
