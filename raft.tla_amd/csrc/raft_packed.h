@@ -844,57 +844,58 @@ RMC_HD void fill_lane_desc(Params& P, int S) {
     for (int l = 0; l < 64; ++l) P.ldesc[l] = l < P.off[10] ? lane_desc(P, l, S) : 0u;
 }
 
-// Per expanded state: a's side of the test (lane a = act, its footprint).
+// Per expanded state: a's side of the test (lane a = act, its footprint),
+// packed into 4 words (it is live across the whole lane walk).
+// Instance order key (0 = none): lanes of families 0-6 by (family, lane),
+// message lanes by (family, message): 1 + (f << 6 | lane) < 2^30 <= (f - 6) << 30 | msg.
+RMC_HD u32 diamond_order(int f, int lane, u32 msg) {
+    return f < 7 ? 1u + (((u32)f << 6) | (u32)lane) : (((u32)(f - 6)) << 30) | msg;
+}
 struct Diamond {
-    u64 ord;   // a's instance order key; 0 = no skipping from this state
+    u32 ord;     // a's instance order key; 0 = no skipping from this state
     u32 k0, k1;  // a's messages (sentinels when absent; never equal to a 30-bit message)
-    int srv;   // a's server word, -1 none
-    int dom;   // max |DOMAIN messages| of b(t) so that b(s) is in the model
+    u32 sd;      // a's server word (bits 0-7, 0xFF none) | max |DOMAIN messages| of b(t) so that b(s) is in the model << 8
 };
 template <int S, int K>
 RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diamond& dm) {
     dm.ord = 0;
     dm.k0 = 0xFFFFFFFFu;
     dm.k1 = 0xFFFFFFFEu;
-    dm.srv = -1;
-    dm.dom = 0;
+    dm.sd = 0xFFu;
     if (a == 255 || !(foot & FOOT_VALID)) return;
     const int fa = lane_family(P, a);
     const u32 mact = (u32)(foot & MSG_MASK), madd = (u32)((foot >> 30) & MSG_MASK);
-    dm.ord = ((u64)fa << 40) | (fa < 7 ? (u64)a : (u64)mact) | (1ull << 48);
+    dm.ord = diamond_order(fa, a, mact);
     if (foot & FOOT_ACT) dm.k0 = mact;
     if (foot & FOOT_ADD) dm.k1 = madd;
-    dm.srv = lane_server<S>(P, a, fa, mact);
+    const int srv = lane_server<S>(P, a, fa, mact);
     int delta = 0;
     if ((foot & FOOT_ADD) && count_of<K>(m, madd) == 1) delta += 1;       // a created the key
     if ((foot & FOOT_CONSUMED) && count_of<K>(m, mact) == 0) delta -= 1;  // a removed its last copy
-    dm.dom = P.max_msgs + delta;
+    dm.sd = (u32)(srv & 0xFF) | ((u32)(P.max_msgs + delta) << 8);
+}
+RMC_HD bool diamond_rest(int sb, u32 mb, const Delta& db, int nmsg_b, const Diamond& dm) {
+    if (sb >= 0 && (u32)sb == (dm.sd & 0xFFu)) return false;
+    const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
+    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
+    return nmsg_b <= (int)(dm.sd >> 8);
 }
 // b's side from lane b's descriptor (lanes < 64): the same test as diamond_skip.
 template <int S, int K>
 RMC_HD bool diamond_skip_desc(const u32 (&m)[K], int b, u32 desc, const Delta& db, int nmsg_b, const Diamond& dm) {
     const int fb = (int)(desc & 15u), tb = (int)((desc >> 4) & 255u), sd = (int)((desc >> 12) & 7u);
     const u32 mb = fb >= 7 ? (selm<K>(m, tb) & MSG_MASK) : 0xFFFFFFFDu;
-    const u64 ob = ((u64)fb << 40) | (fb < 7 ? (u64)b : (u64)mb) | (1ull << 48);
-    if (!(ob < dm.ord)) return false;  // dm.ord = 0: never (the common exit)
+    if (!(diamond_order(fb, b, mb) < dm.ord)) return false;  // dm.ord = 0: never (the common exit)
     const int sb = sd < 7 ? sd : fb == 7 ? (int)m_dst(mb) : -1;
-    if (sb >= 0 && sb == dm.srv) return false;
-    const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
-    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
-    return nmsg_b <= dm.dom;
+    return diamond_rest(sb, mb, db, nmsg_b, dm);
 }
 // b's side: lane b with delta db on t (m = t's bag), nmsg_b = |DOMAIN| of b(t).
 template <int S, int K>
 RMC_HD bool diamond_skip(const u32 (&m)[K], int b, const Delta& db, int nmsg_b, const Diamond& dm, const Params& P) {
     const int fb = lane_family(P, b);
     const u32 mb = fb >= 7 ? (selm<K>(m, b - family_off(P, fb)) & MSG_MASK) : 0xFFFFFFFDu;
-    const u64 ob = ((u64)fb << 40) | (fb < 7 ? (u64)b : (u64)mb) | (1ull << 48);
-    if (!(ob < dm.ord)) return false;  // dm.ord = 0: never
-    const int sb = lane_server<S>(P, b, fb, mb);
-    if (sb >= 0 && sb == dm.srv) return false;
-    const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
-    if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
-    return nmsg_b <= dm.dom;
+    if (!(diamond_order(fb, b, mb) < dm.ord)) return false;  // dm.ord = 0: never
+    return diamond_rest(lane_server<S>(P, b, fb, mb), mb, db, nmsg_b, dm);
 }
 
 // ---- invariants (fused into the insert of a new state) -----------------------------

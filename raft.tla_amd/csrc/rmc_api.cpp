@@ -775,7 +775,9 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     // TLC's "calculated (optimistic)" fingerprint-collision estimate
     c->res.collision_probability = D * (G - D) / 18446744073709551616.0;
     c->res.seconds = secs();
-    if (getenv("RMC_WALK_STATS"))  // lane efficiency of the walk: enabled lanes / visited slots
+    // lane efficiency of the walk: enabled lanes / visited slots (the kernels count
+    // the slots only when built with -DRMC_WALK_STATS_BUILD: a register in the hot loop)
+    if (getenv("RMC_WALK_STATS"))
         fprintf(stderr, "[rmc] lane walk: %llu slots visited, %llu generated, %llu probes: efficiency %.4f\n",
                 (unsigned long long)c->walked, (unsigned long long)c->res.generated,
                 (unsigned long long)c->res.probes, c->walked ? G / (double)c->walked : 0.0);

@@ -661,7 +661,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     uint8_t* l_dest = s_dest[SENTC ? wv : 0];
     u64* l_key = s_lkey[SENTC ? wv : 0];
     u32 n = 0;  // wave-uniform list length
-    u64 gen = 0;
+    u32 gen = 0;  // generated lanes of this thread's states (< 2^32 per launch)
     u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
     u64 pr = 0;  // probes issued by the whole wave (wave-uniform)
     u32 walked = 0;  // (live state, lane) slots this thread's waves visited for it
@@ -868,7 +868,9 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         // SORT: the lanes some state of this wave can enable (wave-uniform, scalar)
         u64 wm = 0;
         if constexpr (SORT) wm = wave_or64(live ? lane_superset<S, K>(w, m, P.V) : 0ull);
+#ifdef RMC_WALK_STATS_BUILD
         walked += live ? (u32)(SORT ? __popcll(wm) : nl) : 0u;  // per thread (a VGPR: no scalar register held)
+#endif
         for (int lane0 = 0; SORT ? (wm != 0) : (lane0 < nl); lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
             u64 lp = 0;  // SORT: this batch's lanes, 7 bits each (127 = none), a scalar
             if constexpr (SORT) {
@@ -1097,7 +1099,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
     // wave reductions of the generated and probe counts, one atomic each per wave
-    u64 gs = gen;
+    u64 gs = (u64)gen;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
         gs += (u64)(u32)__shfl_xor((int)(u32)gs, off) | ((u64)(u32)__shfl_xor((int)(u32)(gs >> 32), off) << 32);
@@ -1145,11 +1147,11 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // The single-GPU expansion kernel: the lane-superset walk over class-sorted
 // windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
 // loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, int PF = 0>
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, int PF = 0, bool PRE = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, true, true, true, false, 16, PI, false, PS, PF>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, PF>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1818,6 +1820,19 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 2>));
+        } else if (expand_variant() >= 18 && expand_variant() <= 19 && SORTED && B.word) {
+            // presorted, 6 probes in flight, the parent's mixes recomputed per lane
+            // instead of held (fewer VGPRs): 6 (18) or 5 (19) waves/SIMD
+#define RMC_PRESORT_NP(WPE)                                                                                  \
+    {                                                                                                        \
+        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, WPE, 0, false>)); \
+        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
+        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
+        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, WPE, 0, false>));                    \
+    }
+            if (expand_variant() == 18) RMC_PRESORT_NP(6)
+            else RMC_PRESORT_NP(5)
+#undef RMC_PRESORT_NP
         } else if (((expand_variant() >= 7 && expand_variant() <= 11) || (expand_variant() >= 14 && expand_variant() <= 17)) &&
                    SORTED && B.word) {
             // windows presorted by k_window_order (no sort in LDS): probes in flight
