@@ -625,12 +625,13 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // so the kernel carries no sort: no LDS bins, scan or block barriers
     static_assert(!PRESORT || (SORT && !REP), "presorted windows: the sorted kernels");
     constexpr bool INSORT = SORT && !PRESORT;
-    // PF: the next tile's state (and its lane + footprint) is loaded while this
-    // one's lanes are walked (presorted windows: its position is one load away);
-    // PF = 1 into registers, PF = 2 by LDS-DMA (global_load_lds: no registers
-    // held across the walk; per wave [word][lane] images, read back at the tile)
+    // PF: the next tile's state (and its lane + footprint) is loaded into
+    // registers while this one's lanes are walked (presorted windows: its
+    // position is one load away).  (An LDS-DMA form, global_load_lds into per-wave
+    // images, was written and dropped in round 4: the loop-carried position
+    // load forced a full vmcnt wait per tile, and it held as many VGPRs.)
     static_assert(!PF || (PRESORT && DIA && !REP), "prefetch: the presorted single-GPU kernel");
-    constexpr bool PFR = PF == 1, PFD = PF == 2;
+    constexpr bool PFR = PF == 1;
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
     typedef RepRec<S, K> RR;
@@ -716,9 +717,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     u64 pf_w[PFR ? S : 1], pf_foot = 0, pf_rel = 0;
     u32 pf_m[PFR ? K : 1], pf_act = 255;
     bool pf_live = false;
-    __shared__ u32 s_pfw[PFD ? 4 : 1][PFD ? NW + 2 : 1][64];  // PFD: state words, footprint lo/hi
-    __shared__ uint8_t s_pfa[PFD ? 4 : 1][64];               // PFD: lane byte
-    u32 pf_word = 0;  // PFD: the position (B.word) of the tile after the prefetched one
     auto pf_rel_of = [&](int k, u32 word, bool& lv) -> u64 {
         const u32 p = (u32)k * 256u + threadIdx.x;
         lv = p < wn;
@@ -740,30 +738,9 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 pf_act = 255;
                 pf_foot = 0;
             }
-        } else if constexpr (PFD) {
-            // the DMA writes lane l's 4 bytes at base + 4 l: one instruction per
-            // word of the record; a dead lane reads the frontier's first record
-            const u64 ix = lo + (pf_live ? pf_rel : 0ull);
-            const u32* src = fr + ix * (u64)FW;
-            const int wvs = __builtin_amdgcn_readfirstlane(wv);  // scalar: the image bases stay in SGPRs
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the previous image was read out
-#pragma unroll
-            for (int c = 0; c < NW; ++c)
-                __builtin_amdgcn_global_load_lds(src + c, &s_pfw[wvs][c][0], 4, 0, 0);
-            const u32* fw = reinterpret_cast<const u32*>(B.foot + ix);
-            __builtin_amdgcn_global_load_lds(fw, &s_pfw[wvs][NW][0], 4, 0, 0);
-            __builtin_amdgcn_global_load_lds(fw + 1, &s_pfw[wvs][NW + 1][0], 4, 0, 0);
-            __builtin_amdgcn_global_load_lds(B.act + ix, &s_pfa[wvs][0], 1, 0, 0);
-            (void)k;
         }
     };
     if constexpr (PFR) pf_issue(0);
-    if constexpr (PFD) {
-        const u32 p0 = threadIdx.x, p1 = 256u + threadIdx.x;
-        pf_rel = pf_rel_of(0, p0 < wn ? (u32)B.word[win + p0] : 0u, pf_live);
-        pf_word = (wt > 1 && p1 < wn) ? (u32)B.word[win + p1] : 0u;
-        pf_issue(0);
-    }
     for (int wk = 0; wk < (int)wt; ++wk) {
         u64 rel;
         bool live;
@@ -792,29 +769,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             pf_a = (int)pf_act;
             pf_f = pf_foot;
             if (wk + 1 < (int)wt) pf_issue(wk + 1);
-        } else if constexpr (PFD) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this tile's image has landed
-            const int ln = me;
-#pragma unroll
-            for (int i = 0; i < S; ++i) w[i] = (u64)s_pfw[wv][2 * i][ln] | ((u64)s_pfw[wv][2 * i + 1][ln] << 32);
-#pragma unroll
-            for (int q = 0; q < K; ++q) m[q] = s_pfw[wv][2 * S + q][ln];
-            pf_f = (u64)s_pfw[wv][NW][ln] | ((u64)s_pfw[wv][NW + 1][ln] << 32);
-            pf_a = (int)s_pfa[wv][ln];
-            if (!live) {
-#pragma unroll
-                for (int i = 0; i < S; ++i) w[i] = 0;
-#pragma unroll
-                for (int q = 0; q < K; ++q) m[q] = 0;
-                pf_a = 255;
-                pf_f = 0;
-            }
-            if (wk + 1 < (int)wt) {  // the next tile: its position was loaded a tile ago
-                pf_rel = pf_rel_of(wk + 1, pf_word, pf_live);
-                const u32 p2 = (u32)(wk + 2) * 256u + threadIdx.x;
-                pf_word = (wk + 2 < (int)wt && p2 < wn) ? (u32)B.word[win + p2] : 0u;
-                pf_issue(wk + 1);
-            }
         } else if (live) {
             load_state<S, K>(rec, w, m);
         } else {
@@ -1815,11 +1769,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 1>));
-        } else if (expand_variant() == 13 && SORTED && B.word) {  // presorted + next-state LDS-DMA
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 2>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 2>));
         } else if (expand_variant() >= 18 && expand_variant() <= 19 && SORTED && B.word) {
             // presorted, 6 probes in flight, the parent's mixes recomputed per lane
             // instead of held (fewer VGPRs): 6 (18) or 5 (19) waves/SIMD
