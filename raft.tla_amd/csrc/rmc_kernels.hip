@@ -610,8 +610,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 //   level's records in B.rep (gathered from every rank); every rank expands
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
-          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
-          int PF = 0>
+          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -625,13 +624,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // so the kernel carries no sort: no LDS bins, scan or block barriers
     static_assert(!PRESORT || (SORT && !REP), "presorted windows: the sorted kernels");
     constexpr bool INSORT = SORT && !PRESORT;
-    // PF: the next tile's state (and its lane + footprint) is loaded into
-    // registers while this one's lanes are walked (presorted windows: its
-    // position is one load away).  (An LDS-DMA form, global_load_lds into per-wave
-    // images, was written and dropped in round 4: the loop-carried position
-    // load forced a full vmcnt wait per tile, and it held as many VGPRs.)
-    static_assert(!PF || (PRESORT && DIA && !REP), "prefetch: the presorted single-GPU kernel");
-    constexpr bool PFR = PF == 1;
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
     typedef RepRec<S, K> RR;
@@ -714,40 +706,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         }
         __syncthreads();
     }
-    u64 pf_w[PFR ? S : 1], pf_foot = 0, pf_rel = 0;
-    u32 pf_m[PFR ? K : 1], pf_act = 255;
-    bool pf_live = false;
-    auto pf_rel_of = [&](int k, u32 word, bool& lv) -> u64 {
-        const u32 p = (u32)k * 256u + threadIdx.x;
-        lv = p < wn;
-        return win + (lv ? word : 0u);
-    };
-    auto pf_issue = [&](int k) {  // PF: start tile k's state on its way
-        if constexpr (PFR) {
-            const u32 p = (u32)k * 256u + threadIdx.x;
-            pf_rel = pf_rel_of(k, p < wn ? (u32)B.word[win + p] : 0u, pf_live);
-            if (pf_live) {
-                load_state<S, K>(fr + (lo + pf_rel) * (u64)FW, pf_w, pf_m);
-                pf_act = B.act[lo + pf_rel];
-                pf_foot = B.foot[lo + pf_rel];
-            } else {
-#pragma unroll
-                for (int i = 0; i < S; ++i) pf_w[i] = 0;
-#pragma unroll
-                for (int q = 0; q < K; ++q) pf_m[q] = 0;
-                pf_act = 255;
-                pf_foot = 0;
-            }
-        }
-    };
-    if constexpr (PFR) pf_issue(0);
     for (int wk = 0; wk < (int)wt; ++wk) {
         u64 rel;
         bool live;
-        if constexpr (PF) {
-            rel = pf_rel;
-            live = pf_live;
-        } else if constexpr (SORT) {
+        if constexpr (SORT) {
             const u32 p = (u32)wk * 256u + threadIdx.x;
             live = p < wn;
             if constexpr (PRESORT) rel = win + (live ? (u32)B.word[win + p] : 0u);
@@ -759,17 +721,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         u64 w[S];
         u32 m[K];
         const u32* rec = fr + (lo + rel) * (u64)FW;
-        int pf_a = 255;
-        u64 pf_f = 0;
-        if constexpr (PFR) {
-#pragma unroll
-            for (int i = 0; i < S; ++i) w[i] = pf_w[i];
-#pragma unroll
-            for (int q = 0; q < K; ++q) m[q] = pf_m[q];
-            pf_a = (int)pf_act;
-            pf_f = pf_foot;
-            if (wk + 1 < (int)wt) pf_issue(wk + 1);
-        } else if (live) {
+        if (live) {
             load_state<S, K>(rec, w, m);
         } else {
 #pragma unroll
@@ -805,10 +757,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             int act = 255;
             u64 foot = 0;
             if (on) {
-                if constexpr (PF) {
-                    act = pf_a;
-                    foot = pf_f;
-                } else if constexpr (REP) {
+                if constexpr (REP) {
                     act = (int)(rec[RR::ACT] & 0xFFu);
                     foot = (u64)rec[RR::FOOT] | ((u64)rec[RR::FOOT + 1] << 32);
                 } else {
@@ -1101,11 +1050,11 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // The single-GPU expansion kernel: the lane-superset walk over class-sorted
 // windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
 // loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, int PF = 0, bool PRE = true>
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, PF>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS>(P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1701,18 +1650,22 @@ static u64 resident_grid(const void* k) {
     return v;
 }
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 6 (default) =
-// k_expand_sort (the lane-superset walk over class-sorted windows of 16
-// tiles, commuting-diamond skipping, probe loads issued during the lane code;
-// profiles/r03/ab/), 1 = every lane of every state (k_expand with the
-// parent's mixes precomputed; also what shapes with more than 64 lanes run).
-// The variants measured and rejected in rounds 2-3 (EARLY, UPROBE, class-sorted
-// flushes, 8-tile windows, role-only classes, probes after the lane code) are
-// in git history, not in the build.
+// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 10 (default) =
+// k_expand_sort over windows of 16 tiles presorted by class (k_window_order;
+// no sort in the kernel, so a smaller block), 6 probes in flight per thread,
+// 5 waves/SIMD (242-247 ms per bench BFS vs 263-269 ms for 6,
+// profiles/r04/ab/); 6 = the round-3 kernel (windows sorted in LDS, 8 probes,
+// 4 waves); 15 = 10 with 5 probes; 18 = 6 probes at 6 waves with the parent's
+// mixes recomputed (80 VGPRs); 1 = every lane of every state (k_expand, what
+// shapes with more than 64 lanes run).  Measured and removed in round 4: 8
+// probes at 5-6 waves, 4 probes at 5-6 waves, 7 probes at 5 waves (VGPR spills
+// or fewer probes in flight), the next tile's state prefetched into registers
+// (4 waves: 260-263 ms) or by LDS-DMA.  Rounds 2-3's rejected variants are in
+// git history.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 6;
+        return e ? atoi(e) : 10;
     }();
     return v;
 }
@@ -1762,47 +1715,22 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                    a, b);
         } else if (verify) {
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
-        } else if (expand_variant() == 6 && SORTED) {
+        } else if (expand_variant() == 6 && SORTED) {  // windows sorted in LDS, 8 probes, 4 waves/SIMD
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if (expand_variant() == 12 && SORTED && B.word) {  // presorted + next-state prefetch
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 1>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0, true, 4, 1>));
-        } else if (expand_variant() >= 18 && expand_variant() <= 19 && SORTED && B.word) {
-            // presorted, 6 probes in flight, the parent's mixes recomputed per lane
-            // instead of held (fewer VGPRs): 6 (18) or 5 (19) waves/SIMD
-#define RMC_PRESORT_NP(WPE)                                                                                  \
+        } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18) && SORTED && B.word) {
+            // windows presorted by k_window_order (no sort in LDS, so a smaller block):
+            // 10 (default) 6 probes in flight per thread at 5 waves/SIMD, 15 5 probes
+            // at 5 waves, 18 6 probes at 6 waves with the parent's mixes recomputed
+#define RMC_PRESORT(BT, WPE, PRE)                                                                            \
     {                                                                                                        \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, WPE, 0, false>)); \
+        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE, PRE>)); \
         const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
         if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
-        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, WPE, 0, false>));                    \
+        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE, PRE>));                        \
     }
-            if (expand_variant() == 18) RMC_PRESORT_NP(6)
-            else RMC_PRESORT_NP(5)
-#undef RMC_PRESORT_NP
-        } else if (((expand_variant() >= 7 && expand_variant() <= 11) || (expand_variant() >= 14 && expand_variant() <= 17)) &&
-                   SORTED && B.word) {
-            // windows presorted by k_window_order (no sort in LDS): probes in flight
-            // per thread x waves/SIMD: 7 (8, 4), 8 (8, 5), 9 (8, 6), 10 (6, 5), 11 (4, 6),
-            // 14 (6, 6), 15 (5, 5), 16 (4, 5), 17 (7, 5)
-#define RMC_PRESORT(BT, WPE)                                                                                 \
-    {                                                                                                        \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE>)); \
-        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
-        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
-        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE>));                             \
-    }
-            if (expand_variant() == 7) RMC_PRESORT(kBatch, 4)
-            else if (expand_variant() == 8) RMC_PRESORT(kBatch, 5)
-            else if (expand_variant() == 9) RMC_PRESORT(kBatch, 6)
-            else if (expand_variant() == 10) RMC_PRESORT(6, 5)
-            else if (expand_variant() == 11) RMC_PRESORT(4, 6)
-            else if (expand_variant() == 14) RMC_PRESORT(6, 6)
-            else if (expand_variant() == 15) RMC_PRESORT(5, 5)
-            else if (expand_variant() == 16) RMC_PRESORT(4, 5)
-            else RMC_PRESORT(7, 5)
+            if (expand_variant() == 10) RMC_PRESORT(6, 5, true)
+            else if (expand_variant() == 15) RMC_PRESORT(5, 5, true)
+            else RMC_PRESORT(6, 6, false)
 #undef RMC_PRESORT
         } else {  // 1, and shapes with more than 64 lanes
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
