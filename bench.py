@@ -429,7 +429,8 @@ def main(argv=None):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-            "kernel": "k_expand_sort (librmc's default expansion kernel)" if not sharded
+            "kernel": ("k_expand_sort (librmc's default expansion kernel; kernel_ms_per_step brackets each "
+                       "expansion launch with HIP events, i.e. k_window_order + k_expand_sort)") if not sharded
                       else "k_expand_dist (librmc's sharded expansion kernel)",
             "kernel_ms_per_step": ks * 1e3,
             "launches_per_step": nlaunch, "alg_bytes_per_launch": b_alg / nlaunch,

@@ -999,26 +999,42 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
         if (const char* e = getenv("RMC_DIST_NCCL_BLOCKING")) D.nonblocking = atoi(e) ? 0 : 1;
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = D.nonblocking ? 0 : 1;
-        // the init call itself on a helper thread, waited for under the
-        // deadline: a non-blocking init returns at once, but the call does not
-        // promise so for every bootstrap state (a peer that never connects)
+        // The whole set-up — the init call and, on the non-blocking communicator,
+        // its completion — runs on a helper thread (on this ctx's device) that
+        // lives until it is complete (RCCL's group state of a call is the calling
+        // thread's), waited for here under the deadline: the call does not
+        // promise to return at once for every bootstrap state (a peer that never
+        // connects).  On expiry the communicator, once the call has returned it,
+        // is aborted (bounded); a call that never returns is left to the process exit.
         struct Init {
-            std::atomic<int> done{0};
-            ncclComm_t comm = nullptr;
+            std::atomic<int> done{0}, quit{0};
+            std::atomic<ncclComm_t> comm{nullptr};
             ncclResult_t r = ncclSuccess;
         };
         auto in = std::make_shared<Init>();
-        std::thread([in, world, u, rank, cfg]() mutable {
-            in->r = ncclCommInitRankConfig(&in->comm, world, u, rank, &cfg);
+        const int dev = c->cfg.device;
+        const bool nb = D.nonblocking != 0;
+        std::thread([in, world, u, rank, cfg, dev, nb]() mutable {
+            (void)hipSetDevice(dev);
+            ncclComm_t cm = nullptr;
+            ncclResult_t r = ncclCommInitRankConfig(&cm, world, u, rank, &cfg);
+            in->comm.store(cm);
+            while (nb && r == ncclInProgress && cm && !in->quit.load()) {
+                ncclResult_t a = ncclSuccess;
+                if (ncclCommGetAsyncError(cm, &a) != ncclSuccess) break;
+                r = a;
+                if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+            in->r = r;
             in->done.store(1);
         }).detach();
         const double t_init = now_s();
         while (!in->done.load()) {
             if (now_s() - t_init > D.timeout_s) {
-                // the helper still owns the call: left to the process exit
-                D.comm = nullptr;
-                D.rccl = 0;
-                const int rc = deadline_fail(c, "ncclCommInitRankConfig (the init call; it has not returned)");
+                in->quit.store(1);
+                D.comm = in->comm.load();  // aborted (bounded) by deadline_fail when the call returned it
+                const int rc = deadline_fail(c, D.comm ? "ncclCommInitRankConfig (waiting for every rank)"
+                                                       : "ncclCommInitRankConfig (the call has not returned)");
                 const std::string msg = c->err;
                 free_dist(c);
                 c->err = msg;
@@ -1026,9 +1042,10 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
             }
             std::this_thread::sleep_for(std::chrono::microseconds(200));
         }
-        D.comm = in->comm;
+        D.comm = in->comm.load();
         ncclResult_t r = in->r;
         if (r != ncclSuccess && r != ncclInProgress) {
+            if (D.comm) (void)abort_bounded(D.comm);
             D.comm = nullptr;
             free_dist(c);
             return fail(c, RMC_E_HIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));

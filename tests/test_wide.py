@@ -70,8 +70,8 @@ def test_reference_mcraft_cfg_under_a_depth_bound():
     """the reference's MCraft.cfg layout (no CONSTRAINT,
     tests/golden/models/MCunbounded) runs past the packed capacity — depth 6
     needed a 4th copy of a message (Duplicate) — to depth 8 on the wide
-    layout, level by level equal to the C oracle run with bounds no state of
-    those depths reaches."""
+    layout, level by level equal to the C oracle run with terms and counts
+    unbounded and log / bag bounds no state of those depths reaches."""
     cfgp = os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg")
     base, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, depth_bounded=True)
     assert (base.max_term, base.max_log_len, base.max_msgs, base.max_dup) == (255, 8, 16, 255)
@@ -82,7 +82,9 @@ def test_reference_mcraft_cfg_under_a_depth_bound():
         with rmc.Checker(c) as ck:
             r = ck.run()
             levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
-        ref, ln, _ = oracle_c.bfs(3, 2, 127, 4, 8, 127, threads=8, max_levels=depth, capacity=1 << 25)
+        # terms and counts unbounded (-1); Len(log) <= 3 and 8 messages never bind
+        # within 7 steps (a leader needs 5 steps before its first ClientRequest)
+        ref, ln, _ = oracle_c.bfs(3, 2, -1, 3, 8, -1, threads=8, max_levels=depth, capacity=1 << 25)
         assert (r.distinct, r.generated, r.depth, r.left_on_queue) == (ref.distinct, ref.generated, ref.depth,
                                                                       ref.left_on_queue), depth
         assert levels == ln, depth

@@ -20,8 +20,7 @@ def main():
         for name, cname, total, n in db.execute(
                 "select kernel_name, counter_name, sum(value), count(value) from counters_collection "
                 "group by kernel_name, counter_name").fetchall():
-            if "k_expand" not in name and "k_owner" not in name and "k_store" not in name \
-                    and "k_materialize" not in name:
+            if not any(k in name for k in ("k_expand", "k_window_order", "k_owner", "k_store", "k_materialize")):
                 continue
             k = out["kernels"].setdefault(name.split("(")[0], {})
             k[cname] = {"total": total, "launches": n}
