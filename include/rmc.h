@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 4
+#define RMC_ABI_VERSION 5
 
 /* Capacity of the packed encoding (DESIGN.md "Packed state"): the layout the
  * BFS kernels run on when every bound fits it. */
@@ -41,12 +41,12 @@ extern "C" {
  * capacity; an unbounded field is given the capacity itself, and a successor
  * beyond it stops the search with RMC_E_CAPACITY naming the field. */
 #define RMC_WIDE_MAX_TERM 255
-#define RMC_WIDE_MAX_LOG 8
-#define RMC_WIDE_MAX_MSGS 16
+#define RMC_WIDE_MAX_LOG 32
+#define RMC_WIDE_MAX_MSGS 64
 #define RMC_WIDE_MAX_DUP 255
 /* Sizes of the decoded state view (rmc_state_view): the wide capacity. */
-#define RMC_VIEW_LOG 8
-#define RMC_VIEW_MSGS 16
+#define RMC_VIEW_LOG 32
+#define RMC_VIEW_MSGS 64
 
 /* Error codes. */
 #define RMC_OK 0

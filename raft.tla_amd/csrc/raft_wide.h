@@ -7,13 +7,13 @@
 // shipped (terms grow at raft.tla:146-148, logs at :206-211, counts at
 // :410-412) and Smokeraft.cfg's depth-100 walks (Smokeraft.cfg:46-48).  This
 // layout is one byte per scalar field: terms and counts up to 255, logs of up
-// to 8 entries, up to 16 distinct messages, and a canonical form in which
+// to 32 entries, up to 64 distinct messages, and a canonical form in which
 // byte equality is TLA+ value equality (fields a message type does not use
 // are 0; the bag is sorted by the message bytes; unused entries and slots are
 // 0).  The search on it is the same BFS (one lane per action instance, at most
 // one successor per lane) without the packed layout's
 // incremental tricks: a lane copies its parent, applies the action, and the
-// fingerprint hashes the whole 568-byte record.  Models whose bounds fit the
+// fingerprint hashes the whole 5,080-byte record.  Models whose bounds fit the
 // packed capacity never use it.
 //
 // Compiled for the host (codec) and for gfx950 (rmc_wide.hip).
@@ -26,15 +26,15 @@ namespace rmc {
 namespace wide {
 
 constexpr int WS = 5;    // servers held (= the packed layout's)
-constexpr int LW = 8;    // log entries per server
-constexpr int KW = 16;   // distinct messages in the bag
+constexpr int LW = 32;   // log entries per server (rmc.h RMC_WIDE_MAX_LOG)
+constexpr int KW = 64;   // distinct messages in the bag (rmc.h RMC_WIDE_MAX_MSGS)
 constexpr int TMAX = 255, CMAX = 255;  // largest term / count a field holds
 constexpr uint8_t NIL = 255;           // votedFor = Nil
 
 struct WEnt {
     uint8_t term, value;
 };
-// One message record (raft.tla:443-475): 24 bytes, fields a type does not use 0.
+// One message record (raft.tla:443-475): 8 + 2 LW bytes, fields a type does not use 0.
 struct alignas(8) WMsg {
     uint8_t type, term, src, dst;  // mtype, mterm, msource, mdest
     int8_t a;    // RVQ mlastLogTerm | RVP mvoteGranted | AEQ mprevLogIndex (-1: Smokeraft.tla:35) | AEP msuccess
@@ -43,7 +43,8 @@ struct alignas(8) WMsg {
     uint8_t n;   // AEQ Len(mentries) (<= 1) | RVP Len(mlog)
     WEnt e[LW];  // AEQ mentries | RVP mlog (= log[i], raft.tla:259)
 };
-static_assert(sizeof(WMsg) == 24, "WMsg layout");
+static_assert(sizeof(WMsg) == 8 + 2 * LW && sizeof(WMsg) % 8 == 0, "WMsg layout");
+constexpr int WMWORDS = (int)(sizeof(WMsg) / 8);
 // The ten variables of raft.tla:31-74.
 struct WState {
     uint8_t ct[WS], st[WS], vf[WS], ci[WS], len[WS], vR[WS], vG[WS];
@@ -57,7 +58,10 @@ struct WState {
 constexpr int WWORDS = (int)(sizeof(WState) / 8);
 static_assert(sizeof(WState) % 8 == 0, "WState is read as u64 words");
 
-// Lane table with KW message lanes per bag family.
+// Lane table with KW message lanes per bag family; WLMASK u64
+// words hold a mask over every lane of the largest shape (S = 5).
+constexpr int WLANES_MAX = 5 + 5 + 25 + 5 + 5 * VMAX + 5 + 25 + 3 * KW;
+constexpr int WLMASK = (WLANES_MAX + 63) / 64;
 struct WLanes {
     int off[11];
     RMC_HD void init(int S) {
@@ -103,18 +107,18 @@ RMC_HD void wcopy_state(WState& d, const WState& s) {
     for (int k = 0; k < WWORDS; ++k) x[k] = y[k];
 }
 
-// Message order of the canonical bag: the record as three u64 words compared in
+// Message order of the canonical bag: the record as WMWORDS u64 words compared in
 // turn (a total order; byte equality = record equality).  Host and device sort by it.
 RMC_HD int wmsg_cmp(const WMsg& a, const WMsg& b) {
     const u64* x = reinterpret_cast<const u64*>(&a);
     const u64* y = reinterpret_cast<const u64*>(&b);
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < WMWORDS; ++k)
         if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
     return 0;
 }
 RMC_HD void wmsg_zero(WMsg& m) {
     u64* x = reinterpret_cast<u64*>(&m);
-    x[0] = x[1] = x[2] = 0;
+    for (int k = 0; k < WMWORDS; ++k) x[k] = 0;
 }
 
 RMC_HD int wquorum(const WModel& M, unsigned set) { return 2 * __builtin_popcount(set) > M.S; }  // raft.tla:81

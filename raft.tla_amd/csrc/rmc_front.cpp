@@ -901,7 +901,7 @@ static int parse_model(const char* cfg_path, const char* tla_path, const char* r
         if (flags & (RMC_FLAG_UNBOUNDED_TERM | RMC_FLAG_UNBOUNDED_LOG | RMC_FLAG_UNBOUNDED_MSGS | RMC_FLAG_UNBOUNDED_DUP))
             notes.push_back("no CONSTRAINT bounds every field: the search runs under the depth bound on the wide "
                             "layout and stops with a capacity error if a successor exceeds it (currentTerm 255, "
-                            "Len(log) 8, 16 messages, count 255)");
+                            "Len(log) 32, 64 messages, count 255)");
     }
     if (g.max_term < 0 || g.max_log_len < 0 || g.max_msgs < 0 || g.max_dup < 0)
         return fail("the model is infinite without a CONSTRAINT bounding currentTerm, Len(log), "

@@ -1062,13 +1062,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // (deferred to k_ties).  WS: the lane-superset walk over class-sorted windows
 // of 16 tiles, 4 waves/SIMD (72.1-72.7 vs 75.0-75.3 ms for 8 tiles on the
 // MCraftBench bounds); otherwise (more than 64 lanes) every lane, 5 waves/SIMD.
-template <int S, int K, int BATCH, bool WS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
+// PS: windows presorted by k_window_order at WPE waves/SIMD (RMC_SYM_VARIANT=1, A/B).
+template <int S, int K, int BATCH, bool WS, bool PS = false, int WPE = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PS ? WPE : S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
 k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (WS && Lanes<S, K>::N <= 64)
+    if constexpr (PS && WS && Lanes<S, K>::N <= 64)
+        expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16, 0, false, true>(P, PT, B, lo, hi);
+    else if constexpr (WS && Lanes<S, K>::N <= 64)
         expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16>(P, PT, B, lo, hi);
     else
         expand_body<S, K, true, BATCH, false, false, false>(P, PT, B, lo, hi);
+}
+
+// SYMMETRY expansion kernel (RMC_SYM_VARIANT, A/B): 0 (default) windows sorted
+// in LDS, 8 probes, 4 waves/SIMD; 1 windows presorted by k_window_order, 6
+// probes, 5 waves/SIMD.
+static int sym_variant() {
+    static int v = [] {
+        const char* e = getenv("RMC_SYM_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
 }
 
 // The sharded expansion: send markers in the local set, diamond skipping and
@@ -1710,7 +1724,14 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else
+            else if (sym_variant() == 1 && SORTED && B.word) {
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_sym<S, K, 6, true, true, 5>));
+                const u64 want = resident_grid(kp);
+                const u64 gs = blocks < want ? blocks : want;
+                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
+                hipLaunchKernelGGL((k_expand_sym<S, K, 6, true, true, 5>), dim3((unsigned)gs), dim3(256), 0, st, P, PT,
+                                   B, a, b);
+            } else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
         } else if (verify) {

@@ -28,9 +28,12 @@ bool wide_wanted(const rmc_config& g) {
 
 int validate_wide(const rmc_config* c, std::string* why) {
     auto bad = [&](const char* s) { *why = s; return RMC_E_INVAL; };
+    static_assert(wide::LW == RMC_WIDE_MAX_LOG && wide::KW == RMC_WIDE_MAX_MSGS && wide::TMAX == RMC_WIDE_MAX_TERM &&
+                      wide::CMAX == RMC_WIDE_MAX_DUP && RMC_VIEW_LOG >= wide::LW && RMC_VIEW_MSGS >= wide::KW,
+                  "the wide layout's capacity is rmc.h's RMC_WIDE_MAX_*");
     if (c->max_term < 1 || c->max_term > RMC_WIDE_MAX_TERM) return bad("max_term must be 1..255 (wide layout)");
-    if (c->max_log_len < 0 || c->max_log_len > RMC_WIDE_MAX_LOG) return bad("max_log_len must be 0..8 (wide layout)");
-    if (c->max_msgs < 0 || c->max_msgs > RMC_WIDE_MAX_MSGS) return bad("max_msgs must be 0..16 (wide layout)");
+    if (c->max_log_len < 0 || c->max_log_len > RMC_WIDE_MAX_LOG) return bad("max_log_len must be 0..32 (wide layout)");
+    if (c->max_msgs < 0 || c->max_msgs > RMC_WIDE_MAX_MSGS) return bad("max_msgs must be 0..64 (wide layout)");
     if (c->max_dup < 1 || c->max_dup > RMC_WIDE_MAX_DUP) return bad("max_dup must be 1..255 (wide layout)");
     if (c->flags & (RMC_FLAG_SYMMETRY | RMC_FLAG_VERIFY_STATES | RMC_FLAG_SPILL))
         return bad("the wide layout (bounds beyond the packed capacity) supports no SYMMETRY, verification or spill");

@@ -2,7 +2,7 @@
 // the successor listing and the random walks of models whose fields outgrow
 // the packed layout (MCraft.cfg as shipped under a depth bound, Smokeraft's
 // unbounded depth-100 walks).  One thread per state or behaviour; each lane
-// materialises its successor (568 bytes, private memory), the fingerprint
+// materialises its successor (5,080 bytes, private memory), the fingerprint
 // hashes the whole canonical record, and new states are inserted into the
 // same kind of open-addressing HBM set as the packed kernels use.
 #include <hip/hip_runtime.h>
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
         if (record) wcopy_state(rec[0], s);
         int v = wcheck_invariants(M, s);
         if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 44) | ((u64)(v - 1) << 40) | b));
-        u64 excl[2] = {0, 0};  // mode 0: lanes whose successor left the bounds this step
+        u64 excl[WLMASK] = {};  // mode 0: lanes whose successor left the bounds this step
         for (int dd = 2; dd <= depth && !v;) {
             int pick = -1;
             if (mode == 2) {
@@ -187,7 +187,9 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
                 }
             }
             if (pick < 0) {
-                if (excl[0] | excl[1]) ++trunc;  // mode 0: every enabled successor leaves the bounds
+                u64 any = 0;
+                for (int q = 0; q < WLMASK; ++q) any |= excl[q];
+                if (any) ++trunc;  // mode 0: every enabled successor leaves the bounds
                 else ++dead;
                 break;
             }
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
                 break;
             }
             wcopy_state(s, t);
-            excl[0] = excl[1] = 0;
+            for (int q = 0; q < WLMASK; ++q) excl[q] = 0;
             ++steps;
             if (record) wcopy_state(rec[dd - 1], s);
             v = wcheck_invariants(M, s);

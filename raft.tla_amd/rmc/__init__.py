@@ -17,8 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
 
 MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8  # the packed layout's capacity
-WIDE_MAX_TERM, WIDE_MAX_LOG, WIDE_MAX_MSGS, WIDE_MAX_DUP = 255, 8, 16, 255  # the wide layout's
-VIEW_LOG, VIEW_MSGS = 8, 16  # rmc_state_view sizes (RMC_VIEW_LOG, RMC_VIEW_MSGS)
+WIDE_MAX_TERM, WIDE_MAX_LOG, WIDE_MAX_MSGS, WIDE_MAX_DUP = 255, 32, 64, 255  # the wide layout's
+VIEW_LOG, VIEW_MSGS = 32, 64  # rmc_state_view sizes (RMC_VIEW_LOG, RMC_VIEW_MSGS)
 SIM_WITHIN_CAPACITY, SIM_TRUNCATE, SIM_TLC = 0, 1, 2
 FLAG_SYMMETRY, FLAG_CHECK_DEADLOCK, FLAG_BUG_QUORUM, FLAG_VERIFY_STATES, FLAG_SPILL = 1, 2, 4, 8, 16
 INV_TYPEOK, INV_ONE_LEADER, INV_LOG_MATCHING, INV_MESSAGES = 1, 2, 4, 8

@@ -50,7 +50,7 @@ def test_version_and_state_bytes():
 def test_create_validates_config():
     lib = rmc.native()
     ctx = C.c_void_p()
-    bad = rmc.make_config(max_log_len=9)  # beyond the wide layout's 8 entries too
+    bad = rmc.make_config(max_log_len=33)  # beyond the wide layout's 32 entries too
     assert lib.rmc_create(C.byref(bad), C.byref(ctx)) == -22
     bad = rmc.make_config(max_log_len=4, symmetry=True)  # the wide layout has no SYMMETRY
     assert lib.rmc_create(C.byref(bad), C.byref(ctx)) == -22

@@ -239,7 +239,7 @@ def test_simulation_models():
     c, sc, _ = load(os.path.join(SPECS, "MCraftSmoke.cfg"), builtin_raft=True, simulate=True)
     # its CONSTRAINT is the run budget only (Smokeraft.cfg:46): no field is bounded,
     # so the walks run on the wide layout (its capacity)
-    assert (sc.smoke_k, sc.smoke_nat, c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (2, 2, 255, 8, 16, 255)
+    assert (sc.smoke_k, sc.smoke_nat, c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (2, 2, 255, 32, 64, 255)
 
 
 def test_simulation_refuses_a_different_smokeinit(tmp_path):
@@ -260,7 +260,7 @@ def test_reference_models_in_place():
     # under a depth bound (TLC -depth) it is accepted at the wide layout's capacity
     c, _, info = load("/root/reference/MCraft.cfg", depth_bounded=True)
     unb = rmc.FLAG_UNBOUNDED_TERM | rmc.FLAG_UNBOUNDED_LOG | rmc.FLAG_UNBOUNDED_MSGS | rmc.FLAG_UNBOUNDED_DUP
-    assert (c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (3, 2, 255, 8, 16, 255)
+    assert (c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (3, 2, 255, 32, 64, 255)
     assert (c.flags & unb) == unb and c.invariants == rmc.INV_TYPEOK
     assert "/root/reference/raft.tla verified" in info and "depth bound" in info
     c, sc, info = load("/root/reference/Smokeraft.cfg", simulate=True)
@@ -312,7 +312,7 @@ def test_unconstrained_model_needs_a_depth_bound():
         load(cfgp, builtin_raft=True)
     c, _, info = load(cfgp, builtin_raft=True, depth_bounded=True)
     unb = rmc.FLAG_UNBOUNDED_TERM | rmc.FLAG_UNBOUNDED_LOG | rmc.FLAG_UNBOUNDED_MSGS | rmc.FLAG_UNBOUNDED_DUP
-    assert (c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (255, 8, 16, 255) and (c.flags & unb) == unb
+    assert (c.max_term, c.max_log_len, c.max_msgs, c.max_dup) == (255, 32, 64, 255) and (c.flags & unb) == unb
     assert "depth bound" in info
     # a bounded model is unaffected by the option
     c2, _, _ = load(os.path.join(SPECS, "MCraftBounded.cfg"), builtin_raft=True, depth_bounded=True)
