@@ -1738,10 +1738,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
         } else if (expand_variant() == 6 && SORTED) {  // windows sorted in LDS, 8 probes, 4 waves/SIMD
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18) && SORTED && B.word) {
+        } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18 || expand_variant() == 19) &&
+                   SORTED && B.word) {
             // windows presorted by k_window_order (no sort in LDS, so a smaller block):
             // 10 (default) 6 probes in flight per thread at 5 waves/SIMD, 15 5 probes
-            // at 5 waves, 18 6 probes at 6 waves with the parent's mixes recomputed
+            // at 5 waves, 18 (19) 6 (5) probes at 6 waves with the parent's mixes recomputed
 #define RMC_PRESORT(BT, WPE, PRE)                                                                            \
     {                                                                                                        \
         const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE, PRE>)); \
@@ -1751,7 +1752,8 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     }
             if (expand_variant() == 10) RMC_PRESORT(6, 5, true)
             else if (expand_variant() == 15) RMC_PRESORT(5, 5, true)
-            else RMC_PRESORT(6, 6, false)
+            else if (expand_variant() == 18) RMC_PRESORT(6, 6, false)
+            else RMC_PRESORT(5, 6, false)
 #undef RMC_PRESORT
         } else {  // 1, and shapes with more than 64 lanes
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
