@@ -145,11 +145,14 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
     for (u64 b = (u64)blockIdx.x * 64ull + threadIdx.x; b < n_beh; b += (u64)gridDim.x * 64ull) {
         if (rec_beh >= 0 && (i64)b != rec_beh) continue;
         u64 rs = mix64(seed ^ (b * 0xD1B54A32D192ED03ull));
-        WState s, t;
-        wcopy_state(s, inits[w_rand(rs) % n_init]);
+        // two records used in turn (the successor becomes the current state by
+        // swapping the roles, not by a 5-KB copy)
+        WState buf[2];
+        int cur = 0;
+        wcopy_state(buf[0], inits[w_rand(rs) % n_init]);
         const bool record = (i64)b == rec_beh;
-        if (record) wcopy_state(rec[0], s);
-        int v = wcheck_invariants(M, s);
+        if (record) wcopy_state(rec[0], buf[cur]);
+        int v = wcheck_invariants(M, buf[cur]);
         if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 44) | ((u64)(v - 1) << 40) | b));
         u64 excl[WLMASK] = {};  // mode 0: lanes whose successor left the bounds this step
         for (int dd = 2; dd <= depth && !v;) {
@@ -159,7 +162,7 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
                 u32 na = 0;
                 int fam_on[3] = {0, 0, 0};
                 for (int lane = 0; lane < nl; ++lane) {
-                    if (wlane(M, s, lane, nullptr) == W_OFF) continue;
+                    if (wlane(M, buf[cur], lane, nullptr) == W_OFF) continue;
                     if (lane < o7) ++na;
                     else fam_on[lane < o8 ? 0 : lane < o9 ? 1 : 2] += 1;
                 }
@@ -167,21 +170,21 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
                 if (na) {
                     u32 a = (u32)(w_rand(rs) % na);
                     for (int lane = 0; lane < o7 && pick < 0; ++lane)
-                        if (wlane(M, s, lane, nullptr) != W_OFF && a-- == 0) pick = lane;
+                        if (wlane(M, buf[cur], lane, nullptr) != W_OFF && a-- == 0) pick = lane;
                     for (int f = 0; f < 3 && pick < 0; ++f) {
                         if (!fam_on[f]) continue;
                         if (a-- != 0) continue;
                         const int lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
                         u32 k = (u32)(w_rand(rs) % (u64)fam_on[f]);
                         for (int lane = lo; lane < hi && pick < 0; ++lane)
-                            if (wlane(M, s, lane, nullptr) != W_OFF && k-- == 0) pick = lane;
+                            if (wlane(M, buf[cur], lane, nullptr) != W_OFF && k-- == 0) pick = lane;
                     }
                 }
             } else {
                 u32 cnt = 0;
                 for (int lane = 0; lane < nl; ++lane) {  // reservoir: uniform over the enabled lanes
                     if ((excl[lane >> 6] >> (lane & 63)) & 1ull) continue;
-                    if (wlane(M, s, lane, nullptr) == W_OFF) continue;
+                    if (wlane(M, buf[cur], lane, nullptr) == W_OFF) continue;
                     ++cnt;
                     if (w_rand(rs) % cnt == 0) pick = lane;
                 }
@@ -193,8 +196,8 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
                 else ++dead;
                 break;
             }
-            const int r = wlane(M, s, pick, &t);
-            if (r != W_ON || !win_model(M, t)) {
+            const int r = wlane(M, buf[cur], pick, &buf[cur ^ 1]);
+            if (r != W_ON || !win_model(M, buf[cur ^ 1])) {
                 if (mode == 0) {  // exclude it and draw again (a lane whose successor overflows too)
                     excl[pick >> 6] |= 1ull << (pick & 63);
                     continue;
@@ -202,11 +205,11 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
                 ++trunc;
                 break;
             }
-            wcopy_state(s, t);
+            cur ^= 1;
             for (int q = 0; q < WLMASK; ++q) excl[q] = 0;
             ++steps;
-            if (record) wcopy_state(rec[dd - 1], s);
-            v = wcheck_invariants(M, s);
+            if (record) wcopy_state(rec[dd - 1], buf[cur]);
+            v = wcheck_invariants(M, buf[cur]);
             if (v)
                 atomicMin((unsigned long long*)&out->viol, (unsigned long long)(((u64)dd << 44) | ((u64)(v - 1) << 40) | b));
             ++dd;

@@ -56,7 +56,7 @@ def test_wide_layout_matches_oracle_levels(name, force_wide):
 def test_wide_layout_violation_and_trace(name, force_wide):
     g = GOLDEN[name]
     p = g["params"]
-    with rmc.Checker(cfg_from(p)) as ck:
+    with rmc.Checker(cfg_from(p, capacity=int(g["distinct"] * 1.25) + (1 << 16))) as ck:  # 5-KB records
         r = ck.run()
         trace = ck.trace()
     assert r.violated_inv == g["violated_inv"] and r.violation_depth == g["violation_depth"]
