@@ -8,7 +8,7 @@ P=${OUT:-gpurun_out/pmc}
 mkdir -p $P
 B="--steps 1 --warmup 0 --no-cpu --no-probe-ceiling ${BENCH_ARGS}"
 for v in $ENVS; do export $v; done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $P/kt -o kt -- python3 bench.py $B > $P/kt.json 2> $P/kt.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py $B > $P/kt.json 2> $P/kt.err || exit 1
 find $P/kt -name "*.db" -delete
 pass() {  # name counters...
   local name=$1; shift
