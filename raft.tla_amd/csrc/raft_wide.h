@@ -191,15 +191,16 @@ RMC_HD void wbag_remove(WState& s, const WMsg& m) {
 // Lane `lane` on s (raft.tla:136-417, one action instance): W_OFF when the
 // instance is not enabled, W_ON when it is (*t = the successor, if t is
 // given), else the field its successor overflows (W_TERM .. W_DUP; *t is not
-// written).  t == nullptr only evaluates the guard (the simulation's draw).
-RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
+// written).  t == nullptr only evaluates the guard (the simulation's draw);
+// pre: *t already holds a copy of s (a wave that copied it cooperatively).
+RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre = false) {
     const int S = M.S;
     const int f = M.L.family(lane), x = lane - M.L.off[f];
     switch (f) {
     case 0: {  // Restart(i) :136-143 — always enabled
         const int i = x;
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         t->st[i] = FOLLOWER;
         t->vR[i] = 0;
         t->vG[i] = 0;
@@ -215,7 +216,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         if (s.st[i] != FOLLOWER && s.st[i] != CANDIDATE) return W_OFF;
         if (s.ct[i] >= TMAX) return W_TERM;
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         t->st[i] = CANDIDATE;
         t->ct[i] = (uint8_t)(s.ct[i] + 1);
         t->vf[i] = NIL;
@@ -236,7 +237,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         m.dst = (uint8_t)j;
         const int fit = wbag_fits(s, m);
         if (fit != W_ON || !t) return fit;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         return wbag_add(*t, m);
     }
     case 3: {  // BecomeLeader(i) :195-203
@@ -244,7 +245,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         if (s.st[i] != CANDIDATE) return W_OFF;
         if (M.bug_quorum ? s.vG[i] == 0 : !wquorum(M, s.vG[i])) return W_OFF;
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         t->st[i] = LEADER;
         for (int j = 0; j < S; ++j) {
             t->ni[i][j] = (uint8_t)(s.len[i] + 1);
@@ -257,7 +258,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         if (v >= M.V || s.st[i] != LEADER) return W_OFF;
         if (s.len[i] >= LW) return W_LOG;
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         t->log[i][s.len[i]].term = s.ct[i];
         t->log[i][s.len[i]].value = (uint8_t)v;
         t->len[i] = (uint8_t)(s.len[i] + 1);
@@ -274,7 +275,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
                 if (s.mi[i][q] >= idx) agree |= 1u << q;
             if (wquorum(M, agree)) best = idx;  // Max(agreeIndexes)
         }
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         if (best > 0 && s.log[i][best - 1].term == s.ct[i]) t->ci[i] = (uint8_t)best;
         return W_ON;
     }
@@ -299,7 +300,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         m.dst = (uint8_t)j;
         const int fit = wbag_fits(s, m);
         if (fit != W_ON || !t) return fit;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         return wbag_add(*t, m);
     }
     case 7: {  // Receive(m) :388-403 for bag slot x
@@ -308,7 +309,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         const int i = m.dst, j = m.src, ct = s.ct[i];
         if (m.term > ct) {  // UpdateTerm :373-379 — m stays
             if (!t) return W_ON;
-            wcopy_state(*t, s);
+            if (!pre) wcopy_state(*t, s);
             t->ct[i] = m.term;
             t->st[i] = FOLLOWER;
             t->vf[i] = NIL;
@@ -330,7 +331,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
             const int fit = wbag_fits(s, r);  // Reply :102-103: add the response, then remove the request
             if (fit != W_ON || !t) return fit;
             const WMsg q = m;
-            wcopy_state(*t, s);
+            if (!pre) wcopy_state(*t, s);
             if (grant) t->vf[i] = (uint8_t)j;
             wbag_add(*t, r);
             wbag_remove(*t, q);
@@ -338,7 +339,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         }
         if (m.type == RVP) {
             if (!t) return W_ON;
-            wcopy_state(*t, s);
+            if (!pre) wcopy_state(*t, s);
             if (m.term == ct) {  // HandleRequestVoteResponse :267-279
                 t->vR[i] |= (uint8_t)(1u << j);
                 if (m.a) t->vG[i] |= (uint8_t)(1u << j);
@@ -359,14 +360,14 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
                 const int fit = wbag_fits(s, r);
                 if (fit != W_ON || !t) return fit;
                 const WMsg q = m;
-                wcopy_state(*t, s);
+                if (!pre) wcopy_state(*t, s);
                 wbag_add(*t, r);
                 wbag_remove(*t, q);
                 return W_ON;
             }
             if (s.st[i] == CANDIDATE) {  // ReturnToFollowerState :295-299 — m stays
                 if (!t) return W_ON;
-                wcopy_state(*t, s);
+                if (!pre) wcopy_state(*t, s);
                 t->st[i] = FOLLOWER;
                 return W_ON;
             }
@@ -381,14 +382,14 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
                 const int fit = wbag_fits(s, r);
                 if (fit != W_ON || !t) return fit;
                 const WMsg q = m;
-                wcopy_state(*t, s);
+                if (!pre) wcopy_state(*t, s);
                 wbag_add(*t, r);
                 wbag_remove(*t, q);
                 return W_ON;
             }
             if (len >= index) {  // ConflictAppendEntriesRequest :319-325 — drops the LAST entry, m stays
                 if (!t) return W_ON;
-                wcopy_state(*t, s);
+                if (!pre) wcopy_state(*t, s);
                 t->len[i] = (uint8_t)(len - 1);
                 t->log[i][len - 1].term = 0;
                 t->log[i][len - 1].value = 0;
@@ -397,7 +398,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
             if (len == pidx) {  // NoConflictAppendEntriesRequest :327-331 — m stays
                 if (len >= LW) return W_LOG;
                 if (!t) return W_ON;
-                wcopy_state(*t, s);
+                if (!pre) wcopy_state(*t, s);
                 t->log[i][len] = m.e[0];
                 t->len[i] = (uint8_t)(len + 1);
                 return W_ON;
@@ -406,7 +407,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         }
         // AEP
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         if (m.term == ct) {  // HandleAppendEntriesResponse :360-370 (no Leader guard)
             if (m.a) {
                 t->ni[i][j] = (uint8_t)(m.b + 1);
@@ -423,14 +424,14 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t) {
         if (x >= s.nmsg) return W_OFF;
         if (s.cnt[x] >= CMAX) return W_DUP;
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         t->cnt[x] += 1;
         return W_ON;
     }
     default: {  // DropMessage(m) :415-417
         if (x >= s.nmsg) return W_OFF;
         if (!t) return W_ON;
-        wcopy_state(*t, s);
+        if (!pre) wcopy_state(*t, s);
         wbag_remove_at(*t, x);
         return W_ON;
     }

@@ -220,6 +220,136 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
     if (dead) atomicAdd((unsigned long long*)&out->deadlocked, (unsigned long long)dead);
 }
 
+// The same walks, one WAVE per behaviour (RMC_WSIM=1, the default): the two
+// 5-KB records live in LDS instead of one lane's private memory, the 64 lanes
+// evaluate the action guards in parallel (a ballot per 64 lanes of the lane
+// table), copy the record together, and lane 0 applies the drawn action and
+// checks the invariants.  The draws are the thread kernel's (the same random
+// stream per behaviour), so both give the same behaviours.
+constexpr int WSIM_WAVES = 4;  // behaviours per 256-thread block (2 x 5,080 B of LDS each)
+__global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M, const WState* inits, u64 n_init,
+                                                                u64 n_beh, int depth, u64 seed, int mode,
+                                                                SimCounters* out, i64 rec_beh, WState* rec) {
+    __shared__ WState s_buf[WSIM_WAVES][2];
+    __shared__ int s_res[WSIM_WAVES];
+    const int wv = (int)(threadIdx.x >> 6), ln = (int)(threadIdx.x & 63);
+    u64 steps = 0, trunc = 0, dead = 0;  // lane 0's tallies
+    const int nl = M.L.off[10];
+    const int o7 = M.L.off[7], o8 = M.L.off[8], o9 = M.L.off[9];
+    constexpr int NC = (WLANES_MAX + 63) / 64;  // 64-lane chunks of the lane table
+    auto copy = [&](WState& d, const WState& s) {  // the whole wave, 8 bytes a lane at a time
+        u64* x = reinterpret_cast<u64*>(&d);
+        const u64* y = reinterpret_cast<const u64*>(&s);
+        for (int k = ln; k < WWORDS; k += 64) x[k] = y[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (u64 b = (u64)blockIdx.x * WSIM_WAVES + wv; b < n_beh; b += (u64)gridDim.x * WSIM_WAVES) {  // wave-uniform
+        if (rec_beh >= 0 && (i64)b != rec_beh) continue;
+        u64 rs = mix64(seed ^ (b * 0xD1B54A32D192ED03ull));  // every lane: the same stream
+        int cur = 0;
+        copy(s_buf[wv][0], inits[w_rand(rs) % n_init]);
+        const bool record = (i64)b == rec_beh;
+        if (record && ln == 0) wcopy_state(rec[0], s_buf[wv][0]);
+        int v = ln == 0 ? wcheck_invariants(M, s_buf[wv][0]) : 0;
+        v = __shfl(v, 0);
+        if (v && ln == 0)
+            atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 44) | ((u64)(v - 1) << 40) | b));
+        u64 excl[WLMASK] = {};  // mode 0: lanes whose successor left the bounds this step (uniform)
+        for (int dd = 2; dd <= depth && !v;) {
+            const WState& s = s_buf[wv][cur];
+            // guards in parallel: en[c] bit l = lane 64 c + l enabled (wave-uniform masks)
+            u64 en[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int lane = 64 * c + ln;
+                const bool on = lane < nl && wlane(M, s, lane, nullptr) != W_OFF;
+                en[c] = __ballot(on);
+            }
+            int pick = -1;
+            if (mode == 2) {  // TLC's draw, exactly as k_wsimulate
+                u32 na = 0;
+                int fam_on[3] = {0, 0, 0};
+                for (int c = 0; c < NC; ++c) {
+                    for (u64 mm = en[c]; mm; mm &= mm - 1) {
+                        const int lane = 64 * c + __builtin_ctzll(mm);
+                        if (lane < o7) ++na;
+                        else fam_on[lane < o8 ? 0 : lane < o9 ? 1 : 2] += 1;
+                    }
+                }
+                na += (u32)(fam_on[0] > 0) + (u32)(fam_on[1] > 0) + (u32)(fam_on[2] > 0);
+                if (na) {
+                    u32 a = (u32)(w_rand(rs) % na);
+                    for (int c = 0; c < NC && pick < 0; ++c)
+                        for (u64 mm = en[c]; mm && pick < 0; mm &= mm - 1) {
+                            const int lane = 64 * c + __builtin_ctzll(mm);
+                            if (lane < o7 && a-- == 0) pick = lane;
+                        }
+                    for (int f = 0; f < 3 && pick < 0; ++f) {
+                        if (!fam_on[f]) continue;
+                        if (a-- != 0) continue;
+                        const int lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
+                        u32 k = (u32)(w_rand(rs) % (u64)fam_on[f]);
+                        for (int c = 0; c < NC && pick < 0; ++c)
+                            for (u64 mm = en[c]; mm && pick < 0; mm &= mm - 1) {
+                                const int lane = 64 * c + __builtin_ctzll(mm);
+                                if (lane >= lo && lane < hi && k-- == 0) pick = lane;
+                            }
+                    }
+                }
+            } else {  // reservoir over the enabled lanes in lane order (k_wsimulate's draws)
+                u32 cnt = 0;
+                for (int c = 0; c < NC; ++c)
+                    for (u64 mm = en[c]; mm; mm &= mm - 1) {
+                        const int lane = 64 * c + __builtin_ctzll(mm);
+                        if ((excl[lane >> 6] >> (lane & 63)) & 1ull) continue;
+                        ++cnt;
+                        if (w_rand(rs) % cnt == 0) pick = lane;
+                    }
+            }
+            if (pick < 0) {
+                u64 any = 0;
+                for (int q = 0; q < WLMASK; ++q) any |= excl[q];
+                if (any) ++trunc;
+                else ++dead;
+                break;
+            }
+            WState& t = s_buf[wv][cur ^ 1];
+            copy(t, s);
+            if (ln == 0) {
+                const int r = wlane(M, s, pick, &t, true);
+                s_res[wv] = (r != W_ON || !win_model(M, t)) ? 1 : 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (s_res[wv]) {
+                if (mode == 0) {
+                    excl[pick >> 6] |= 1ull << (pick & 63);
+                    continue;
+                }
+                ++trunc;
+                break;
+            }
+            cur ^= 1;
+            for (int q = 0; q < WLMASK; ++q) excl[q] = 0;
+            ++steps;
+            if (record && ln == 0) wcopy_state(rec[dd - 1], t);
+            v = ln == 0 ? wcheck_invariants(M, t) : 0;
+            v = __shfl(v, 0);
+            if (v && ln == 0)
+                atomicMin((unsigned long long*)&out->viol, (unsigned long long)(((u64)dd << 44) | ((u64)(v - 1) << 40) | b));
+            ++dd;
+        }
+    }
+    if (ln == 0) {
+        atomicAdd((unsigned long long*)&out->steps, (unsigned long long)steps);
+        if (trunc) atomicAdd((unsigned long long*)&out->truncated, (unsigned long long)trunc);
+        if (dead) atomicAdd((unsigned long long*)&out->deadlocked, (unsigned long long)dead);
+    }
+}
+
 // ---- host launchers ---------------------------------------------------------------
 static unsigned grid_for(u64 n, u64 threads, u64 maxg) {
     const u64 b = (n + threads - 1) / threads;
@@ -244,8 +374,16 @@ hipError_t launch_wlist(const WModel& M, const WState* in, u64 n, WSucc* out, u6
 }
 hipError_t launch_wsimulate(const WModel& M, const WState* inits, u64 n_init, u64 n_beh, int depth, u64 seed, int mode,
                             SimCounters* out, i64 rec_beh, WState* rec, hipStream_t st) {
-    hipLaunchKernelGGL(k_wsimulate, dim3(grid_for(n_beh, 64, 16384)), dim3(64), 0, st, M, inits, n_init, n_beh, depth,
-                       seed, mode, out, rec_beh, rec);
+    static const int wave = [] {  // RMC_WSIM=0: one thread per behaviour (k_wsimulate, A/B)
+        const char* e = getenv("RMC_WSIM");
+        return e ? atoi(e) : 1;
+    }();
+    if (wave)
+        hipLaunchKernelGGL(k_wsimulate_w, dim3(grid_for(n_beh, WSIM_WAVES, 8192)), dim3(64 * WSIM_WAVES), 0, st, M,
+                           inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec);
+    else
+        hipLaunchKernelGGL(k_wsimulate, dim3(grid_for(n_beh, 64, 16384)), dim3(64), 0, st, M, inits, n_init, n_beh,
+                           depth, seed, mode, out, rec_beh, rec);
     return hipGetLastError();
 }
 
