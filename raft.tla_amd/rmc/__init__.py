@@ -15,6 +15,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librmc.so")
+if os.environ.get("RMC_LIB"):  # another in-tree build of librmc (same-box A/B of two builds)
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", os.environ["RMC_LIB"])
 
 MAX_SERVERS, MAX_LOG, MAX_MSGS = 5, 3, 8  # the packed layout's capacity
 WIDE_MAX_TERM, WIDE_MAX_LOG, WIDE_MAX_MSGS, WIDE_MAX_DUP = 255, 32, 64, 255  # the wide layout's
