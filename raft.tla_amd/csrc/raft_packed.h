@@ -114,22 +114,6 @@ RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59) ^ RMC_
 // table stays uniformly loaded.
 RMC_HD u32 owner_of(u64 key, u32 world) { return (u32)(((key >> 32) * (u64)world) >> 32); }
 
-// ---- stored-state record (the state store, B.store) ------------------------------
-// One record per stored state: the packed state (2S + K words), the footprint
-// of the lane that discovered it (2 words, commuting diamonds) and that lane
-// (1 word, low byte), padded to 64 B when it fits — one HBM granule holds
-// everything the expansion kernel reads of a frontier state (three scattered
-// loads before round 4: the state, B.act and B.foot) — else to a multiple of 32 B.
-RMC_HD constexpr int store_words(int S, int K) {
-    return 2 * S + K + 3 <= 16 ? 16 : (2 * S + K + 3 + 7) / 8 * 8;
-}
-template <int S, int K>
-struct SRec {
-    static constexpr int NW = 2 * S + K;      // packed-state words
-    static constexpr int FOOT = NW, ACT = NW + 2;
-    static constexpr int SW = store_words(S, K);  // words per record
-};
-
 // ---- model parameters (runtime part) --------------------------------------------
 struct Params {
     int V, max_term, max_log, max_msgs, max_dup, bug_quorum, inv_mask, symmetry;

@@ -63,7 +63,6 @@ void fill_params(rmc_ctx* c) {
     c->sh.sym = (g.flags & RMC_FLAG_SYMMETRY) != 0;
     c->sh.verify = (g.flags & RMC_FLAG_VERIFY_STATES) != 0;
     c->NW = 2 * c->sh.S + c->sh.K;
-    c->SW = rmc::store_words(c->sh.S, c->sh.K);
     Params& P = c->P;
     P.V = g.n_values;
     P.max_term = g.max_term;
@@ -319,10 +318,11 @@ int read_counters(rmc_ctx* c) {
 void spill_rebase(rmc_ctx* c, u64 base) {
     SpillState& X = c->spill;
     X.base = base;
-    const uintptr_t sw = (uintptr_t)c->SW;
-    c->B.store = (u32*)((uintptr_t)X.store - (uintptr_t)base * sw * 4);
+    const uintptr_t nw = (uintptr_t)c->NW;
+    c->B.store = (u32*)((uintptr_t)X.store - (uintptr_t)base * nw * 4);
     c->B.parent = (u64*)((uintptr_t)X.parent - (uintptr_t)base * 8);
     c->B.act = (uint8_t*)((uintptr_t)X.act - (uintptr_t)base);
+    c->B.foot = (u64*)((uintptr_t)X.foot - (uintptr_t)base * 8);
     c->B.cls = (uint8_t*)((uintptr_t)X.cls - (uintptr_t)base);
     c->B.cap = base + X.win;
 }
@@ -373,7 +373,7 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
     const u64 n = a - X.base;
     if (!n) return 0;
     const auto t0 = std::chrono::steady_clock::now();
-    const u64 W = (u64)c->SW * 4;  // store records
+    const u64 W = (u64)c->NW * 4;
     u64* hp = X.h_parent + X.base;
     uint8_t* ha = X.h_act + X.base;
     if (X.ahead.joinable()) X.ahead.join();
@@ -394,6 +394,7 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
                                  hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.parent + off, X.parent + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.act + off, X.act + n + off, k, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipMemcpyAsync(X.foot + off, X.foot + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipMemcpyAsync(X.cls + off, X.cls + n + off, k, hipMemcpyDeviceToDevice, c->st));
     }
     HIPCHK(c, hipStreamSynchronize(c->st));
@@ -488,7 +489,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     }
 
     // ---- capacity: state store + parents + lanes + fingerprint set (load <= 0.5)
-    const u64 per_state = (u64)c->SW * 4 + 8 + 1 + 1;  // record (state, footprint, lane), parent, lane, class
+    const u64 per_state = (u64)c->NW * 4 + 8 + 1 + 8 + 1;  // state, parent, lane, footprint, class
     const bool spill = (cfg->flags & RMC_FLAG_SPILL) != 0;
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -512,9 +513,9 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     }
     c->B.cap = win;
     c->B.tmask = slots - 1;
-    if (hipMalloc(&c->B.store, win * (u64)c->SW * 4) != hipSuccess ||
+    if (hipMalloc(&c->B.store, win * (u64)c->NW * 4) != hipSuccess ||
         hipMalloc(&c->B.parent, win * 8) != hipSuccess || hipMalloc(&c->B.act, win) != hipSuccess ||
-        hipMalloc(&c->B.cls, win) != hipSuccess ||
+        hipMalloc(&c->B.foot, win * 8) != hipSuccess || hipMalloc(&c->B.cls, win) != hipSuccess ||
         hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
         hipMalloc(&c->B.word, (1ull << 24) * 2) != hipSuccess ||  // presorted windows of one launch
         hipMalloc(&c->d_staged, (size_t)c->NW * 4 * 64) != hipSuccess) {
@@ -527,6 +528,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     c->spill.store = c->B.store;
     c->spill.parent = c->B.parent;
     c->spill.act = c->B.act;
+    c->spill.foot = c->B.foot;
     c->spill.cls = c->B.cls;
     // classes are a layout hint (any value is a valid class): zero them once so
     // recovered or never-written states sort deterministically
@@ -574,6 +576,7 @@ void rmc_destroy(rmc_ctx* c) {
     (void)hipFree(c->spill.store ? c->spill.store : c->B.store);
     (void)hipFree(c->spill.parent ? c->spill.parent : c->B.parent);
     (void)hipFree(c->spill.act ? c->spill.act : c->B.act);
+    (void)hipFree(c->spill.foot ? c->spill.foot : c->B.foot);
     (void)hipFree(c->spill.cls ? c->spill.cls : c->B.cls);
     (void)hipFree(c->B.table);
     (void)hipFree(c->B.ctr);
@@ -807,11 +810,10 @@ int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
 namespace {
 // The header embeds the ABI structs rmc_config and rmc_result, so its size is
 // written too and must match: a struct that grows changes kCkptVersion.
-constexpr uint32_t kCkptVersion = 4;  // 3: rmc_result with parked / exchange_wait_seconds; 4: store records
-                                      // (state + footprint + lane, store_words) instead of bare states
+constexpr uint32_t kCkptVersion = 3;  // 3: rmc_result with parked / exchange_wait_seconds
 struct CkptHeader {
     char magic[8];
-    uint32_t version, nw;  // nw: words per stored-state record (store_words)
+    uint32_t version, nw;
     uint32_t header_bytes, pad_;
     rmc_config cfg;
     uint64_t count, nlevels;
@@ -873,7 +875,7 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     memcpy(h.magic, kCkptMagic, 8);
     h.version = kCkptVersion;
     h.header_bytes = (uint32_t)sizeof(CkptHeader);
-    h.nw = (uint32_t)c->SW;
+    h.nw = (uint32_t)c->NW;
     h.cfg = c->cfg;
     h.count = c->level_start.back();
     h.nlevels = c->level_start.size();
@@ -892,7 +894,7 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!rc) rc = move_file(c, f, c->B.parent + base, nd * 8, true);
     if (base) put(c->spill.h_act, base);
     if (!rc) rc = move_file(c, f, c->B.act + base, nd, true);
-    if (!rc) rc = move_file(c, f, c->B.store + h.first * (u64)c->SW, (h.count - h.first) * (u64)c->SW * 4, true);
+    if (!rc) rc = move_file(c, f, c->B.store + h.first * (u64)c->NW, (h.count - h.first) * (u64)c->NW * 4, true);
     if (!rc && h.slots) rc = move_file(c, f, c->B.table, h.slots * 8, true);
     if (fclose(f) != 0 && !rc) rc = fail(c, RMC_E_IO, "checkpoint close failed");
     return rc;
@@ -922,7 +924,7 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     else if (h.shard != (c->dist.on ? (c->dist.rank | (c->dist.world << 16)) : 0))
         rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another shard layout (rank / world), or of a "
                                   "single-GPU run recovered on a sharded ctx or the reverse");
-    else if (h.nw != (uint32_t)c->SW || !same_model(h.cfg, c->cfg))
+    else if (h.nw != (uint32_t)c->NW || !same_model(h.cfg, c->cfg))
         rc = fail(c, RMC_E_INVAL, "recover: the checkpoint is of another model (constants, bounds, flags or seed)");
     else if (h.first && (!c->spill.on || h.slots != c->table_slots))
         rc = fail(c, RMC_E_INVAL, "recover: a spilled checkpoint holds the fingerprint set, not the spilled "
@@ -954,7 +956,7 @@ int rmc_recover(rmc_ctx* c, const char* path) {
         spill_rebase(c, 0);
         c->spill.faulted = std::max(c->spill.faulted, s);  // fread backs the links it writes
     }
-    const u64 SW = (u64)c->SW, W = SW * 4;  // store records
+    const u64 NW = (u64)c->NW, W = NW * 4;
     u32* dstore = c->spill.on ? c->spill.store : c->B.store;
     u64* dparent = c->spill.on ? c->spill.parent : c->B.parent;
     uint8_t* dact = c->spill.on ? c->spill.act : c->B.act;
@@ -963,8 +965,10 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     };
     HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
-    // footprints travel in the store records: the recovered frontier skips
-    // commuting diamonds like the search that wrote it
+    // footprints are not checkpointed: the recovered frontier is expanded without
+    // diamond skipping (FOOT_VALID clear), the levels after it with
+    HIPCHK(c, hipMemsetAsync(c->spill.on ? c->spill.foot : c->B.foot, 0,
+                             (c->spill.on ? c->spill.win : c->B.cap) * 8, c->st));
     HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
     if (s) get(c->spill.h_parent, s * 8);
@@ -975,7 +979,7 @@ int rmc_recover(rmc_ctx* c, const char* path) {
         // no set in the file: rehash the states below s through the free part
         // of the window (the frontier is loaded after them, at its start)
         const u64 piece = c->spill.win - (h.count - s);
-        u32* area = dstore + (h.count - s) * SW;
+        u32* area = dstore + (h.count - s) * NW;
         for (u64 p = 0; p < s && !rc; p += piece) {
             const u64 k = std::min(piece, s - p);
             rc = move_file(c, f, area, k * W, false);
@@ -1034,7 +1038,7 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
     int rc = 0;
     for (size_t q = 0; q < chain.size() && !rc; ++q) {
         if (!c->spill.on || chain[q] >= c->spill.base) {
-            HIPCHK(c, hipMemcpy(cur.data(), c->B.store + chain[q] * (u64)c->SW, NW * 4, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(cur.data(), c->B.store + chain[q] * NW, NW * 4, hipMemcpyDeviceToHost));
         } else if (q == 0) {  // Init (raft.tla:125-129), the one initial state
             rmc_state_view iv;
             init_view(c->cfg, &iv);

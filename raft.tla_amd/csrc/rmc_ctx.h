@@ -92,6 +92,7 @@ struct SpillState {
     rmc::u32* store = nullptr;  // the real device allocations
     rmc::u64* parent = nullptr;
     uint8_t* act = nullptr;
+    rmc::u64* foot = nullptr;
     uint8_t* cls = nullptr;
     rmc::u64* h_parent = nullptr;  // host, [total_cap], reserved address space,
     uint8_t* h_act = nullptr;      // pages touched as levels spill
@@ -106,7 +107,6 @@ struct rmc_ctx {
     rmc::Params P{};
     rmc::PermTable PT{};
     int NW = 0;  // 32-bit words per packed state
-    int SW = 0;  // 32-bit words per stored-state record (store_words: state, footprint, lane)
     hipStream_t st = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // bracket each level's expansion launches
     rmc::DevBufs B{};

@@ -844,7 +844,7 @@ int trace_sharded(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t
             HIPCHK(c, hipMemcpy(&a, c->B.act + idx, 1, hipMemcpyDeviceToHost));
             head[0] = 1 | ((u64)a << 8);
             memcpy(mine.data(), head, 16);
-            HIPCHK(c, hipMemcpy(mine.data() + 16, c->B.store + idx * (u64)c->SW, (u64)c->NW * 4, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(mine.data() + 16, c->B.store + idx * (u64)c->NW, (u64)c->NW * 4, hipMemcpyDeviceToHost));
         }
         if (int rc = allgather(c, mine.data(), RB, all.data())) return rc;
         const uint8_t* rec = all.data() + (u64)owner * RB;

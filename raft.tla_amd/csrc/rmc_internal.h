@@ -27,11 +27,10 @@ struct Counters {
 };
 
 struct DevBufs {
-    u32* store;      // stored-state records (SRec: packed state, footprint, lane; store_words each);
-                     // levels are contiguous ranges
+    u32* store;      // packed states, (2S + K) words each; levels are contiguous ranges
     u64* parent;     // parent index per state (~0 for initial states)
-    uint8_t* act;    // lane that produced the state (255 for initial states): the trace link
-                     // (spills, traces, checkpoints); the kernels read the record's copy
+    uint8_t* act;    // lane that produced the state (255 for initial states)
+    u64* foot;       // messages the producing lane acted on / added (make_foot; 0 = unknown)
     uint8_t* cls;    // window-sort class of each state (state_class_fine; a layout hint)
     uint16_t* word;  // presorted windows (k_window_order): the launch's window positions in class order
     u64* table;      // fingerprint set, power-of-two slots, 0 = empty

@@ -98,32 +98,6 @@ __device__ __forceinline__ void load_state(const u32* __restrict__ base, u64 (&w
     }
 }
 
-// A stored-state record (SRec, 16-byte aligned: SW is a multiple of 4) with
-// 16-byte loads: the state, its discovering lane's footprint and the lane.
-template <int S, int K>
-__device__ __forceinline__ void load_record(const u32* __restrict__ rec, u64 (&w)[S], u32 (&m)[K], u64& foot,
-                                            u32& act) {
-    typedef SRec<S, K> SR;
-    static_assert(SR::SW % 4 == 0, "records are 16-byte aligned");
-    constexpr int NQ = (SR::ACT + 1 + 3) / 4;
-    u32 v[NQ * 4];
-    const uint4* q = reinterpret_cast<const uint4*>(rec);
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-        const uint4 x = q[i];
-        v[4 * i] = x.x;
-        v[4 * i + 1] = x.y;
-        v[4 * i + 2] = x.z;
-        v[4 * i + 3] = x.w;
-    }
-#pragma unroll
-    for (int i = 0; i < S; ++i) w[i] = (u64)v[2 * i] | ((u64)v[2 * i + 1] << 32);
-#pragma unroll
-    for (int k = 0; k < K; ++k) m[k] = v[2 * S + k];
-    foot = (u64)v[SR::FOOT] | ((u64)v[SR::FOOT + 1] << 32);
-    act = v[SR::ACT];
-}
-
 template <int S, int K>
 __device__ __forceinline__ void store_state(u32* __restrict__ base, const u64 (&w)[S], const u32 (&m)[K]) {
     u64* ws = reinterpret_cast<u64*>(base);
@@ -133,20 +107,18 @@ __device__ __forceinline__ void store_state(u32* __restrict__ base, const u64 (&
     for (int q = 0; q < K; ++q) base[2 * S + q] = m[q];
 }
 
-// Store one new state at index ni: its record (the packed state, the
-// footprint and lane of its discovering lane: SRec), its trace link (global
-// parent ref), its window-sort class (B.cls: a layout hint, read 1 B per
-// state by the next level's window sort) and the fused invariant check.
+// Store one new state at index ni: the packed state, its trace link (global
+// parent ref, lane), the footprint of its discovering lane (commuting
+// diamonds; only shapes whose kernels skip diamonds keep them), its
+// window-sort class (B.cls: a layout hint, read 1 B per state by the next
+// level's window sort) and the fused invariant check.
 template <int S, int K>
 __device__ __forceinline__ void store_new(const Params& P, const DevBufs& B, u64 ni, const u64 (&wo)[S],
                                           const u32 (&mo)[K], u64 parent, int lane, u64 foot) {
-    typedef SRec<S, K> SR;
-    u32* r = B.store + ni * (u64)SR::SW;
-    store_state<S, K>(r, wo, mo);
-    *reinterpret_cast<u64*>(r + SR::FOOT) = foot;  // NW is even: 8-byte aligned
-    r[SR::ACT] = (u32)lane;
+    store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
     B.parent[ni] = parent;
     B.act[ni] = (uint8_t)lane;
+    if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = foot;
     B.cls[ni] = (uint8_t)state_class_fine<S, K>(wo, mo);
     const int v = check_invariants<S, K>(wo, mo, P);
     if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
@@ -223,7 +195,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         }
         u64 w[S];
         u32 m[K];
-        const u32* pr = REP ? B.rep + (lo + rel) * (u64)RR::RR : B.store + (lo + rel) * (u64)SRec<S, K>::SW;
+        const u32* pr = REP ? B.rep + (lo + rel) * (u64)RR::RR : B.store + (lo + rel) * (u64)NW;
         load_state<S, K>(pr, w, m);
         Delta d;
         u64 foot;
@@ -329,8 +301,8 @@ __device__ __forceinline__ int verify_hit(const u64 (&w)[S], const u32 (&m)[K], 
     lane_delta<S, K>(w, m, lane, P, d);
     PackedState<S, K> o;
     materialise<S, K>(w, m, d, o.w, o.m);
-    if constexpr (SYM) return same_orbit<S, K>(o, B.store + ix * (u64)SRec<S, K>::SW, PT) ? 0 : 1;
-    return same_state<S, K>(o.w, o.m, B.store + ix * (u64)SRec<S, K>::SW) ? 0 : 1;
+    if constexpr (SYM) return same_orbit<S, K>(o, B.store + ix * (u64)NW, PT) ? 0 : 1;
+    return same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW) ? 0 : 1;
 }
 
 __device__ __forceinline__ u64 wave_sum64(u64 v) {
@@ -353,7 +325,7 @@ __global__ __launch_bounds__(256) void k_publish(const Params P, const PermTable
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + i * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + i * (u64)NW, w, m);
         const u64 key = verify_key<S, K, SYM>(w, m, P, PT);
         u64 s = key & B.tmask;
         u64 n = 0;
@@ -374,7 +346,7 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable 
         const int lane = (int)(sl >> 56);
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + parent * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + parent * (u64)NW, w, m);
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);
         PackedState<S, K> o;
@@ -386,8 +358,8 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable 
         }
         ++vchk;
         bool same;
-        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)SRec<S, K>::SW, PT);
-        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)SRec<S, K>::SW);
+        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)NW, PT);
+        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW);
         vcol += same ? 0u : 1u;
     }
     vchk = wave_sum64(vchk);
@@ -521,7 +493,7 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
         }
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + (lo + rel) * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);
         u64 wo[S];
@@ -583,7 +555,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
         }
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + (lo + rel) * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
         Delta d;
         u64 foot;
         if constexpr (Lanes<S, K>::N <= 64) {  // the lane's descriptor: no family-offset compares
@@ -655,7 +627,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
     typedef RepRec<S, K> RR;
-    constexpr int FW = REP ? RR::RR : SRec<S, K>::SW;  // words per frontier record
+    constexpr int FW = REP ? RR::RR : NW;  // words per frontier record
     const u32* const fr = REP ? B.rep : B.store;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
     constexpr bool LISTOWN = DIST && !REP;  // list entries carry their owner
@@ -749,11 +721,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         u64 w[S];
         u32 m[K];
         const u32* rec = fr + (lo + rel) * (u64)FW;
-        u64 r_foot = 0;  // a store record's footprint and lane (loaded with the state)
-        u32 r_act = 255;
         if (live) {
-            if constexpr (REP) load_state<S, K>(rec, w, m);
-            else load_record<S, K>(rec, w, m, r_foot, r_act);
+            load_state<S, K>(rec, w, m);
         } else {
 #pragma unroll
             for (int i = 0; i < S; ++i) w[i] = 0;
@@ -788,13 +757,12 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             int act = 255;
             u64 foot = 0;
             if (on) {
-                // the lane and footprint share the state's record (one granule)
                 if constexpr (REP) {
                     act = (int)(rec[RR::ACT] & 0xFFu);
                     foot = (u64)rec[RR::FOOT] | ((u64)rec[RR::FOOT + 1] << 32);
                 } else {
-                    act = (int)(r_act & 0xFFu);
-                    foot = r_foot;
+                    act = (int)B.act[lo + rel];
+                    foot = B.foot[lo + rel];
                 }
             }
             diamond_of<S, K>(m, act, foot, P, dm);
@@ -1063,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_capacity_check(const Params P, const De
     for (u64 t = lo + (u64)blockIdx.x * 256 + threadIdx.x; t < hi; t += (u64)gridDim.x * 256) {
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + t * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + t * (u64)NW, w, m);
         for (int lane = 0; lane < nl; ++lane) {
             Delta d;
             lane_delta<S, K>(w, m, lane, P, d);
@@ -1281,7 +1249,7 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
         }
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + pidx * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + pidx * (u64)NW, w, m);
         Delta dl;
         lane_delta<S, K>(w, m, lane, P, dl);
         u64 wo[S];
@@ -1356,8 +1324,8 @@ __global__ __launch_bounds__(256) void k_compare_remote(const Params P, const Pe
         }
         ++vchk;
         bool same;
-        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)SRec<S, K>::SW, PT);
-        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)SRec<S, K>::SW);
+        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)NW, PT);
+        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW);
         vcol += same ? 0u : 1u;
     }
     vchk = wave_sum64(vchk);
@@ -1387,7 +1355,7 @@ __global__ __launch_bounds__(256) void k_ties(const Params P, const PermTable PT
             const u64 rec = B.ties[t];
             pidx = rec & ((1ull << 56) - 1);
             lane = (int)(rec >> 56);
-            load_state<S, K>(B.store + pidx * (u64)SRec<S, K>::SW, w, m);
+            load_state<S, K>(B.store + pidx * (u64)NW, w, m);
             lane_delta<S, K>(w, m, lane, P, d);
             u64 base[S];
 #pragma unroll
@@ -1499,7 +1467,7 @@ __global__ __launch_bounds__(256) void k_rehash(const Params P, const PermTable 
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + i * (u64)SRec<S, K>::SW, w, m);
+        load_state<S, K>(B.store + i * (u64)NW, w, m);
         u64 key = SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m);
         key &= P.fp_mask;
         key = key ? key : 1ull;
@@ -1516,18 +1484,17 @@ __global__ __launch_bounds__(256) void k_pack_rep(const DevBufs B, u64 lo, u64 h
     typedef RepRec<S, K> RR;
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u32* r = out + (i - lo) * (u64)RR::RR;
-        const uint2* src = reinterpret_cast<const uint2*>(B.store + i * (u64)SRec<S, K>::SW);
+        const uint2* src = reinterpret_cast<const uint2*>(B.store + i * (u64)NW);
         uint2* dst = reinterpret_cast<uint2*>(r);
 #pragma unroll
         for (int q = 0; q < NW / 2; ++q) dst[q] = src[q];
         const u64 ref = B.ref_tag | i;
-        const u32* sr = B.store + i * (u64)SRec<S, K>::SW;
-        const u64 f = (u64)sr[SRec<S, K>::FOOT] | ((u64)sr[SRec<S, K>::FOOT + 1] << 32);
+        const u64 f = Lanes<S, K>::N <= 64 ? B.foot[i] : 0ull;
         r[RR::REF] = (u32)ref;
         r[RR::REF + 1] = (u32)(ref >> 32);
         r[RR::FOOT] = (u32)f;
         r[RR::FOOT + 1] = (u32)(f >> 32);
-        r[RR::ACT] = (sr[SRec<S, K>::ACT] & 0xFFu) | ((u32)B.cls[i] << 8);
+        r[RR::ACT] = (u32)B.act[i] | ((u32)B.cls[i] << 8);
         r[RR::ACT + 1] = 0;
     }
 }
