@@ -1090,11 +1090,11 @@ static int sym_variant() {
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1686,7 +1686,8 @@ static int expand_variant() {
 
 // Sharded expansion kernel (RMC_DIST_KVARIANT, A/B): 0 (default) windows of 8
 // tiles sorted in LDS; 1 windows of 16 tiles presorted by k_window_order; 2 the
-// same with 6 probes in flight per thread at 5 waves/SIMD.
+// same with 6 probes in flight per thread at 5 waves/SIMD (default); 3 5 probes
+// at 6 waves with the parent's mixes recomputed (the single-GPU default's shape).
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
@@ -1772,6 +1773,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
+        } else if (dist_kvariant() == 3 && SORTED && B.word) {  // presorted, 5 probes, 6 waves, no parent mixes
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, false>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, false>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));

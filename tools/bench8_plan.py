@@ -21,7 +21,13 @@ the rehearsal), rounds = ceil(frontier / N / min(2^24, kcap / rho)) with rho =
 kappa / N keys per state to one owner (librmc's round sizing, rmc_dist.cpp).
 
     python tools/bench8_plan.py prefix_levels.jsonl prefix_rounds.txt prefix_dist8.json shape_levels.jsonl [N]
+        [--sizing profiles/r03/sizing_next_bounds.txt]
+
+--sizing: per-level new-state counts of a longer depth-bounded run of the same
+model (tools/sizing.py) extend the measured prefix before the tail is
+extrapolated (counts only; the time per state is the prefix's).
 """
+import re
 import collections
 import json
 import math
@@ -98,12 +104,29 @@ def memory_plan(n, distinct):
 
 
 def main():
-    lv, rounds_p, pr_p, shape_p = sys.argv[1:5]
-    n = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+    args = sys.argv[1:]
+    sizing = None
+    if "--sizing" in args:
+        k = args.index("--sizing")
+        sizing = args[k + 1]
+        del args[k:k + 2]
+    lv, rounds_p, pr_p, shape_p = args[:4]
+    n = int(args[4]) if len(args) > 4 else 8
     t1, frontier, total1, rounds, keys_in, states, pr = dcm.load(lv, rounds_p, pr_p)
     pl = news(lv)
     depth_p = max(pl)
     prefix_new = [1] + [pl[i]["new"] for i in range(1, depth_p + 1)]
+    if sizing:  # "<model> level L distinct D new N" lines (level L's new states = new[L])
+        ext = {}
+        for ln in open(sizing):
+            mm = re.search(r"3:2:2:1:4:1:\S* level (\d+) distinct (\d+) new (\d+)", ln)
+            if mm:
+                ext[int(mm.group(1))] = int(mm.group(3))
+        for L in sorted(ext):
+            if L == len(prefix_new):
+                prefix_new.append(ext[L])
+            elif L < len(prefix_new):
+                assert prefix_new[L] == ext[L], (L, prefix_new[L], ext[L])
     sl = news(shape_p)
     shape_new = [1] + [sl[i]["new"] for i in sorted(sl)]
     f = min(t1.values())
@@ -115,7 +138,8 @@ def main():
              for r in range(n)]
     kshare = [sum(keys_in[L][r] for L in last3) / max(1, sum(sum(keys_in[L].values()) for L in last3))
               for r in range(n)]
-    print(json.dumps({"prefix_depth": depth_p, "prefix_distinct": sum(prefix_new), "f_level_us": f * 1e6,
+    print(json.dumps({"prefix_depth": depth_p, "counted_levels": len(prefix_new) - 1,
+                      "counted_distinct": sum(prefix_new), "f_level_us": f * 1e6,
                       "tau_ns_per_frontier_state": tau * 1e9, "generated_per_frontier_state": gen_per,
                       "keys_per_expanded_state": kappa, "rank_state_share_max": max(share)}))
     kcap = min(1 << 25, max(1 << 20, (1 << 26) // n))
@@ -132,7 +156,7 @@ def main():
             St[L].update(states[L])
             Ro[L] = set(rounds[L])
         for L in range(depth_p + 1, len(full)):
-            F = full[L - 1]
+            F = full[L - 1]  # level L expands the states found at level L - 1
             T1[L] = f + F * tau
             Fr[L] = F
             Ki[L].update({r: F * kappa * kshare[r] for r in range(n)})
