@@ -1062,39 +1062,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // (deferred to k_ties).  WS: the lane-superset walk over class-sorted windows
 // of 16 tiles, 4 waves/SIMD (72.1-72.7 vs 75.0-75.3 ms for 8 tiles on the
 // MCraftBench bounds); otherwise (more than 64 lanes) every lane, 5 waves/SIMD.
-// PS: windows presorted by k_window_order at WPE waves/SIMD (RMC_SYM_VARIANT=1, A/B).
-template <int S, int K, int BATCH, bool WS, bool PS = false, int WPE = 4>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PS ? WPE : S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
+// (Round 4: windows presorted by k_window_order, 6 probes, 5 waves/SIMD measured
+// 78.0-78.5 vs 78.6-78.9 ms on the MCraftBench bounds, profiles/r04/ab/sym_variant_r04n.txt:
+// neutral, removed.)
+template <int S, int K, int BATCH, bool WS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
 k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (PS && WS && Lanes<S, K>::N <= 64)
-        expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16, 0, false, true>(P, PT, B, lo, hi);
-    else if constexpr (WS && Lanes<S, K>::N <= 64)
+    if constexpr (WS && Lanes<S, K>::N <= 64)
         expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16>(P, PT, B, lo, hi);
     else
         expand_body<S, K, true, BATCH, false, false, false>(P, PT, B, lo, hi);
 }
 
-// SYMMETRY expansion kernel (RMC_SYM_VARIANT, A/B): 0 (default) windows sorted
-// in LDS, 8 probes, 4 waves/SIMD; 1 windows presorted by k_window_order, 6
-// probes, 5 waves/SIMD.
-static int sym_variant() {
-    static int v = [] {
-        const char* e = getenv("RMC_SYM_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
+
 
 // The sharded expansion: send markers in the local set, diamond skipping and
 // the lane-superset walk over class-sorted windows of 8 tiles (4 waves/SIMD;
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1686,8 +1677,10 @@ static int expand_variant() {
 
 // Sharded expansion kernel (RMC_DIST_KVARIANT, A/B): 0 (default) windows of 8
 // tiles sorted in LDS; 1 windows of 16 tiles presorted by k_window_order; 2 the
-// same with 6 probes in flight per thread at 5 waves/SIMD (default); 3 5 probes
-// at 6 waves with the parent's mixes recomputed (the single-GPU default's shape).
+// same with 6 probes in flight per thread at 5 waves/SIMD (default: 293-299 vs
+// 299-304 ms for 0 at one rank, profiles/r04/ab/dist_kvariant_*; 5 probes at 6
+// waves without parent mixes, the single-GPU default's shape, spills 48 B here:
+// 305-307 ms, removed).
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
@@ -1725,14 +1718,7 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else if (sym_variant() == 1 && SORTED && B.word) {
-                const void* kp = reinterpret_cast<const void*>(&(k_expand_sym<S, K, 6, true, true, 5>));
-                const u64 want = resident_grid(kp);
-                const u64 gs = blocks < want ? blocks : want;
-                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
-                hipLaunchKernelGGL((k_expand_sym<S, K, 6, true, true, 5>), dim3((unsigned)gs), dim3(256), 0, st, P, PT,
-                                   B, a, b);
-            } else
+            else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
         } else if (verify) {
@@ -1773,11 +1759,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
-        } else if (dist_kvariant() == 3 && SORTED && B.word) {  // presorted, 5 probes, 6 waves, no parent mixes
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, false>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, false>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
