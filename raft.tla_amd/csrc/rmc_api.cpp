@@ -517,7 +517,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         hipMalloc(&c->B.parent, win * 8) != hipSuccess || hipMalloc(&c->B.act, win) != hipSuccess ||
         hipMalloc(&c->B.foot, win * 8) != hipSuccess || hipMalloc(&c->B.cls, win) != hipSuccess ||
         hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
-        hipMalloc(&c->B.word, (1ull << 24) * 2) != hipSuccess ||  // presorted windows of one launch
+        hipMalloc(&c->B.word, (1ull << kMaxLaunchLog2) * 2) != hipSuccess ||  // presorted windows of one launch
         hipMalloc(&c->d_staged, (size_t)c->NW * 4 * 64) != hipSuccess) {
         c->err = "device allocation failed (capacity " + std::to_string(win) + " states)";
         return bail(RMC_E_NOMEM);
@@ -655,7 +655,15 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         c->target_idx = c->h_ctr->viol >> 4;
     }
     }  // !resume
-    const u64 CHUNK = 1ull << 24;  // k_expand_sort keeps relative indices in 24 bits
+    // states per expansion launch: at most kMaxLaunch (B.word holds one launch's
+    // presorted positions), and a level is cut into EQUAL launches, so no launch
+    // is a small remainder that leaves most of the resident grid idle
+    // (RMC_LAUNCH_LOG2: a smaller cap, A/B)
+    static const u64 CHUNK = [] {
+        const char* e = getenv("RMC_LAUNCH_LOG2");
+        const int l = e ? std::max(16, std::min(kMaxLaunchLog2, atoi(e))) : kMaxLaunchLog2;
+        return 1ull << l;
+    }();
     while (!c->have_target) {
         const u64 lo = c->level_start[depth - 1], hi = c->level_start[depth];
         if (lo == hi) break;  // fixpoint
@@ -672,8 +680,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         // the tie buffer cannot overflow whatever the model's tie rate
         const u64 sym_chunk = c->sh.sym ? std::max<u64>(1, std::min<u64>(CHUNK, c->B.tie_cap / (u64)c->P.off[10])) : CHUNK;
         const u64 chunk = c->sh.verify ? (1ull << 20) : c->sh.sym ? sym_chunk : CHUNK;
+        const u64 nlaunch = (hi - lo + chunk - 1) / chunk;
+        const u64 even = (hi - lo + nlaunch - 1) / nlaunch;  // <= chunk
         for (u64 a = lo, b = 0; a < hi; a = b) {
-            b = std::min(hi, a + chunk);
+            b = std::min(hi, a + even);
             if (c->spill.on) {
                 // every lane yields at most one new state: a launch of n states
                 // stays inside the window when n * lanes <= room.  Launches

@@ -23,6 +23,7 @@ struct Counters {
     u64 vcount;     // deferred hits in vbuf (stored twin not yet published)
     u64 nties;      // SYMMETRY: successors with tied signatures deferred to k_ties
     u64 novf;       // sharded: keys that did not fit their owner's outbox (parked in B.ovf)
+    u64 wnext;      // dynamic work units: the next (window, wave slot) of the launch (zeroed by k_window_order)
     u64 walked;     // (state, lane) slots the lane walk visited (RMC_WALK_STATS: lane efficiency = generated / walked)
 };
 
@@ -118,6 +119,9 @@ hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply
 // has more to send: host_more, or parked keys beyond ovf_done; bit 1: its
 // parking buffer overflowed), out[2W] = novf.
 hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st);
+// States per single-GPU expansion launch at most (B.word holds one launch's
+// presorted window positions).
+constexpr int kMaxLaunchLog2 = 25;
 // Presorted windows: k_window_order over the launch [lo, hi) for an expansion
 // grid of `grid` blocks and windows of at most wt_max tiles (B.word).
 hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st);

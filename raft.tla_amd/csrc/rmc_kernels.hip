@@ -610,7 +610,8 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 //   level's records in B.rep (gathered from every rank); every rank expands
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
-          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false>
+          bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
+          bool DYN = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -624,6 +625,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // so the kernel carries no sort: no LDS bins, scan or block barriers
     static_assert(!PRESORT || (SORT && !REP), "presorted windows: the sorted kernels");
     constexpr bool INSORT = SORT && !PRESORT;
+    // DYN: each wave takes its next unit of work — one wave's quarter of a
+    // presorted window (its 64 lanes of every tile) — from a launch-wide
+    // counter, instead of the block's fixed share of windows: the waves end
+    // together however unequal the units' costs and whatever the window count
+    static_assert(!DYN || PRESORT, "dynamic units: presorted windows");
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
     typedef RepRec<S, K> RR;
@@ -667,7 +673,17 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         const u64 per_block = (nf + (u64)gridDim.x * 256ull - 1) / ((u64)gridDim.x * 256ull);
         wt = per_block < (u64)WT ? (per_block ? per_block : 1ull) : (u64)WT;
     }
-    for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {  // block-uniform
+    u32 q64 = (u32)threadIdx.x & ~63u;  // this thread's window slot base (DYN: the unit's)
+    u64 win = DYN ? 0ull : (u64)blockIdx.x * 256ull * wt;
+    for (;; win += (u64)gridDim.x * 256ull * wt) {  // block-uniform (DYN: wave-uniform)
+    if constexpr (DYN) {
+        u32 unit = 0;
+        if (me == 0) unit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
+        unit = (u32)__builtin_amdgcn_readfirstlane(__shfl((int)unit, 0));
+        win = (u64)(unit >> 2) * 256ull * wt;
+        q64 = (unit & 3u) * 64u;
+    }
+    if (win >= nf) break;
     u32 wn = 0;  // SORT: states in this window
     if constexpr (SORT) wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
     if constexpr (INSORT) {
@@ -710,7 +726,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         u64 rel;
         bool live;
         if constexpr (SORT) {
-            const u32 p = (u32)wk * 256u + threadIdx.x;
+            const u32 p = (u32)wk * 256u + q64 + (u32)me;
             live = p < wn;
             if constexpr (PRESORT) rel = win + (live ? (u32)B.word[win + p] : 0u);
             else rel = win + (live ? s_ord[p] : 0u);
@@ -1050,11 +1066,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // The single-GPU expansion kernel: the lane-superset walk over class-sorted
 // windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
 // loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true>
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, bool DYN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
-        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, DYN>(P, PT, B, lo,
+                                                                                                     hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1132,10 +1149,12 @@ __global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64
 // launch size and the expansion grid exactly as the kernel computes it), each
 // counting-sorted by the states' 1-byte classes: word[win + i] = the i-th
 // position of window win in class order.
-__global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo, u64 nf, u64 wt, uint16_t* word) {
+__global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo, u64 nf, u64 wt, uint16_t* word,
+                                                      unsigned long long* wnext) {
     __shared__ u32 bins[256];
     __shared__ uint8_t cs[256 * 16];
     const u32 tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0) *wnext = 0;  // the next expansion launch's dynamic work counter
     for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {
         const u32 wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
         __syncthreads();
@@ -1169,13 +1188,13 @@ __global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo
 hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st) {
     const u64 nf = hi - lo;
     if (nf == 0) return hipSuccess;
-    if (wt_max > 16) return hipErrorInvalidValue;
+    if (wt_max > 16 || nf > (1ull << kMaxLaunchLog2)) return hipErrorInvalidValue;
     // the expansion kernel's window size for this launch (expand_body: per_block)
     const u64 per_block = (nf + grid * 256ull - 1) / (grid * 256ull);
     const u64 wt = per_block < wt_max ? (per_block ? per_block : 1ull) : wt_max;
     const u64 nwin = (nf + 256ull * wt - 1) / (256ull * wt);
     hipLaunchKernelGGL(k_window_order, dim3((unsigned)(nwin < grid ? nwin : grid)), dim3(256), 0, st, B.cls, lo, nf,
-                       wt, B.word);
+                       wt, B.word, (unsigned long long*)&B.ctr->wnext);
     return hipGetLastError();
 }
 
@@ -1725,6 +1744,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
         } else if (expand_variant() == 6 && SORTED) {  // windows sorted in LDS, 8 probes, 4 waves/SIMD
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
+        } else if (expand_variant() == 20 && SORTED && B.word) {  // 19 with dynamic per-wave work units
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, true>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, true>));
         } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18 || expand_variant() == 19) &&
                    SORTED && B.word) {
             // windows presorted by k_window_order (no sort in LDS, so a smaller block):
