@@ -1674,22 +1674,24 @@ static u64 resident_grid(const void* k) {
     return v;
 }
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 10 (default) =
+// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 20 (default) =
 // k_expand_sort over windows of 16 tiles presorted by class (k_window_order;
-// no sort in the kernel, so a smaller block), 6 probes in flight per thread,
-// 5 waves/SIMD (242-247 ms per bench BFS vs 263-269 ms for 6,
-// profiles/r04/ab/); 6 = the round-3 kernel (windows sorted in LDS, 8 probes,
-// 4 waves); 15 = 10 with 5 probes; 18 = 6 probes at 6 waves with the parent's
-// mixes recomputed (80 VGPRs); 1 = every lane of every state (k_expand, what
-// shapes with more than 64 lanes run).  Measured and removed in round 4: 8
-// probes at 5-6 waves, 4 probes at 5-6 waves, 7 probes at 5 waves (VGPR spills
-// or fewer probes in flight), the next tile's state prefetched into registers
-// (4 waves: 260-263 ms) or by LDS-DMA.  Rounds 2-3's rejected variants are in
-// git history.
+// no sort in the kernel, so a smaller block), 5 probes in flight per thread,
+// the parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD), each wave
+// taking its next quarter-window from a launch-wide counter (229-232 vs
+// 241-243 ms for the same kernel with fixed shares, 19; profiles/r04/ab/);
+// 19 = fixed shares; 10 = 6 probes at 5 waves with the mixes held (247-250
+// ms); 15 = 5 probes at 5 waves; 18 = 6 probes at 6 waves (spills); 6 = the
+// round-3 kernel (windows sorted in LDS, 8 probes, 4 waves: 263-269 ms); 1 =
+// every lane of every state (k_expand, what shapes with more than 64 lanes
+// run).  Measured and removed in round 4: 8 probes at 5-6 waves, 4 probes at
+// 5-6 waves, 7 probes at 5 waves (spills or fewer probes in flight), the next
+// tile's state prefetched into registers or by LDS-DMA, 64-B store records.
+// Rounds 2-3's rejected variants are in git history.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 19;
+        return e ? atoi(e) : 20;
     }();
     return v;
 }
