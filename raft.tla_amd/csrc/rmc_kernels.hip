@@ -1098,11 +1098,11 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool DYN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true, DYN>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1785,6 +1785,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
+        } else if (dist_kvariant() == 3 && SORTED && B.word) {  // 2 with dynamic per-wave work units
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5, true>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5, true>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
