@@ -6,6 +6,7 @@ must equal the oracle's."""
 import json
 import os
 import random
+import sys
 from collections import Counter, defaultdict
 
 import pytest
@@ -65,6 +66,40 @@ def test_bfs_matches_oracle(name):
     assert res.depth == g["depth"]
     assert res.left_on_queue == g["left_on_queue"]
     assert res.violated_inv == 0 and res.deadlock == 0
+
+
+SMALL_LAUNCHES = r"""
+import json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], 'raft.tla_amd'))
+sys.path.insert(0, sys.argv[1])
+import rmc
+from tests.test_gpu import cfg_from, GOLDEN, run
+out = {}
+for name in ("small", "bounded_prefix14", "tiny2_v2"):
+    g = GOLDEN[name]
+    res, levels, _ = run(cfg_from(g["params"], capacity=max(1 << 22, int(g["distinct"] * 1.25))))
+    out[name] = [levels == g["level_new"], res.distinct == g["distinct"], res.generated == g["generated"],
+                 res.depth == g["depth"], int(res.expand_launches)]
+print(json.dumps(out))
+"""
+
+
+def test_many_launches_per_level_keep_every_count(tmp_path):
+    """Levels cut into many equal launches (RMC_LAUNCH_LOG2=16: launches of at
+    most 65,536 states), each drained by dynamic per-wave work units: every
+    per-level count of three golden models (levels of up to 0.15-0.6 M states)
+    is unchanged."""
+    import subprocess
+    script = tmp_path / "small_launches.py"
+    script.write_text(SMALL_LAUNCHES)
+    env = dict(os.environ, RMC_LAUNCH_LOG2="16")
+    r = subprocess.run([sys.executable, str(script), ROOT], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    for name, (lv, d, gen, dep, launches) in out.items():
+        assert lv and d and gen and dep, name
+        assert launches > GOLDEN[name]["depth"], (name, launches)  # some level took several launches
 
 
 @pytest.mark.parametrize("prefix", ["bench_prefix22", "bench_prefix24"])
