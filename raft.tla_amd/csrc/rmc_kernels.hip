@@ -611,7 +611,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
           bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
-          bool DYN = false>
+          int DYN = 0>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -628,8 +628,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // DYN: each wave takes its next unit of work — one wave's quarter of a
     // presorted window (its 64 lanes of every tile) — from a launch-wide
     // counter, instead of the block's fixed share of windows: the waves end
-    // together however unequal the units' costs and whatever the window count
-    static_assert(!DYN || PRESORT, "dynamic units: presorted windows");
+    // together however unequal the units' costs and whatever the window count.
+    // DYN == 2 asks for the next unit as the current one starts, so the counter's
+    // round trip overlaps the unit's first loads instead of preceding them.
+    static_assert(DYN == 0 || PRESORT, "dynamic units: presorted windows");
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
     typedef RepRec<S, K> RR;
@@ -675,10 +677,16 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     u32 q64 = (u32)threadIdx.x & ~63u;  // this thread's window slot base (DYN: the unit's)
     u64 win = DYN ? 0ull : (u64)blockIdx.x * 256ull * wt;
+    u32 nunit = 0;  // DYN == 2: the unit already asked for (lane 0)
+    if constexpr (DYN == 2)
+        if (me == 0) nunit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
     for (;; win += (u64)gridDim.x * 256ull * wt) {  // block-uniform (DYN: wave-uniform)
-    if constexpr (DYN) {
-        u32 unit = 0;
-        if (me == 0) unit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
+    if constexpr (DYN != 0) {
+        u32 unit = nunit;
+        if (me == 0) {
+            if constexpr (DYN == 1) unit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
+            else nunit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
+        }
         unit = (u32)__builtin_amdgcn_readfirstlane(__shfl((int)unit, 0));
         win = (u64)(unit >> 2) * 256ull * wt;
         q64 = (unit & 3u) * 64u;
@@ -1066,7 +1074,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // The single-GPU expansion kernel: the lane-superset walk over class-sorted
 // windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
 // loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, bool DYN = false>
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64)
@@ -1098,11 +1106,11 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool DYN = false>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true, DYN>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1701,7 +1709,8 @@ static int expand_variant() {
 // same with 6 probes in flight per thread at 5 waves/SIMD (default: 293-299 vs
 // 299-304 ms for 0 at one rank, profiles/r04/ab/dist_kvariant_*; 5 probes at 6
 // waves without parent mixes, the single-GPU default's shape, spills 48 B here:
-// 305-307 ms, removed).
+// 305-307 ms, removed; 2 with dynamic per-wave units: 300-307 vs 298-305 ms on
+// two boxes, profiles/r04/ab/dist_kvariant_2_3_*, removed).
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
@@ -1746,11 +1755,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
         } else if (expand_variant() == 6 && SORTED) {  // windows sorted in LDS, 8 probes, 4 waves/SIMD
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if (expand_variant() == 20 && SORTED && B.word) {  // 19 with dynamic per-wave work units
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, true>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, true>));
+        } else if ((expand_variant() == 20 || expand_variant() == 21) && SORTED && B.word) {
+            // 19 with dynamic per-wave work units (21: the next unit asked for one unit ahead)
+#define RMC_DYN(D)                                                                                               {                                                                                                                const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, D>));         const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                                  if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                                     RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, D>));                          }
+            if (expand_variant() == 20) RMC_DYN(1)
+            else RMC_DYN(2)
+#undef RMC_DYN
         } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18 || expand_variant() == 19) &&
                    SORTED && B.word) {
             // windows presorted by k_window_order (no sort in LDS, so a smaller block):
@@ -1785,11 +1795,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
-        } else if (dist_kvariant() == 3 && SORTED && B.word) {  // 2 with dynamic per-wave work units
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5, true>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5, true>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
