@@ -507,14 +507,16 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // Sharded mode with send markers (MARK): the local fingerprint set doubles
 // as the record of keys already sent — a successor owned elsewhere is
 // CAS-inserted into it like a local one, so the probe loop is the single-GPU
-// loop and a remote key is shipped at most once per rank (a lossless
-// sent-cache).  The list carries only (rel | owner << 24, lane); here each
-// listed successor is re-derived: owned ones are stored as in flush_new,
-// the others get their key back from the materialised successor (the
-// fingerprint is order-free: it equals the incremental probe key) and go to
-// the owner's outbox with a ticket.  One reservation atomic per destination.
+// loop (no owner computed per probe) and a remote key is shipped at most once
+// per rank (a lossless sent-cache).  The list carries only (rel, lane); here
+// each listed successor's owner is found from its changed word (a first pass,
+// only with more than one rank; it goes to rel's top byte: a sharded launch
+// holds < 2^24 states), then each is re-derived: owned ones are stored as in
+// flush_new, the others get their key back from the materialised successor
+// (the fingerprint is order-free: it equals the incremental probe key) and go
+// to the owner's outbox with a ticket.  One reservation atomic per destination.
 template <int S, int K>
-__device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+__device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u64 lo, u32* l_rel,
                                            const uint8_t* l_lane, u32 n) {
     constexpr int NW = 2 * S + K;
     wave_sync_lds();
@@ -523,7 +525,27 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
     u64 mine = 0;  // lane dd: entries for destination dd, then its next slot
     for (u32 e0 = 0; e0 < n; e0 += 64) {
         const u32 e = e0 + (u32)me;
-        const u32 dest = e < n ? (l_rel[e] >> 24) : 0xFFu;
+        u32 dest = 0xFFu;
+        if (e < n) {
+            dest = 0;
+            if (B.world > 1) {
+                u64 w[S];
+                u32 m[K];
+                load_state<S, K>(B.store + (lo + l_rel[e]) * (u64)NW, w, m);
+                Delta d;
+                if constexpr (Lanes<S, K>::N <= 64) lane_delta_desc<S, K>(w, m, P.ldesc[l_lane[e]], P, d);
+                else lane_delta<S, K>(w, m, l_lane[e], P, d);
+                if (B.owner_mode == 0) {
+                    u64 wo[S];
+                    u32 mo[K];
+                    materialise<S, K>(w, m, d, wo, mo);
+                    dest = owner_of(fp_of_materialised<S, K>(wo, mo, P), B.world);
+                } else {
+                    dest = owner_succ_w<S>(0ull, d, w, B);
+                }
+                l_rel[e] |= dest << 24;
+            }
+        }
         for (u32 dd = 0; dd < B.world; ++dd) {
             const u64 bal = __ballot(dest == dd);
             if ((u32)me == dd) mine += (u64)__popcll(bal);
@@ -628,9 +650,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // DYN: each wave takes its next unit of work — one wave's quarter of a
     // presorted window (its 64 lanes of every tile) — from a launch-wide
     // counter, instead of the block's fixed share of windows: the waves end
-    // together however unequal the units' costs and whatever the window count.
-    // DYN == 2 asks for the next unit as the current one starts, so the counter's
-    // round trip overlaps the unit's first loads instead of preceding them.
+    // together however unequal the units' costs and whatever the window count
     static_assert(DYN == 0 || PRESORT, "dynamic units: presorted windows");
     // (the marker kernel measured no gain from PIPE at one rank: 308.7-309.7 vs 307.4-308.7 ms)
     constexpr int NW = 2 * S + K;
@@ -638,7 +658,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     constexpr int FW = REP ? RR::RR : NW;  // words per frontier record
     const u32* const fr = REP ? B.rep : B.store;
     constexpr bool TIEDEFER = SYM && !DIST && !VERIFY;
-    constexpr bool LISTOWN = DIST && !REP;  // list entries carry their owner
+    constexpr bool LISTOWN = SENTC;  // list entries carry their owner (MARK: found at flush time)
     constexpr int WT = SORT ? WTILES : 1;   // tiles per window
     __shared__ uint16_t s_ord[INSORT ? 256 * WT : 1];  // window positions in class order
     __shared__ uint8_t s_wcls[INSORT ? 256 * WT : 1];  // class of each window position
@@ -677,16 +697,10 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     u32 q64 = (u32)threadIdx.x & ~63u;  // this thread's window slot base (DYN: the unit's)
     u64 win = DYN ? 0ull : (u64)blockIdx.x * 256ull * wt;
-    u32 nunit = 0;  // DYN == 2: the unit already asked for (lane 0)
-    if constexpr (DYN == 2)
-        if (me == 0) nunit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
     for (;; win += (u64)gridDim.x * 256ull * wt) {  // block-uniform (DYN: wave-uniform)
     if constexpr (DYN != 0) {
-        u32 unit = nunit;
-        if (me == 0) {
-            if constexpr (DYN == 1) unit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
-            else nunit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
-        }
+        u32 unit = 0;
+        if (me == 0) unit = (u32)atomicAdd((unsigned long long*)&B.ctr->wnext, 1ull);
         unit = (u32)__builtin_amdgcn_readfirstlane(__shfl((int)unit, 0));
         win = (u64)(unit >> 2) * 256ull * wt;
         q64 = (unit & 3u) * 64u;
@@ -847,7 +861,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         int nmb = 0;
                         if constexpr (PRE)
                             in_model = delta_fp_pre<S, K>(w, m, pmx, d, P, &h, DIA ? &nmb : nullptr,
-                                                          DIST ? &hwn : nullptr);
+                                                          (REP || SENTC) ? &hwn : nullptr);
                         else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
                         if constexpr (DIA)
                             if (in_model && h != h0 &&
@@ -861,7 +875,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         key = key ? key : 1ull;
                         if constexpr (REP) {  // a replicated level: only the owner probes
                             if (owner_succ<S, K>(key, d, pmx, hwn, B, powner) != B.rank) key = 0;
-                        } else if constexpr (DIST) {
+                        } else if constexpr (SENTC) {
                             if constexpr (PRE)
                                 s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(key, d, pmx, hwn, B, B.rank);
                             else  // no parent mixes: the successor's words 0 and 1 when it changes one
@@ -993,8 +1007,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 if (bal) {
                     if (is_new) {
                         const u32 pos = n + (u32)__popcll(bal & lt_mask);
-                        l_rel[pos] = (MARK && !REP) ? (u32)rel | ((u32)s_own[LISTOWN ? b : 0][threadIdx.x] << 24)
-                                                    : (u32)rel;
+                        l_rel[pos] = (u32)rel;
                         l_lane[pos] = (uint8_t)(SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b);
                         if constexpr (SENTC) {
                             l_dest[pos] = s_own[b][threadIdx.x];
@@ -1106,11 +1119,11 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, 0, false, true, DYN>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1682,13 +1695,15 @@ static u64 resident_grid(const void* k) {
     return v;
 }
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 20 (default) =
+// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 19 (default) =
 // k_expand_sort over windows of 16 tiles presorted by class (k_window_order;
 // no sort in the kernel, so a smaller block), 5 probes in flight per thread,
-// the parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD), each wave
-// taking its next quarter-window from a launch-wide counter (229-232 vs
-// 241-243 ms for the same kernel with fixed shares, 19; profiles/r04/ab/);
-// 19 = fixed shares; 10 = 6 probes at 5 waves with the mixes held (247-250
+// the parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD), each block
+// taking a fixed share of the windows; 20 = each wave taking its next
+// quarter-window from a launch-wide counter instead (a tie over three boxes:
+// 229-232 vs 241-243, 240 vs 228-234 and 229-242 vs 227-234 ms for 19,
+// profiles/r04/ab/expand_dynamic_units_*; asking for the next unit one unit
+// ahead measured 245-255 ms, removed); 10 = 6 probes at 5 waves with the mixes held (247-250
 // ms); 15 = 5 probes at 5 waves; 18 = 6 probes at 6 waves (spills); 6 = the
 // round-3 kernel (windows sorted in LDS, 8 probes, 4 waves: 263-269 ms); 1 =
 // every lane of every state (k_expand, what shapes with more than 64 lanes
@@ -1699,7 +1714,7 @@ static u64 resident_grid(const void* k) {
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 20;
+        return e ? atoi(e) : 19;
     }();
     return v;
 }
@@ -1755,12 +1770,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
         } else if (expand_variant() == 6 && SORTED) {  // windows sorted in LDS, 8 probes, 4 waves/SIMD
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if ((expand_variant() == 20 || expand_variant() == 21) && SORTED && B.word) {
-            // 19 with dynamic per-wave work units (21: the next unit asked for one unit ahead)
-#define RMC_DYN(D)                                                                                               {                                                                                                                const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, D>));         const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                                  if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                                     RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, D>));                          }
-            if (expand_variant() == 20) RMC_DYN(1)
-            else RMC_DYN(2)
-#undef RMC_DYN
+        } else if (expand_variant() == 20 && SORTED && B.word) {  // 19 with dynamic per-wave work units
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
         } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18 || expand_variant() == 19) &&
                    SORTED && B.word) {
             // windows presorted by k_window_order (no sort in LDS, so a smaller block):
@@ -1790,11 +1804,21 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
-        } else if (dist_kvariant() == 2 && SORTED && B.word) {  // presorted, 6 probes in flight, 5 waves/SIMD
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
+        } else if (dist_kvariant() >= 2 && dist_kvariant() <= 5 && SORTED && B.word) {
+            // presorted windows: 2 6 probes in flight at 5 waves/SIMD with the parent's
+            // mixes held; 4 (5) the single-GPU kernel's shape, 5 probes at 6 waves
+            // with the mixes recomputed (and dynamic per-wave units)
+#define RMC_DPS(BT, WPE, PRE, DYN)                                                                           \
+    {                                                                                                        \
+        const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN>)); \
+        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
+        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
+        RMC_EXPAND_LAUNCH((k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN>));                            \
+    }
+            if (dist_kvariant() == 4) RMC_DPS(5, 6, false, 0)
+            else if (dist_kvariant() == 5) RMC_DPS(5, 6, false, 1)
+            else RMC_DPS(6, 5, true, 0)
+#undef RMC_DPS
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
