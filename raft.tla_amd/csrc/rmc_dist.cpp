@@ -563,9 +563,8 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             } else if (cursor < hi) {
                 const u64 target = (u64)(D.fill * (double)kcap / std::max(rho, 0.02));
                 // the rest of the level in equal rounds of at most this size (not full
-                // rounds and a small remainder: a small round idles most of the grid);
-                // < 2^24 states: flush_mark keeps the owner in rel's top byte
-                const u64 cap = std::max<u64>(1, std::min<u64>({(u64)1 << 24, target, split_cap}));
+                // rounds and a small remainder: a small round idles most of the grid)
+                const u64 cap = std::max<u64>(1, std::min<u64>({1ull << kMaxLaunchLog2, target, split_cap}));
                 const u64 rest = hi - cursor, nr = (rest + cap - 1) / cap;
                 const u64 n = (rest + nr - 1) / nr;
                 HIPCHK(c, hipEventRecord(S.k0, c->st));

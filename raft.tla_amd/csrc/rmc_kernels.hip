@@ -510,14 +510,14 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
 // loop (no owner computed per probe) and a remote key is shipped at most once
 // per rank (a lossless sent-cache).  The list carries only (rel, lane); here
 // each listed successor's owner is found from its changed word (a first pass,
-// only with more than one rank; it goes to rel's top byte: a sharded launch
-// holds < 2^24 states), then each is re-derived: owned ones are stored as in
+// only with more than one rank, into l_dest), then each is re-derived: owned
+// ones are stored as in
 // flush_new, the others get their key back from the materialised successor
 // (the fingerprint is order-free: it equals the incremental probe key) and go
 // to the owner's outbox with a ticket.  One reservation atomic per destination.
 template <int S, int K>
-__device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u64 lo, u32* l_rel,
-                                           const uint8_t* l_lane, u32 n) {
+__device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                           const uint8_t* l_lane, uint8_t* l_dest, u32 n) {
     constexpr int NW = 2 * S + K;
     wave_sync_lds();
     const int me = (int)__lane_id();
@@ -543,7 +543,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
                 } else {
                     dest = owner_succ_w<S>(0ull, d, w, B);
                 }
-                l_rel[e] |= dest << 24;
+                l_dest[e] = (uint8_t)dest;
             }
         }
         for (u32 dd = 0; dd < B.world; ++dd) {
@@ -558,8 +558,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
     for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
         const u32 e = e0 + (u32)me;
         const bool valid = e < n;
-        const u32 rd = valid ? l_rel[e] : 0xFF000000u;
-        const u32 dest = rd >> 24;
+        const u32 dest = !valid ? 0xFFu : B.world > 1 ? (u32)l_dest[e] : 0u;
         u64 slot = ~0ull;
         for (u32 dd = 0; dd < B.world; ++dd) {
             const u64 bal = __ballot(dest == dd);
@@ -569,7 +568,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
             if ((u32)me == dd) mine += (u64)__popcll(bal);
         }
         if (!valid) continue;
-        const u64 rel = rd & 0xFFFFFFu;
+        const u64 rel = l_rel[e];
         const int lane = l_lane[e];
         if (dest == B.rank && slot >= B.cap) {
             atomicOr(&B.ctr->overflow, 1u);
@@ -670,7 +669,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     constexpr int LCAP = SENTC ? 256 : WCAP;
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
-    __shared__ uint8_t s_dest[SENTC ? 4 : 1][SENTC ? LCAP : 1];
+    __shared__ uint8_t s_dest[(SENTC || MARK) ? 4 : 1][(SENTC || MARK) ? LCAP : 1];  // owner per listed successor
     __shared__ u64 s_lkey[SENTC ? 4 : 1][SENTC ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
     __shared__ uint8_t s_own[LISTOWN ? BATCH : 1][LISTOWN ? 256 : 1];  // owner rank per probe
@@ -679,7 +678,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     const u64 lt_mask = (1ull << me) - 1ull;
     u32* l_rel = s_rel[wv];
     uint8_t* l_lane = s_lane[wv];
-    uint8_t* l_dest = s_dest[SENTC ? wv : 0];
+    uint8_t* l_dest = s_dest[(SENTC || MARK) ? wv : 0];
     u64* l_key = s_lkey[SENTC ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u32 gen = 0;  // generated lanes of this thread's states (< 2^32 per launch)
@@ -1017,7 +1016,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
                         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
-                        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+                        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
                         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
@@ -1034,7 +1033,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     if (n) {
         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
-        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, n);
+        else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
