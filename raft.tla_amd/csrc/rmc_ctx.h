@@ -52,7 +52,7 @@ struct DistState {
     rmc::u64 sent_slots = 0;
     int debug = 0;                  // RMC_DIST_DEBUG: one stderr line per round
     int table_grown = 0;            // rmc_shard doubled the fingerprint set once (send markers)
-    int split = 2;                  // RMC_DIST_SPLIT: rounds a large level is cut into at least
+    int split = 2;                  // RMC_DIST_SPLIT: rounds a large level is cut into at least (1 at world 1)
     int overlap = 1;                // RMC_DIST_OVERLAP=0: the next expansion waits for the exchange
     double fill = 0.5;              // RMC_DIST_FILL: expected fill of the fullest outbox a round aims at
                                     // (> 1 forces parking: a test hook)

@@ -538,8 +538,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         u64 cursor = lo, ovf_known = 0, ovf_done = 0;
         const u64 frontier = hi - lo;
         // at least D.split rounds for a large level, so one round's count
-        // exchange and read-back overlap the next round's expansion (at one
-        // rank too: without the split the one-rank bench loses 8 ms to them)
+        // exchange and read-back overlap the next round's expansion
         const u64 split_cap = frontier >= (1ull << 21) ? (frontier + D.split - 1) / (u64)D.split : frontier;
         u64 round_states[2] = {0, 0};  // states expanded by the round held in each set
         int round_kind[2] = {0, 0};    // 0 empty, 1 expansion, 2 drain
@@ -964,6 +963,10 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     }
     D.ag_cap = 4096;
     D.debug = getenv("RMC_DIST_DEBUG") != nullptr;
+    // rounds per large level: 2 at world > 1 so one round's exchange overlaps the next
+    // round's expansion; 1 at world 1, where no round exchanges anything (283.4-283.7
+    // vs 289.8-294.0 ms on the one-rank bench, profiles/r04/ab/dist_split_r04u.txt)
+    D.split = world > 1 ? 2 : 1;
     if (const char* s = getenv("RMC_DIST_SPLIT")) D.split = std::max(1, std::min(64, atoi(s)));
     if (const char* s = getenv("RMC_DIST_OVERLAP")) D.overlap = atoi(s) != 0;
     if (c->sh.verify) D.overlap = 0;  // rounds in order: each publishes its states before the next compares

@@ -27,7 +27,10 @@ Level 1's t1 holds the fingerprint set's clearing (a memset of the whole
 table), which shrinks with the per-rank table: it is charged as
 t1[1] * table_rank / table_1.
 
-    python tools/dist_cost_model.py levels.jsonl rounds.err per_rank.json N [rep_max ...]
+    python tools/dist_cost_model.py levels.jsonl rounds.err per_rank.json N [rep_max ...] [--k-dist K]
+
+k_dist: the sharded expansion kernel's time per state against the unsharded
+kernel's (1.0 assumes the same rate; the one-rank bench measures it).
 """
 import collections
 import json
@@ -110,8 +113,14 @@ LATENCIES = ((10e-6, 15e-6, 5e-6, 40e-6), (20e-6, 30e-6, 8e-6, 80e-6), (40e-6, 6
 
 
 def main():
-    lv_path, log_path, pr_path, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    reps = [int(x) for x in sys.argv[5:]] or [0, 1 << 18, 1 << 19, 1 << 20, 1 << 21, 1 << 22]
+    args = sys.argv[1:]
+    k_dist = 1.0
+    if "--k-dist" in args:
+        i = args.index("--k-dist")
+        k_dist = float(args[i + 1])
+        del args[i:i + 2]
+    lv_path, log_path, pr_path, n = args[0], args[1], args[2], int(args[3])
+    reps = [int(x) for x in args[4:]] or [0, 1 << 18, 1 << 19, 1 << 20, 1 << 21, 1 << 22]
     data = load(lv_path, log_path, pr_path)
     t1, frontier, total1, rounds, keys_in, states, pr = data
     stored = [p["stored"] for p in pr["per_rank"]]
@@ -131,7 +140,7 @@ def main():
                       "f_level_us": min(t1.values()) * 1e6, "table_frac_level1": table_frac}))
     for rep in reps:
         for lat in LATENCIES:
-            print(json.dumps(model(*data, n=n, rep_max=rep, lat=lat, table_frac=table_frac)))
+            print(json.dumps(model(*data, n=n, rep_max=rep, lat=lat, k_dist=k_dist, table_frac=table_frac)))
 
 
 if __name__ == "__main__":
