@@ -1118,11 +1118,11 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0, int PI = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, 0, false, true, DYN>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, PI, false, true, DYN>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1803,20 +1803,22 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
-        } else if (dist_kvariant() >= 2 && dist_kvariant() <= 5 && SORTED && B.word) {
+        } else if (dist_kvariant() >= 2 && dist_kvariant() <= 6 && SORTED && B.word) {
             // presorted windows: 2 6 probes in flight at 5 waves/SIMD with the parent's
             // mixes held; 4 (5) the single-GPU kernel's shape, 5 probes at 6 waves
-            // with the mixes recomputed (and dynamic per-wave units)
-#define RMC_DPS(BT, WPE, PRE, DYN)                                                                           \
+            // with the mixes recomputed (and dynamic per-wave units); 6 = 4 with the
+            // probe loads issued during the lane code, as the single-GPU kernel does
+#define RMC_DPS(BT, WPE, PRE, DYN, PI)                                                                       \
     {                                                                                                        \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN>)); \
+        const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN, PI>)); \
         const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
         if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
-        RMC_EXPAND_LAUNCH((k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN>));                            \
+        RMC_EXPAND_LAUNCH((k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN, PI>));                        \
     }
-            if (dist_kvariant() == 4) RMC_DPS(5, 6, false, 0)
-            else if (dist_kvariant() == 5) RMC_DPS(5, 6, false, 1)
-            else RMC_DPS(6, 5, true, 0)
+            if (dist_kvariant() == 4) RMC_DPS(5, 6, false, 0, 0)
+            else if (dist_kvariant() == 5) RMC_DPS(5, 6, false, 1, 0)
+            else if (dist_kvariant() == 6) RMC_DPS(5, 6, false, 0, (K <= 4 ? 1 : 0))
+            else RMC_DPS(6, 5, true, 0, 0)
 #undef RMC_DPS
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
