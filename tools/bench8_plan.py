@@ -17,11 +17,11 @@ its tail is extrapolated from what one GPU can measure:
 Per extrapolated level: t1 = f + frontier * tau (tau: seconds per frontier
 state over the prefix's last 3 levels), keys to owners = frontier * kappa
 (kappa: keys sent per expanded state over the prefix's last 3 levels, from
-the rehearsal), rounds = ceil(frontier / N / min(2^24, kcap / rho)) with rho =
+the rehearsal), rounds = ceil(frontier / N / min(2^25, kcap / rho)) with rho =
 kappa / N keys per state to one owner (librmc's round sizing, rmc_dist.cpp).
 
     python tools/bench8_plan.py prefix_levels.jsonl prefix_rounds.txt prefix_dist8.json shape_levels.jsonl [N]
-        [--sizing profiles/r03/sizing_next_bounds.txt]
+        [--sizing profiles/r03/sizing_next_bounds.txt] [--k-dist K]
 
 --sizing: per-level new-state counts of a longer depth-bounded run of the same
 model (tools/sizing.py) extend the measured prefix before the tail is
@@ -106,6 +106,11 @@ def memory_plan(n, distinct):
 def main():
     args = sys.argv[1:]
     sizing = None
+    k_dist = 1.0  # the sharded kernel's time per state against the unsharded kernel's
+    if "--k-dist" in args:
+        k = args.index("--k-dist")
+        k_dist = float(args[k + 1])
+        del args[k:k + 2]
     if "--sizing" in args:
         k = args.index("--sizing")
         sizing = args[k + 1]
@@ -162,16 +167,16 @@ def main():
             Ki[L].update({r: F * kappa * kshare[r] for r in range(n)})
             St[L].update({r: F * share[r] for r in range(n)})
             rho = kappa / n
-            per_round = min(1 << 24, kcap / max(rho, 0.02))
+            per_round = min(1 << 25, kcap / max(rho, 0.02))
             Ro[L] = set(range(max(1, math.ceil(F / n / per_round))))
         tot1 = sum(T1.values())
-        row = {"stretch": stretch, "depth": len(full) - 1, "distinct_est": distinct,
+        row = {"stretch": stretch, "k_dist": k_dist, "depth": len(full) - 1, "distinct_est": distinct,
                "generated_est": int(sum(pl[L]["generated"] for L in pl) + sum(
                    full[L - 1] * gen_per for L in range(depth_p + 1, len(full)))),
                "T1_model_s": tot1, "peak_level_new": max(full)}
         row["memory"] = memory_plan(n, distinct)
         for lat in dcm.LATENCIES:
-            m = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat)
+            m = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist)
             row.setdefault("T_N_ms", []).append(round(m["T_N_ms"], 1))
             row.setdefault("speedup", []).append(round(m["speedup"], 2))
             row.setdefault("rate_G_per_s", []).append(round(distinct / m["T_N_ms"] / 1e6, 2))
