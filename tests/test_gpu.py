@@ -86,9 +86,8 @@ print(json.dumps(out))
 
 def test_many_launches_per_level_keep_every_count(tmp_path):
     """Levels cut into many equal launches (RMC_LAUNCH_LOG2=16: launches of at
-    most 65,536 states), each drained by dynamic per-wave work units: every
-    per-level count of three golden models (levels of up to 0.15-0.6 M states)
-    is unchanged."""
+    most 65,536 states): every per-level count of three golden models (levels
+    of up to 0.09-0.24 M new states) is unchanged."""
     import subprocess
     script = tmp_path / "small_launches.py"
     script.write_text(SMALL_LAUNCHES)
@@ -99,7 +98,10 @@ def test_many_launches_per_level_keep_every_count(tmp_path):
     out = json.loads(r.stdout.strip().splitlines()[-1])
     for name, (lv, d, gen, dep, launches) in out.items():
         assert lv and d and gen and dep, name
-        assert launches > GOLDEN[name]["depth"], (name, launches)  # some level took several launches
+        # every expanded level in launches of at most 2^16 states (bounded_prefix14's one
+        # larger level is its last, never expanded)
+        assert launches >= sum(-(-x // 65536) for x in GOLDEN[name]["level_new"][:-1]), (name, launches)
+    assert out["small"][4] > GOLDEN["small"]["depth"] and out["tiny2_v2"][4] > GOLDEN["tiny2_v2"]["depth"]
 
 
 @pytest.mark.parametrize("prefix", ["bench_prefix22", "bench_prefix24"])
