@@ -1118,11 +1118,11 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0, int PI = 0>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, PI, false, true, DYN>(P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1724,7 +1724,10 @@ static int expand_variant() {
 // 299-304 ms for 0 at one rank, profiles/r04/ab/dist_kvariant_*; 5 probes at 6
 // waves without parent mixes, the single-GPU default's shape, spills 48 B here:
 // 305-307 ms, removed; 2 with dynamic per-wave units: 300-307 vs 298-305 ms on
-// two boxes, profiles/r04/ab/dist_kvariant_2_3_*, removed).
+// two boxes, profiles/r04/ab/dist_kvariant_2_3_*, removed; with the owner found
+// at flush time, the single-GPU kernel's shape (5 probes, 6 waves, mixes
+// recomputed; 80 B of scratch here) 296-297 ms, with early probe loads 289-291,
+// against 282-283 ms for 2, profiles/r04/ab/dist_kvariant_2_4_6_r04z.txt, removed).
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
@@ -1803,23 +1806,11 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
-        } else if (dist_kvariant() >= 2 && dist_kvariant() <= 6 && SORTED && B.word) {
-            // presorted windows: 2 6 probes in flight at 5 waves/SIMD with the parent's
-            // mixes held; 4 (5) the single-GPU kernel's shape, 5 probes at 6 waves
-            // with the mixes recomputed (and dynamic per-wave units); 6 = 4 with the
-            // probe loads issued during the lane code, as the single-GPU kernel does
-#define RMC_DPS(BT, WPE, PRE, DYN, PI)                                                                       \
-    {                                                                                                        \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN, PI>)); \
-        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
-        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
-        RMC_EXPAND_LAUNCH((k_expand_dist<S, K, BT, false, true, WPE, PRE, DYN, PI>));                        \
-    }
-            if (dist_kvariant() == 4) RMC_DPS(5, 6, false, 0, 0)
-            else if (dist_kvariant() == 5) RMC_DPS(5, 6, false, 1, 0)
-            else if (dist_kvariant() == 6) RMC_DPS(5, 6, false, 0, (K <= 4 ? 1 : 0))
-            else RMC_DPS(6, 5, true, 0, 0)
-#undef RMC_DPS
+        } else if (dist_kvariant() == 2 && SORTED && B.word) {  // presorted, 6 probes in flight, 5 waves/SIMD
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
