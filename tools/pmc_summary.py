@@ -37,9 +37,10 @@ def main():
                 "avg_us": float(row["AverageNs"]) / 1e3 if ns else float(row["AverageUs"]),
                 "total_ms": float(row["TotalDurationNs"]) / 1e6 if ns else float(row["TotalDurationUs"]) / 1e3,
                 "pct": float(row["Percentage"])}
-    exp = [k for k in tot if "k_expand_sort" in k]
+    kname = os.environ.get("PMC_KERNEL", "k_expand_sort")  # k_expand_dist for the sharded path
+    exp = [k for k in tot if kname in k and "true, false" not in k.split("<")[-1][:20]]
     if not exp:
-        sys.exit("no k_expand_sort counters in " + src)
+        sys.exit("no " + kname + " counters in " + src)
     k = exp[0]
     c = tot[k]
     n = c["FETCH_SIZE"]["launches"]
@@ -47,7 +48,7 @@ def main():
     wo = [x for x in tot if "k_window_order" in x]
     wo_b = ((tot[wo[0]]["FETCH_SIZE"]["total"] + tot[wo[0]]["WRITE_SIZE"]["total"]) * 1024.0
             if wo and "FETCH_SIZE" in tot[wo[0]] else None)
-    kt = next((v for kk, v in kavg.items() if "k_expand_sort" in kk), None)
+    kt = next((v for kk, v in kavg.items() if kname in kk and "<3, 4, 8, true" not in kk), None)
     traffic = {
         "command": "tools/gpu/pmc.sh: rocprofv3 --kernel-trace --stats, then one --pmc pass per counter group "
                    "(FETCH_SIZE | WRITE_SIZE | SQ instruction mix | SQ waits | LDS) -- python3 bench.py --steps 1 "
