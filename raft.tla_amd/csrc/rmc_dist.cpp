@@ -337,7 +337,6 @@ void free_dist(rmc_ctx* c) {
     if (D.xs) (void)hipStreamSynchronize(D.xs);
     (void)hipFree(c->B.sent);
     (void)hipFree(c->B.ovf);
-    (void)hipFree(c->B.pend);
     for (auto& S : D.set) {
         (void)hipFree(S.key_out);
         (void)hipFree(S.tick_out);
@@ -375,7 +374,6 @@ void free_dist(rmc_ctx* c) {
     if (D.xs) (void)hipStreamDestroy(D.xs);
     c->B.sent = nullptr; c->B.key_out = nullptr; c->B.tick_out = nullptr; c->B.ocount = nullptr;
     c->B.st_out = nullptr; c->B.scount = nullptr; c->B.ovf = nullptr; c->B.ovf_cap = 0;
-    c->B.pend = nullptr; c->B.pend_cap = 0;
     D.key_in = nullptr; D.rep_out = nullptr; D.rep_in = nullptr; D.st_in = nullptr; D.sa = nullptr; D.h_sa = nullptr;
     D.ag_dev = nullptr;
     D.ag_cap = 0;
@@ -441,9 +439,6 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             if (k.overflow & 2u)
                 return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(r) +
                                                    " (raise keys_per_dest)");
-            if (k.overflow & 32u)
-                return fail(c, RMC_E_CAPACITY, "deferred-flush list full on rank " + std::to_string(r) +
-                                                   " (RMC_DIST_KVARIANT=7/8)");
             if (k.overflow)
                 return fail(c, RMC_E_CAPACITY, "state store full on rank " + std::to_string(r) +
                                                    " (raise rmc_config.state_capacity)");
@@ -925,13 +920,6 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     if (!c->sh.verify && c->sh.sym) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
     const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
     ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
-    // deferred flush (RMC_DIST_KVARIANT=7/8, A/B): the listed successors of one
-    // launch (about one per expanded state; a full list fails the level by name)
-    if (const char* kv = getenv("RMC_DIST_KVARIANT"))
-        if ((atoi(kv) == 7 || atoi(kv) == 8) && !c->sh.verify && !c->sh.sym && c->B.cap <= (1ull << 32)) {
-            ok = ok && hipMalloc(&c->B.pend, (1ull << 26) * 8) == hipSuccess;
-            if (ok) c->B.pend_cap = 1ull << 26;
-        }
     for (auto& S : D.set) {
         ok = ok && hipMalloc(&S.key_out, W * kcap * 8) == hipSuccess && hipMalloc(&S.tick_out, W * kcap * 8) == hipSuccess &&
              hipMalloc(&S.ocount, 8 * W) == hipSuccess && hipMalloc(&S.cx, 8 * (4 * W + 1)) == hipSuccess &&

@@ -25,7 +25,6 @@ struct Counters {
     u64 novf;       // sharded: keys that did not fit their owner's outbox (parked in B.ovf)
     u64 wnext;      // dynamic work units: the next (window, wave slot) of the launch (zeroed by k_window_order)
     u64 walked;     // (state, lane) slots the lane walk visited (RMC_WALK_STATS: lane efficiency = generated / walked)
-    u64 npend;      // sharded, deferred flush (RMC_DIST_KVARIANT=7/8): listed successors in B.pend this launch
 };
 
 struct DevBufs {
@@ -70,10 +69,6 @@ struct DevBufs {
     // canonicalised by k_ties after each expansion launch
     u64* ties;
     u64 tie_cap;
-    // sharded, deferred flush: the expansion lists each new (parent | lane << 56) here
-    // and k_flush_pending stores or ships them after the launch
-    u64* pend;
-    u64 pend_cap;
 };
 
 struct PermTable {

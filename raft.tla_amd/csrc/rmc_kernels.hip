@@ -611,50 +611,6 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
     wave_sync_lds();
 }
 
-// Sharded, deferred flush (RMC_DIST_KVARIANT=7/8): the expansion kernel only
-// appends its listed successors (parent index | lane << 56) to B.pend, one
-// reservation atomic per flush, so it carries none of flush_mark's registers;
-// k_flush_pending runs flush_mark over them after the launch.
-__device__ __forceinline__ void flush_defer(const DevBufs& B, u64 lo, const u32* l_rel, const uint8_t* l_lane,
-                                            u32 n) {
-    wave_sync_lds();
-    const int me = (int)__lane_id();
-    u64 base = 0;
-    if (me == 0) base = atomicAdd((unsigned long long*)&B.ctr->npend, (unsigned long long)n);
-    base = bcast64(base, 0);
-    for (u32 e = (u32)me; e < n; e += 64) {
-        const u64 q = base + e;
-        if (q < B.pend_cap) B.pend[q] = (lo + l_rel[e]) | ((u64)l_lane[e] << 56);
-    }
-    wave_sync_lds();
-}
-
-// Each wave takes chunks of up to WCAP pending successors into LDS and flushes
-// them as the in-kernel flush would (store indices < 2^32: checked on the host).
-template <int S, int K>
-__global__ __launch_bounds__(256) void k_flush_pending(const Params P, const DevBufs B) {
-    __shared__ u32 s_rel[4][WCAP];
-    __shared__ uint8_t s_lane[4][WCAP];
-    __shared__ uint8_t s_dest[4][WCAP];
-    const int wv = (int)(threadIdx.x >> 6);
-    const int me = (int)__lane_id();
-    const u64 np = B.ctr->npend;
-    if (np > B.pend_cap) {  // the list overflowed: reported at the level end, nothing flushed
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&B.ctr->overflow, 32u);
-        return;
-    }
-    const u64 waves = (u64)gridDim.x * 4ull;
-    for (u64 c0 = ((u64)blockIdx.x * 4ull + (u64)wv) * (u64)WCAP; c0 < np; c0 += waves * (u64)WCAP) {
-        const u32 cnt = (u32)((np - c0) < (u64)WCAP ? (np - c0) : (u64)WCAP);
-        for (u32 e = (u32)me; e < cnt; e += 64) {
-            const u64 v = B.pend[c0 + e];
-            s_rel[wv][e] = (u32)(v & ((1ull << 48) - 1));
-            s_lane[wv][e] = (uint8_t)(v >> 56);
-        }
-        flush_mark<S, K>(P, B, 0ull, s_rel[wv], s_lane[wv], s_dest[wv], cnt);
-    }
-}
-
 // Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
 // processed BATCH at a time so BATCH fingerprint probes per thread are in
 // flight together (the kernel is bound by probe latency, not bandwidth).
@@ -676,7 +632,7 @@ __global__ __launch_bounds__(256) void k_flush_pending(const Params P, const Dev
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
           bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
-          int DYN = 0, bool DEFER = false>
+          int DYN = 0>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -1060,7 +1016,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
                         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
-                        else if constexpr (MARK && DEFER) flush_defer(B, lo, l_rel, l_lane, n);
                         else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
                         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
@@ -1078,7 +1033,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     if (n) {
         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
-        else if constexpr (MARK && DEFER) flush_defer(B, lo, l_rel, l_lane, n);
         else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
@@ -1164,12 +1118,11 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool PRE = true, bool DEFER = false>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, PRE, true, true, true, 16, 0, false, true, 0, DEFER>(P, PT, B, lo,
-                                                                                                          hi);
+        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 64)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1858,22 +1811,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
-        } else if ((dist_kvariant() == 7 || dist_kvariant() == 8) && SORTED && B.word && B.pend) {
-            // deferred flush: 7 the single-GPU kernel's shape (5 probes, 6 waves, mixes
-            // recomputed), 8 variant 2's shape; then k_flush_pending over the listed successors
-            if (hipError_t e = hipMemsetAsync(&B.ctr->npend, 0, 8, st)) return e;
-#define RMC_DEF(BT, WPE, PRE)                                                                                \
-    {                                                                                                        \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, BT, false, true, WPE, PRE, true>)); \
-        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
-        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
-        RMC_EXPAND_LAUNCH((k_expand_dist<S, K, BT, false, true, WPE, PRE, true>));                           \
-    }
-            if (dist_kvariant() == 7) RMC_DEF(5, 6, false)
-            else RMC_DEF(6, 5, true)
-#undef RMC_DEF
-            const void* fp = reinterpret_cast<const void*>(&(k_flush_pending<S, K>));
-            hipLaunchKernelGGL((k_flush_pending<S, K>), dim3((unsigned)resident_grid(fp)), dim3(256), 0, st, P, B);
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
