@@ -1727,7 +1727,11 @@ static int expand_variant() {
 // two boxes, profiles/r04/ab/dist_kvariant_2_3_*, removed; with the owner found
 // at flush time, the single-GPU kernel's shape (5 probes, 6 waves, mixes
 // recomputed; 80 B of scratch here) 296-297 ms, with early probe loads 289-291,
-// against 282-283 ms for 2, profiles/r04/ab/dist_kvariant_2_4_6_r04z.txt, removed).
+// against 282-283 ms for 2, profiles/r04/ab/dist_kvariant_2_4_6_r04z.txt, removed;
+// the flush deferred to a kernel after the launch (the expansion only lists new
+// successors: 80 VGPRs, no scratch, 6 waves) 283-286 vs 282-286 ms, the parents
+// re-read cold by the separate pass, profiles/r04/ab/dist_deferred_flush_r04h.txt,
+// removed).
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
