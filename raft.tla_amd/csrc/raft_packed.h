@@ -123,8 +123,8 @@ struct Params {
                     // capacity, and a successor beyond it is an error (capacity_exceeded), not filtered
     u64 fp_mask;  // full-state verification mode: fingerprint bits kept (~0 = all; fewer only
                   // to provoke collisions in tests, rmc_set_fp_bits)
-    u32 ldesc[64];  // per-lane descriptor for lanes < 64 (lane_desc): family | index in family << 4 |
-                    // acting server << 12 (7: none or per message); filled by fill_lane_desc
+    u32 ldesc[128];  // per-lane descriptor (lane_desc; every shape has < 128 lanes): family | index in
+                     // family << 4 | acting server << 12 (7: none or per message); filled by fill_lane_desc
 };
 
 // Lane table: Restart S, Timeout S, RequestVote S^2,
@@ -461,7 +461,7 @@ RMC_HD void lane_delta(const u64 (&w)[S], const u32 (&m)[K], int lane, const Par
     }
 }
 
-// The same from a lane descriptor (Params.ldesc, lanes < 64: lane_desc).
+// The same from a lane descriptor (Params.ldesc: lane_desc).
 template <int S, int K>
 RMC_HD void lane_delta_desc(const u64 (&w)[S], const u32 (&m)[K], u32 desc, const Params& P, Delta& d) {
     const int fam = (int)(desc & 15u), t = (int)((desc >> 4) & 255u);
@@ -619,27 +619,43 @@ RMC_HD u32 state_class_fine(const u64 (&w)[S], const u32 (&m)[K]) {
     if constexpr (S <= 3) return c * 9u + (u32)(nmsg < 8 ? nmsg : 8);  // <= 242
     return c | ((u32)(nmsg < 3 ? nmsg : 3) << (S + 1));                 // S + 3 <= 8 bits
 }
+// A set of lanes (every shape has fewer than 128): bit l of lo (l < 64) or of hi.
+struct LaneMask {
+    u64 lo, hi;
+    RMC_HD bool has(int l) const { return l < 64 ? ((lo >> l) & 1ull) != 0 : ((hi >> (l - 64)) & 1ull) != 0; }
+    // OR in `bits` shifted left by sh (sh and the bits' width are compile-time in the callers)
+    RMC_HD void put(u64 bits, int sh) {
+        if (sh < 64) {
+            lo |= bits << sh;
+            if (sh > 0) hi |= bits >> (64 - sh);
+        } else {
+            hi |= bits << (sh - 64);
+        }
+    }
+};
 template <int S, int K>
-RMC_HD u64 lane_superset(const u64 (&w)[S], const u32 (&m)[K], int V) {
+RMC_HD LaneMask lane_superset(const u64 (&w)[S], const u32 (&m)[K], int V) {
     typedef Lanes<S, K> L;
-    static_assert(L::N <= 64, "lane mask needs <= 64 lanes");
+    static_assert(L::N <= 128, "lane mask holds < 128 lanes");
     // constant expressions: off() is recursive, so a plain call is not folded
     constexpr int O1 = L::off(1), O2 = L::off(2), O3 = L::off(3), O4 = L::off(4), O5 = L::off(5), O6 = L::off(6),
                   O7 = L::off(7), O8 = L::off(8), O9 = L::off(9);
     constexpr u64 SM = (1ull << S) - 1;
-    u64 mk = SM;  // Restart(i): always enabled
+    LaneMask mk{SM, 0ull};  // Restart(i): always enabled
 #pragma unroll
     for (int i = 0; i < S; ++i) {
         const u32 st = w_st(w[i]);
-        if (st != LEADER) mk |= 1ull << (O1 + i);                               // Timeout
-        if (st == CANDIDATE) mk |= (SM << (O2 + i * S)) | (1ull << (O3 + i));  // RequestVote, BecomeLeader
-        if (st == LEADER)
-            mk |= (((1ull << V) - 1) << (O4 + i * VMAX)) | (1ull << (O5 + i)) |  // ClientRequest, AdvanceCommitIndex
-                  (SM << (O6 + i * S));                                        // AppendEntries
+        if (st != LEADER) mk.put(1ull, O1 + i);                                   // Timeout
+        if (st == CANDIDATE) { mk.put(SM, O2 + i * S); mk.put(1ull, O3 + i); }    // RequestVote, BecomeLeader
+        if (st == LEADER) {  // ClientRequest, AdvanceCommitIndex, AppendEntries
+            mk.put((1ull << V) - 1, O4 + i * VMAX);
+            mk.put(1ull, O5 + i);
+            mk.put(SM, O6 + i * S);
+        }
     }
 #pragma unroll
     for (int q = 0; q < K; ++q)
-        if (m[q]) mk |= (1ull << (O7 + q)) | (1ull << (O8 + q)) | (1ull << (O9 + q));
+        if (m[q]) { mk.put(1ull, O7 + q); mk.put(1ull, O8 + q); mk.put(1ull, O9 + q); }
     return mk;
 }
 
@@ -798,7 +814,7 @@ RMC_HD u64 make_foot(const u32 (&m)[K], int lane, const Delta& d, const Params& 
     return f;
 }
 
-// make_foot from lane a's descriptor (lanes < 64: no family-offset compares).
+// make_foot from lane a's descriptor (no family-offset compares).
 template <int S, int K>
 RMC_HD u64 make_foot_desc(const u32 (&m)[K], u32 desc, const Delta& d) {
     u64 f = FOOT_VALID;
@@ -841,15 +857,16 @@ RMC_HD u32 lane_desc(const Params& P, int lane, int S) {
     return (u32)f | ((u32)t << 4) | ((u32)srv << 12) | ((u32)(i & 15) << 16) | ((u32)(j & 15) << 20);
 }
 RMC_HD void fill_lane_desc(Params& P, int S) {
-    for (int l = 0; l < 64; ++l) P.ldesc[l] = l < P.off[10] ? lane_desc(P, l, S) : 0u;
+    for (int l = 0; l < 128; ++l) P.ldesc[l] = l < P.off[10] ? lane_desc(P, l, S) : 0u;
 }
 
 // Per expanded state: a's side of the test (lane a = act, its footprint),
 // packed into 4 words (it is live across the whole lane walk).
 // Instance order key (0 = none): lanes of families 0-6 by (family, lane),
-// message lanes by (family, message): 1 + (f << 6 | lane) < 2^30 <= (f - 6) << 30 | msg.
+// message lanes by (family, message): 1 + (f << 7 | lane) < 2^30 <= (f - 6) << 30 | msg
+// (injective: every shape has fewer than 128 lanes).
 RMC_HD u32 diamond_order(int f, int lane, u32 msg) {
-    return f < 7 ? 1u + (((u32)f << 6) | (u32)lane) : (((u32)(f - 6)) << 30) | msg;
+    return f < 7 ? 1u + (((u32)f << 7) | (u32)lane) : (((u32)(f - 6)) << 30) | msg;
 }
 struct Diamond {
     u32 ord;     // a's instance order key; 0 = no skipping from this state
@@ -880,7 +897,7 @@ RMC_HD bool diamond_rest(int sb, u32 mb, const Delta& db, int nmsg_b, const Diam
     if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
     return nmsg_b <= (int)(dm.sd >> 8);
 }
-// b's side from lane b's descriptor (lanes < 64): the same test as diamond_skip.
+// b's side from lane b's descriptor: the same test as diamond_skip.
 template <int S, int K>
 RMC_HD bool diamond_skip_desc(const u32 (&m)[K], int b, u32 desc, const Delta& db, int nmsg_b, const Diamond& dm) {
     const int fb = (int)(desc & 15u), tb = (int)((desc >> 4) & 255u), sd = (int)((desc >> 12) & 7u);

@@ -37,9 +37,9 @@ struct WEnt {
 // One message record (raft.tla:443-475): 8 + 2 LW bytes, fields a type does not use 0.
 struct alignas(8) WMsg {
     uint8_t type, term, src, dst;  // mtype, mterm, msource, mdest
-    int8_t a;    // RVQ mlastLogTerm | RVP mvoteGranted | AEQ mprevLogIndex (-1: Smokeraft.tla:35) | AEP msuccess
-    uint8_t b;   // RVQ mlastLogIndex | AEQ mprevLogTerm | AEP mmatchIndex
-    uint8_t c;   // AEQ mcommitIndex
+    int8_t a;    // RVP mvoteGranted | AEQ mprevLogIndex (-1: Smokeraft.tla:35) | AEP msuccess
+    uint8_t b;   // RVQ mlastLogTerm | AEQ mprevLogTerm | AEP mmatchIndex (unsigned: terms up to TMAX)
+    uint8_t c;   // RVQ mlastLogIndex | AEQ mcommitIndex
     uint8_t n;   // AEQ Len(mentries) (<= 1) | RVP Len(mlog)
     WEnt e[LW];  // AEQ mentries | RVP mlog (= log[i], raft.tla:259)
 };
@@ -146,6 +146,14 @@ RMC_HD int wbag_fits(const WState& s, const WMsg& m) {
         if (wmsg_cmp(s.msg[k], m) == 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
     return s.nmsg >= KW ? W_MSGS : W_ON;
 }
+// Would Reply(r, s.msg[x]) (raft.tla:102-103: add the response, remove the
+// request) fit?  The capacity is that of the resulting bag: a request with count
+// 1 frees its slot (r never equals a request: the types differ).
+RMC_HD int wreply_fits(const WState& s, const WMsg& r, int x) {
+    for (int k = 0; k < s.nmsg; ++k)
+        if (wmsg_cmp(s.msg[k], r) == 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
+    return (s.nmsg >= KW && s.cnt[x] > 1) ? W_MSGS : W_ON;
+}
 // Bag (+) SetToBag({m}) (raft.tla:88), kept sorted (call after wbag_fits).
 RMC_HD int wbag_add(WState& s, const WMsg& m) {
     int k = 0;
@@ -179,13 +187,6 @@ RMC_HD void wbag_remove_at(WState& s, int k) {
     s.nmsg -= 1;
     wmsg_zero(s.msg[s.nmsg]);
     s.cnt[s.nmsg] = 0;
-}
-RMC_HD void wbag_remove(WState& s, const WMsg& m) {
-    for (int k = 0; k < s.nmsg; ++k)
-        if (wmsg_cmp(s.msg[k], m) == 0) {
-            wbag_remove_at(s, k);
-            return;
-        }
 }
 
 // Lane `lane` on s (raft.tla:136-417, one action instance): W_OFF when the
@@ -231,8 +232,8 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
         wmsg_zero(m);
         m.type = RVQ;
         m.term = s.ct[i];
-        m.a = (int8_t)wlast_term(s, i);
-        m.b = s.len[i];
+        m.b = (uint8_t)wlast_term(s, i);
+        m.c = s.len[i];
         m.src = (uint8_t)i;
         m.dst = (uint8_t)j;
         const int fit = wbag_fits(s, m);
@@ -317,7 +318,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
         }
         if (m.type == RVQ) {  // HandleRequestVoteRequest :244-263
             const int lt = wlast_term(s, i);
-            const int logok = m.a > lt || (m.a == lt && m.b >= s.len[i]);
+            const int logok = m.b > lt || (m.b == lt && m.c >= s.len[i]);
             const int grant = m.term == ct && logok && (s.vf[i] == NIL || s.vf[i] == j);
             WMsg r;
             wmsg_zero(r);
@@ -328,13 +329,13 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
             r.a = (int8_t)grant;
             r.n = s.len[i];
             for (int e = 0; e < s.len[i]; ++e) r.e[e] = s.log[i][e];
-            const int fit = wbag_fits(s, r);  // Reply :102-103: add the response, then remove the request
+            // Reply :102-103 (response added, request removed): the capacity of the net bag
+            const int fit = wreply_fits(s, r, x);
             if (fit != W_ON || !t) return fit;
-            const WMsg q = m;
             if (!pre) wcopy_state(*t, s);
             if (grant) t->vf[i] = (uint8_t)j;
+            wbag_remove_at(*t, x);
             wbag_add(*t, r);
-            wbag_remove(*t, q);
             return W_ON;
         }
         if (m.type == RVP) {
@@ -357,12 +358,11 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
             r.src = (uint8_t)i;
             r.dst = (uint8_t)j;
             if (m.term < ct || (s.st[i] == FOLLOWER && !logok)) {  // Reject :281-293
-                const int fit = wbag_fits(s, r);
+                const int fit = wreply_fits(s, r, x);
                 if (fit != W_ON || !t) return fit;
-                const WMsg q = m;
                 if (!pre) wcopy_state(*t, s);
+                wbag_remove_at(*t, x);
                 wbag_add(*t, r);
-                wbag_remove(*t, q);
                 return W_ON;
             }
             if (s.st[i] == CANDIDATE) {  // ReturnToFollowerState :295-299 — m stays
@@ -379,12 +379,11 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
                 if (m.c != s.ci[i]) return W_OFF;
                 r.a = 1;
                 r.b = (uint8_t)(pidx + m.n);
-                const int fit = wbag_fits(s, r);
+                const int fit = wreply_fits(s, r, x);
                 if (fit != W_ON || !t) return fit;
-                const WMsg q = m;
                 if (!pre) wcopy_state(*t, s);
+                wbag_remove_at(*t, x);
                 wbag_add(*t, r);
-                wbag_remove(*t, q);
                 return W_ON;
             }
             if (len >= index) {  // ConflictAppendEntriesRequest :319-325 — drops the LAST entry, m stays
@@ -504,7 +503,7 @@ RMC_HD int wcheck_invariants(const WModel& M, const WState& s) {
                 if (!(ld > ls || (ld == ls && s.len[dst] >= s.len[src]))) return 4;
             }
             if (m.type == RVQ && s.st[src] == CANDIDATE && cs == m.term)  // :915-920
-                if (m.b != s.len[src] || m.a != wlast_term(s, src)) return 4;
+                if (m.c != s.len[src] || m.b != wlast_term(s, src)) return 4;
             if (m.type == AEQ && m.n > 0 && m.term == cs) {  // :924-930
                 const int p = m.a;
                 if (p + 1 < 1 || p + 1 > s.len[src]) return 4;

@@ -27,7 +27,8 @@ struct DistState {
     struct Set {
         rmc::u64* key_out = nullptr;             // [world][kcap] keys per owner
         rmc::u64* tick_out = nullptr;            // [world][kcap] tickets (parent | lane << 56)
-        unsigned long long* ocount = nullptr;    // [world] keys written per owner
+        unsigned long long* ocount = nullptr;    // [world] keys written per owner, [world]: pool records
+        rmc::u32* pool = nullptr;                // remote-successor pool (phase-2 records, flush_pool)
         rmc::u64* cx = nullptr;                  // device count row: [2W + 1] sent, [2W] received
         rmc::u64* h_cx = nullptr;                // pinned copy of cx
         hipEvent_t ev_exp = nullptr;             // expansion (or drain) of this set's round done
@@ -50,6 +51,7 @@ struct DistState {
     rmc::u64 ag_cap = 0;            // (world + 1) x ag_cap bytes, allocated once per shard
     std::vector<uint8_t> stage_send, stage_recv;  // host transport staging
     rmc::u64 sent_slots = 0;
+    rmc::u64 pool_cap = 0;          // records per pool (one pool per outbox set)
     int debug = 0;                  // RMC_DIST_DEBUG: one stderr line per round
     int table_grown = 0;            // rmc_shard doubled the fingerprint set once (send markers)
     int split = 2;                  // RMC_DIST_SPLIT: rounds a large level is cut into at least (1 at world 1)

@@ -75,15 +75,16 @@ bool abort_bounded(ncclComm_t comm) {
     return done->load() != 0;
 }
 
-int deadline_fail(rmc_ctx* c, const char* what) {
+// pending: the caller left a communicator it could not abort (communicator init).
+int deadline_fail(rmc_ctx* c, const char* what, int pending = 0) {
     DistState& D = c->dist;
     D.aborted = 1;
-    bool aborted = true;
+    bool aborted = !pending;
     if (D.rccl && D.comm) {
         aborted = abort_bounded(D.comm);
         D.comm = nullptr;
-        D.abort_pending = aborted ? 0 : 1;
     }
+    if (D.rccl) D.abort_pending = aborted ? 0 : 1;
     char t[32];
     snprintf(t, sizeof t, "%g", D.timeout_s);
     return fail(c, RMC_E_HIP, std::string("sharded search: ") + what + " did not complete within the " + t +
@@ -341,6 +342,7 @@ void free_dist(rmc_ctx* c) {
         (void)hipFree(S.key_out);
         (void)hipFree(S.tick_out);
         (void)hipFree(S.ocount);
+        (void)hipFree(S.pool);
         (void)hipFree(S.cx);
         if (S.h_cx) (void)hipHostFree(S.h_cx);
         for (hipEvent_t* e : {&S.ev_exp, &S.ev_free, &S.k0, &S.k1, &S.x0, &S.x1})
@@ -424,9 +426,13 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     }
     std::vector<Counters> rows((size_t)W);
     // level end: the all-gathered device counters; errors stop every rank alike
+    bool rows_final = false;  // the level's last count row carried every rank's final counters
     auto level_end = [&]() -> int {
         D.phase = "level end (counter all-gather)";
-        if (int rc = allgather_counters(c, rows.data())) return rc;
+        if (!rows_final) {
+            if (int rc = allgather_counters(c, rows.data())) return rc;
+        }
+        rows_final = false;
         *c->h_ctr = rows[(size_t)me];
         for (int r = 0; r < W; ++r) {
             const Counters& k = rows[(size_t)r];
@@ -485,16 +491,19 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     }
     u64 generated = resume ? saved.generated : 1, probes = resume ? saved.probes : 0;
     int depth = resume ? c->resume_depth : 1;
-    // Replicated levels: the plain kernel on shapes of <= 64 lanes, models
-    // with a CONSTRAINT on every field (the capacity pass reads the store)
-    const bool rep_ok = !verify && !c->sh.sym && c->P.off[10] <= 64 && !c->P.unbounded && D.rep_max > 0;
+    // Replicated levels: the plain kernel (every shape), models with a
+    // CONSTRAINT on every field (the capacity pass reads the store)
+    const bool rep_ok = !verify && !c->sh.sym && !c->P.unbounded && D.rep_max > 0;
     // Round sizing: rho = most keys one round sends one owner, per expanded
     // state, from the previous rounds (it varies along a frontier: states
     // received from other ranks are appended after the local ones).  A round
     // aims at an outbox half full; what does not fit is parked, not lost.
     double rho = 1.0;
     u64 vpub = c->h_ctr->count;  // verification: states [0, vpub) are published (slot -> index)
-    const u64 row_len = 4 * (u64)W + 1;  // cx: [2W] sent pairs, [1] novf, [2W] received pairs
+    // cx: [W] sent blocks of kRowWords, [1] novf, [W] received blocks (count, flags, counters)
+    const u64 RWD = (u64)kRowWords;
+    const u64 row_len = 2 * RWD * (u64)W + 1;
+    auto rx = [&](const u64* cx, int p) { return cx + RWD * (u64)W + 1 + RWD * (u64)p; };  // block from p
     while (!c->have_target) {
         const u64 lo = c->level_start[(size_t)depth - 1], hi = c->level_start[(size_t)depth];
         D.lvl = depth;
@@ -546,11 +555,14 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         auto enqueue_A = [&](u64 k) -> int {
             DistState::Set& S = D.set[k & 1];
             HIPCHK(c, hipStreamWaitEvent(c->st, S.ev_free, 0));
-            HIPCHK(c, hipMemsetAsync(S.ocount, 0, 8 * (u64)W, c->st));
+            HIPCHK(c, hipMemsetAsync(S.ocount, 0, 8 * (u64)(W + 1), c->st));
             DevBufs Bb = c->B;
             Bb.key_out = S.key_out;
             Bb.tick_out = S.tick_out;
             Bb.ocount = S.ocount;
+            Bb.pool = S.pool;
+            Bb.npool = S.ocount + W;
+            Bb.pool_cap = D.pool_cap;
             round_states[k & 1] = 0;
             round_kind[k & 1] = 0;
             S.timed = 0;
@@ -568,6 +580,9 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 const u64 n = (rest + nr - 1) / nr;
                 HIPCHK(c, hipEventRecord(S.k0, c->st));
                 HIPCHK(c, launch(c->sh, 3, c->P, c->PT, Bb, cursor, cursor + n, nullptr, nullptr, 0, nullptr, c->st));
+                // the pool flush's remote successors: keyed and routed to the outboxes
+                if (W > 1 && !verify && !c->sh.sym)
+                    HIPCHK(c, launch(c->sh, 14, c->P, c->PT, Bb, 0, 0, nullptr, nullptr, 0, nullptr, c->st));
                 HIPCHK(c, hipEventRecord(S.k1, c->st));
                 S.timed = 1;
                 c->res.expand_launches += 1;
@@ -606,7 +621,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 Bb.ocount = S.ocount;
                 HIPCHK(c, launch_pack_counts(Bb, host_more ? 1ull : 0ull, ovf_done, S.cx, D.xs));
             }
-            if (int rc = a2a_u64(c, S.cx, S.cx + 2 * W + 1, 2)) return rc;
+            if (int rc = a2a_u64(c, S.cx, S.cx + RWD * (u64)W + 1, RWD)) return rc;
             HIPCHK(c, hipMemcpyAsync(S.h_cx, S.cx, row_len * 8, hipMemcpyDeviceToHost, D.xs));
             HIPCHK(c, hipEventRecord(D.ev_cnt, D.xs));
             // the next round's expansion is queued before waiting, so the GPU
@@ -621,24 +636,25 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             // a rank whose parking buffer overflowed says so in its flags (bit 1):
             // every rank sees every row and stops here alike
             for (int p = 0; p < W; ++p)
-                if (cx[2 * W + 1 + 2 * p + 1] & 2u)
+                if (rx(cx, p)[1] & 2u)
                     return fail(c, RMC_E_CAPACITY, "exchange parking buffer full on rank " + std::to_string(p) +
                                                        " (raise keys_per_dest) at " + where(c));
-            const u64 novf = std::min(cx[2 * W], c->B.ovf_cap);  // never drain past the buffer
+            const u64 novf = std::min(cx[RWD * (u64)W], c->B.ovf_cap);  // never drain past the buffer
             const u64 newly_parked = novf - std::min(novf, ovf_known);
             D.parked += newly_parked;
             ovf_known = std::max(ovf_known, novf);
-            bool global_more = false;
+            bool global_more = false, global_sends = false;
             u64 mx = 0, tot_in = 0;
             for (int p = 0; p < W; ++p) {
-                global_more |= (cx[2 * W + 1 + 2 * p + 1] & 1u) != 0;
-                scnt[(size_t)p] = cx[2 * p] * 8;
+                global_more |= (rx(cx, p)[1] & 1u) != 0;
+                global_sends |= (rx(cx, p)[1] & 4u) != 0;
+                scnt[(size_t)p] = cx[RWD * (u64)p] * 8;
                 soff[(size_t)p] = (u64)p * kcap * 8;
-                rcnt[(size_t)p] = cx[2 * W + 1 + 2 * p] * 8;
+                rcnt[(size_t)p] = rx(cx, p)[0] * 8;
                 roff[(size_t)p] = tot_in * 8;
-                tot_in += cx[2 * W + 1 + 2 * p];
-                mx = std::max(mx, cx[2 * p]);
-                D.keys_sent += cx[2 * p];
+                tot_in += rx(cx, p)[0];
+                mx = std::max(mx, cx[RWD * (u64)p]);
+                D.keys_sent += cx[RWD * (u64)p];
             }
             if (S.timed) {
                 c->res.expand_kernel_seconds += 1e-3 * elapsed_ms(S.k0, S.k1);
@@ -673,7 +689,16 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 HIPCHK(c, hipEventRecord(S.x1, D.xs));
                 S.xtimed = 1;
                 D.chunks += 1;
-                if (!global_more) break;
+                if (!global_more) {
+                    // the level's last round and no rank sent keys in it: nothing
+                    // changes a counter after its count row, so the rows carry
+                    // every rank's final counters — no level-end all-gather
+                    if (!global_sends && !verify) {
+                        for (int p = 0; p < W; ++p) memcpy(&rows[(size_t)p], rx(cx, p) + 2, sizeof(Counters));
+                        rows_final = true;
+                    }
+                    break;
+                }
                 continue;
             }
             // ---- phase 1: keys to their owners, replies back; phase 2 sizes
@@ -697,6 +722,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 Bb.key_out = S.key_out;
                 Bb.tick_out = S.tick_out;
                 Bb.ocount = S.ocount;
+                Bb.pool = S.pool;  // tickets POOL_TICK | index name this set's pool records
                 HIPCHK(c, launch(c->sh, 8, c->P, c->PT, Bb, mx, 0, reinterpret_cast<const u32*>(D.rep_in), nullptr, 0,
                                  nullptr, D.xs));
             }
@@ -709,7 +735,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             u64 tot_st = 0;
             for (int p = 0; p < W; ++p) {
                 // verification ships every key's state (the seen ones to be compared)
-                const u64 ns = D.h_sa[p], nr = verify ? cx[2 * W + 1 + 2 * p] : D.h_sa[W + p];
+                const u64 ns = D.h_sa[p], nr = verify ? rx(cx, p)[0] : D.h_sa[W + p];
                 if (p != me && ns > kcap) return fail(c, RMC_E_HIP, "phase 2: more accepted states than keys sent");
                 soff[(size_t)p] = (u64)p * kcap * RB;
                 scnt[(size_t)p] = p == me ? 0 : ns * RB;
@@ -920,10 +946,14 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     if (!c->sh.verify && c->sh.sym) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
     const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
     ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
+    // the pool flush's remote successors of one round: as many as the round's
+    // outboxes hold (a fuller pool parks tickets); none leave a world of one
+    D.pool_cap = world > 1 ? W * kcap : 64;
     for (auto& S : D.set) {
         ok = ok && hipMalloc(&S.key_out, W * kcap * 8) == hipSuccess && hipMalloc(&S.tick_out, W * kcap * 8) == hipSuccess &&
-             hipMalloc(&S.ocount, 8 * W) == hipSuccess && hipMalloc(&S.cx, 8 * (4 * W + 1)) == hipSuccess &&
-             hipHostMalloc(&S.h_cx, 8 * (4 * W + 1), hipHostMallocDefault) == hipSuccess;
+             hipMalloc(&S.ocount, 8 * (W + 1)) == hipSuccess && hipMalloc(&S.cx, 8 * (2 * kRowWords * W + 1)) == hipSuccess &&
+             hipMalloc(&S.pool, D.pool_cap * RB) == hipSuccess &&
+             hipHostMalloc(&S.h_cx, 8 * (2 * kRowWords * W + 1), hipHostMallocDefault) == hipSuccess;
         for (hipEvent_t* e : {&S.ev_exp, &S.ev_free})
             ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
         for (hipEvent_t* e : {&S.k0, &S.k1, &S.x0, &S.x1}) ok = ok && hipEventCreate(e) == hipSuccess;
@@ -1011,10 +1041,12 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
         // lives until it is complete (RCCL's group state of a call is the calling
         // thread's), waited for here under the deadline: the call does not
         // promise to return at once for every bootstrap state (a peer that never
-        // connects).  On expiry the communicator, once the call has returned it,
-        // is aborted (bounded); a call that never returns is left to the process exit.
+        // connects).  On expiry the helper, which owns the communicator, aborts it
+        // itself once it leaves its poll loop (no other thread frees it while the
+        // helper may still be polling it); this thread waits for that, bounded
+        // (kAbortWait), and a call that never returns is left to the process exit.
         struct Init {
-            std::atomic<int> done{0}, quit{0};
+            std::atomic<int> done{0}, quit{0}, aborted{0};
             std::atomic<ncclComm_t> comm{nullptr};
             ncclResult_t r = ncclSuccess;
         };
@@ -1032,6 +1064,10 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
                 r = a;
                 if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(50));
             }
+            if (in->quit.load() && cm) {  // the waiting thread gave up: the owner aborts
+                (void)ncclCommAbort(cm);
+                in->aborted.store(1);
+            }
             in->r = r;
             in->done.store(1);
         }).detach();
@@ -1039,9 +1075,21 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
         while (!in->done.load()) {
             if (now_s() - t_init > D.timeout_s) {
                 in->quit.store(1);
-                D.comm = in->comm.load();  // aborted (bounded) by deadline_fail when the call returned it
-                const int rc = deadline_fail(c, D.comm ? "ncclCommInitRankConfig (waiting for every rank)"
-                                                       : "ncclCommInitRankConfig (the call has not returned)");
+                const double t_q = now_s();
+                while (!in->done.load() && now_s() - t_q < kAbortWait)
+                    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                const bool returned = in->comm.load() != nullptr;
+                bool aborted = in->aborted.load() != 0;
+                if (in->done.load() && !aborted && returned) {
+                    // the helper completed the init just before it saw quit: it has
+                    // left the communicator, so it is aborted here
+                    aborted = abort_bounded(in->comm.load());
+                }
+                D.comm = nullptr;  // never touched again by this thread
+                const int rc = deadline_fail(c,
+                                             returned ? "ncclCommInitRankConfig (waiting for every rank)"
+                                                      : "ncclCommInitRankConfig (the call has not returned)",
+                                             !returned || aborted ? 0 : 1);
                 const std::string msg = c->err;
                 free_dist(c);
                 c->err = msg;

@@ -46,16 +46,24 @@ struct DevBufs {
     u64 smask;                 // sent-cache slots - 1
     // two-phase exchange: phase 1 keys, phase 2 accepted states
     u64* key_out;              // [world][kcap] keys for each owner
-    u64* tick_out;             // [world][kcap] local tickets: parent index | lane << 56
+    u64* tick_out;             // [world][kcap] local tickets: parent index | lane << 56, or POOL_TICK | pool index
     u64 kcap;                  // keys per destination and chunk
     unsigned long long* ocount;  // [world] keys written per destination
     u32* st_out;               // [world][scap][NW + 4] accepted states for each owner (+ ref, footprint)
     u64 scap;                  // state records per destination and round (= kcap)
     unsigned long long* scount;  // [world] state records written per destination
     // keys whose owner's outbox was full: {key, parent index | dest << 48 | lane << 56},
-    // sent in later exchange rounds of the same level (never dropped)
+    // sent in later exchange rounds of the same level (never dropped); key 0: a
+    // successor the expansion could not put in the pool, keyed by k_route
     u64* ovf;
     u64 ovf_cap;               // records in ovf
+    // remote-successor pool (the sharded expansion's default flush, flush_pool):
+    // every new successor owned by another rank, materialised once as its
+    // phase-2 record {state, global parent ref | lane << 40, footprint}; k_route
+    // then keys it and fills the owners' outboxes with tickets POOL_TICK | index
+    u32* pool;
+    u64 pool_cap;              // records in pool
+    unsigned long long* npool; // records written (may exceed pool_cap: the rest were parked)
     // replicated levels (small levels of a sharded search): the whole level's
     // records, gathered from every rank (RepRec: state, global ref, footprint, lane | class)
     const u32* rep;
@@ -93,7 +101,8 @@ struct Shape {
 //        7 = k_rehash of the stored states [a, b) (recovery).
 //       11 = k_compare_remote of `a` received state records `in` (sharded verification);
 //       12 = k_expand_dist<REP> over the replicated level's records B.rep[a, b);
-//       13 = k_pack_rep of this rank's stored states [a, b) into records at `out`.
+//       13 = k_pack_rep of this rank's stored states [a, b) into records at `out`;
+//       14 = k_route: key the pool's records and fill the outboxes (counts on the device).
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 
@@ -114,10 +123,14 @@ struct SrcOff {
 };
 hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply, u64 n, const SrcOff& so,
                                unsigned long long* acc, hipStream_t st);
-// Sharded mode: the exchange-count row of one round, out[2p] = keys for rank p
-// (min(ocount[p], kcap), 0 for p = rank), out[2p + 1] = flags (bit 0: this rank
-// has more to send: host_more, or parked keys beyond ovf_done; bit 1: its
-// parking buffer overflowed), out[2W] = novf.
+// Sharded mode: the exchange-count row of one round, one block of kRowWords u64
+// per rank p: [0] keys for p (min(ocount[p], kcap), 0 for p = rank), [1] flags
+// (bit 0: this rank has more to send: host_more, or parked keys beyond
+// ovf_done; bit 1: its parking buffer overflowed; bit 2: it sends keys this
+// round), [2..] this rank's Counters (so a round after which nothing changes
+// them ends the level without a counter all-gather); out[kRowWords * W] = novf.
+constexpr int kRowWords = 2 + (int)(sizeof(Counters) / 8);
+static_assert(sizeof(Counters) % 8 == 0, "Counters travel as u64 words");
 hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st);
 // States per single-GPU expansion launch at most (B.word holds one launch's
 // presorted window positions).
@@ -127,6 +140,9 @@ constexpr int kMaxLaunchLog2 = 25;
 hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st);
 // Sharded mode: move parked keys ovf[a, a + n) into the (emptied) outbox; n <= kcap.
 hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st);
+// Outbox ticket of a pool record (bit 48: a parent ticket's index is < 2^48 and
+// its lane sits at bits 56-63).
+constexpr u64 POOL_TICK = 1ull << 48;
 
 // Fingerprint salt for the kernels of shape sh on this device (0 = default
 // hash); returns after the copy (the staging value lives on the caller's stack).

@@ -118,7 +118,7 @@ __device__ __forceinline__ void store_new(const Params& P, const DevBufs& B, u64
     store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
     B.parent[ni] = parent;
     B.act[ni] = (uint8_t)lane;
-    if constexpr (Lanes<S, K>::N <= 64) B.foot[ni] = foot;
+    B.foot[ni] = foot;
     B.cls[ni] = (uint8_t)state_class_fine<S, K>(wo, mo);
     const int v = check_invariants<S, K>(wo, mo, P);
     if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
@@ -199,7 +199,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         load_state<S, K>(pr, w, m);
         Delta d;
         u64 foot;
-        if constexpr (Lanes<S, K>::N <= 64) {  // the lane's descriptor: no family-offset compares
+        if constexpr (Lanes<S, K>::N <= 128) {  // the lane's descriptor: no family-offset compares
             const u32 desc = P.ldesc[lane];
             lane_delta_desc<S, K>(w, m, desc, P, d);
             foot = make_foot_desc<S, K>(m, desc, d);
@@ -224,6 +224,37 @@ __device__ __forceinline__ u64 wave_or64(u64 v) {
     const u32 lo = (u32)__builtin_amdgcn_readfirstlane((int)(u32)v);
     const u32 hi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(v >> 32));
     return ((u64)hi << 32) | lo;
+}
+
+// The OR over the wave's live states of lane_superset (raft_packed.h), built
+// from one ballot per predicate instead of a shuffle reduction of the 64-bit
+// masks: each bit of the mask is an OR of role / slot-occupancy predicates, so
+// "some state of the wave has it" is a ballot.  Scalar result (SGPRs).
+template <int S, int K>
+__device__ __forceinline__ LaneMask lane_superset_wave(const u64 (&w)[S], const u32 (&m)[K], int V, bool live) {
+    typedef Lanes<S, K> L;
+    static_assert(L::N <= 128, "lane mask holds < 128 lanes");
+    constexpr int O1 = L::off(1), O2 = L::off(2), O3 = L::off(3), O4 = L::off(4), O5 = L::off(5), O6 = L::off(6),
+                  O7 = L::off(7), O8 = L::off(8), O9 = L::off(9);
+    constexpr u64 SM = (1ull << S) - 1;
+    LaneMask mk{0ull, 0ull};
+    if (!__ballot(live)) return mk;
+    mk.lo = SM;  // Restart(i): always enabled
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const u32 st = w_st(w[i]);
+        if (__ballot(live && st != LEADER)) mk.put(1ull, O1 + i);
+        if (__ballot(live && st == CANDIDATE)) { mk.put(SM, O2 + i * S); mk.put(1ull, O3 + i); }
+        if (__ballot(live && st == LEADER)) {
+            mk.put((1ull << V) - 1, O4 + i * VMAX);
+            mk.put(1ull, O5 + i);
+            mk.put(SM, O6 + i * S);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+        if (__ballot(live && m[q] != 0u)) { mk.put(1ull, O7 + q); mk.put(1ull, O8 + q); mk.put(1ull, O9 + q); }
+    return mk;
 }
 
 // ---- full-state verification (RMC_FLAG_VERIFY_STATES) ---------------------------
@@ -533,7 +564,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
                 u32 m[K];
                 load_state<S, K>(B.store + (lo + l_rel[e]) * (u64)NW, w, m);
                 Delta d;
-                if constexpr (Lanes<S, K>::N <= 64) lane_delta_desc<S, K>(w, m, P.ldesc[l_lane[e]], P, d);
+                if constexpr (Lanes<S, K>::N <= 128) lane_delta_desc<S, K>(w, m, P.ldesc[l_lane[e]], P, d);
                 else lane_delta<S, K>(w, m, l_lane[e], P, d);
                 if (B.owner_mode == 0) {
                     u64 wo[S];
@@ -579,7 +610,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
         load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
         Delta d;
         u64 foot;
-        if constexpr (Lanes<S, K>::N <= 64) {  // the lane's descriptor: no family-offset compares
+        if constexpr (Lanes<S, K>::N <= 128) {  // the lane's descriptor: no family-offset compares
             const u32 desc = P.ldesc[lane];
             lane_delta_desc<S, K>(w, m, desc, P, d);
             foot = make_foot_desc<S, K>(m, desc, d);
@@ -611,6 +642,115 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
     wave_sync_lds();
 }
 
+// Sharded mode with send markers, the pool flush (default): flush_new with the
+// owner decided per listed successor from its materialised words — a lane that
+// leaves the hashed words alone keeps its parent's owner, this rank — and two
+// reservation atomics per 64 entries, one for the local store, one for the
+// remote-successor pool (B.pool).  A remote successor is written there once, as
+// its phase-2 record; keying it, the per-destination slots and parking are left
+// to k_route after the launch.  So the flush carries no per-destination
+// bookkeeping, no second pass over the list and no re-hash of the successor,
+// and the sharded kernel keeps the single-GPU kernel's registers.  A pool that
+// is full parks the successor's ticket with key 0 (k_route keys it).
+template <int S, int K>
+__device__ __forceinline__ void flush_pool(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
+                                           const uint8_t* l_lane, uint8_t* l_own, u32 n) {
+    constexpr int NW = 2 * S + K, RW = NW + 4;
+    wave_sync_lds();
+    const int me = (int)__lane_id();
+    const u64 lt = (1ull << me) - 1ull;
+    // pass 1 (more than one rank): which listed successors this rank owns (LDS
+    // byte per entry): only lanes that change a hashed server word can leave
+    u32 nown = n;  // wave-uniform
+    if (B.world > 1) {
+        nown = 0;
+        for (u32 e0 = 0; e0 < n; e0 += 64) {
+            const u32 e = e0 + (u32)me;
+            bool own = true;
+            if (e < n) {
+                const int lane = l_lane[e];
+                Delta d;
+                u64 w[S];
+                u32 m[K];
+                load_state<S, K>(B.store + (lo + l_rel[e]) * (u64)NW, w, m);
+                if constexpr (Lanes<S, K>::N <= 128) lane_delta_desc<S, K>(w, m, P.ldesc[lane], P, d);
+                else lane_delta<S, K>(w, m, lane, P, d);
+                if (B.owner_mode == 0) {
+                    u64 wo[S];
+                    u32 mo[K];
+                    materialise<S, K>(w, m, d, wo, mo);
+                    own = owner_of(fp_of_materialised<S, K>(wo, mo, P), B.world) == B.rank;
+                } else if (d.srv >= 0 && d.srv < owner_words<S>(B)) {
+                    own = owner_succ_w<S>(0ull, d, w, B) == B.rank;
+                }
+                l_own[e] = own ? 1 : 0;
+            }
+            nown += (u32)__popcll(__ballot(e < n && own));
+        }
+        wave_sync_lds();
+    }
+    u64 base_l = 0, base_r = 0;
+    if (me == 0 && nown) base_l = atomicAdd((unsigned long long*)&B.ctr->count, (unsigned long long)nown);
+    if (me == 0 && n > nown) base_r = atomicAdd(B.npool, (unsigned long long)(n - nown));
+    base_l = bcast64(base_l, 0);
+    base_r = bcast64(base_r, 0);
+    for (u32 e0 = 0; e0 < n; e0 += 64) {  // wave-uniform rounds
+        const u32 e = e0 + (u32)me;
+        const bool valid = e < n;
+        const bool own = valid && (B.world == 1 || l_own[e]);
+        const u64 bl = __ballot(own), br = __ballot(valid && !own);
+        const u64 ql = base_l + (u64)__popcll(bl & lt), qr = base_r + (u64)__popcll(br & lt);
+        base_l += (u64)__popcll(bl);
+        base_r += (u64)__popcll(br);
+        if (!valid) continue;
+        const u64 rel = l_rel[e];
+        const int lane = l_lane[e];
+        if (own && ql >= B.cap) {
+            atomicOr(&B.ctr->overflow, 1u);
+            continue;
+        }
+        if (!own && qr >= B.pool_cap) {  // pool full: park the ticket, k_route_fix keys it
+            const u64 o = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
+            if (o < B.ovf_cap) {
+                B.ovf[2 * o] = 0;
+                B.ovf[2 * o + 1] = (lo + rel) | ((u64)lane << 56);
+            } else {
+                atomicOr(&B.ctr->overflow, 2u);
+            }
+            continue;
+        }
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + (lo + rel) * (u64)NW, w, m);
+        Delta d;
+        u64 foot;
+        if constexpr (Lanes<S, K>::N <= 128) {
+            const u32 desc = P.ldesc[lane];
+            lane_delta_desc<S, K>(w, m, desc, P, d);
+            foot = make_foot_desc<S, K>(m, desc, d);
+        } else {
+            lane_delta<S, K>(w, m, lane, P, d);
+            foot = make_foot<S, K>(m, lane, d, P);
+        }
+        u64 wo[S];
+        u32 mo[K];
+        materialise<S, K>(w, m, d, wo, mo);
+        const u64 parent = B.ref_tag | (lo + rel);
+        if (own) {
+            store_new<S, K>(P, B, ql, wo, mo, parent, lane, foot);
+            continue;
+        }
+        u32* r = B.pool + qr * (u64)RW;
+        store_state<S, K>(r, wo, mo);
+        const u64 ref = parent | ((u64)lane << 40);
+        r[NW] = (u32)ref;
+        r[NW + 1] = (u32)(ref >> 32);
+        r[NW + 2] = (u32)foot;
+        r[NW + 3] = (u32)(foot >> 32);
+    }
+    wave_sync_lds();
+}
+
 // Grid-stride over 256-state tiles of the frontier [lo, hi).  Lanes are
 // processed BATCH at a time so BATCH fingerprint probes per thread are in
 // flight together (the kernel is bound by probe latency, not bandwidth).
@@ -632,9 +772,10 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
           bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
-          int DYN = 0>
+          int DYN = 0, bool POOL = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
+    static_assert(!POOL || (MARK && !REP), "the pool flush: the send-marker kernel");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
     static_assert(!DIA || (!SYM && !VERIFY), "diamond skipping: not under SYMMETRY or verification");
     static_assert(!SORT || !VERIFY, "SORT: not with verification");
@@ -669,7 +810,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     constexpr int LCAP = SENTC ? 256 : WCAP;
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
-    __shared__ uint8_t s_dest[(SENTC || MARK) ? 4 : 1][(SENTC || MARK) ? LCAP : 1];  // owner per listed successor
+    constexpr bool LDEST = SENTC || MARK;
+    __shared__ uint8_t s_dest[LDEST ? 4 : 1][LDEST ? LCAP : 1];  // owner per listed successor
     __shared__ u64 s_lkey[SENTC ? 4 : 1][SENTC ? LCAP : 1];  // sharded: the key of each listed successor
     __shared__ u64 s_key[BATCH][256];
     __shared__ uint8_t s_own[LISTOWN ? BATCH : 1][LISTOWN ? 256 : 1];  // owner rank per probe
@@ -678,7 +820,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     const u64 lt_mask = (1ull << me) - 1ull;
     u32* l_rel = s_rel[wv];
     uint8_t* l_lane = s_lane[wv];
-    uint8_t* l_dest = s_dest[(SENTC || MARK) ? wv : 0];
+    uint8_t* l_dest = s_dest[LDEST ? wv : 0];
     u64* l_key = s_lkey[SENTC ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u32 gen = 0;  // generated lanes of this thread's states (< 2^32 per launch)
@@ -805,19 +947,32 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             diamond_of<S, K>(m, act, foot, P, dm);
         }
         u32 g = 0;
-        // SORT: the lanes some state of this wave can enable (wave-uniform, scalar)
-        u64 wm = 0;
-        if constexpr (SORT) wm = wave_or64(live ? lane_superset<S, K>(w, m, P.V) : 0ull);
+        // SORT: the lanes some state of this wave can enable (wave-uniform, scalar;
+        // wm_hi: lanes 64-127, shapes of more than 64 lanes only)
+        constexpr bool WIDE_MASK = Lanes<S, K>::N > 64;
+        u64 wm = 0, wm_hi = 0;
+        if constexpr (SORT) {
+            const LaneMask lm = lane_superset_wave<S, K>(w, m, P.V, live);
+            wm = lm.lo;
+            if constexpr (WIDE_MASK) wm_hi = lm.hi;
+        }
 #ifdef RMC_WALK_STATS_BUILD
-        walked += live ? (u32)(SORT ? __popcll(wm) : nl) : 0u;  // per thread (a VGPR: no scalar register held)
+        walked += live ? (u32)(SORT ? __popcll(wm) + __popcll(wm_hi) : nl) : 0u;  // per thread (a VGPR)
 #endif
-        for (int lane0 = 0; SORT ? (wm != 0) : (lane0 < nl); lane0 += BATCH) {  // wave-uniform loop (pr: probes issued)
+        for (int lane0 = 0; SORT ? ((wm | wm_hi) != 0) : (lane0 < nl); lane0 += BATCH) {  // wave-uniform (pr: probes)
             u64 lp = 0;  // SORT: this batch's lanes, 7 bits each (127 = none), a scalar
             if constexpr (SORT) {
 #pragma unroll
                 for (int b = 0; b < BATCH; ++b) {
-                    const u64 ln = wm ? (u64)__builtin_ctzll(wm) : 127ull;
-                    wm &= wm - 1;
+                    u64 ln;
+                    if constexpr (WIDE_MASK) {
+                        ln = wm ? (u64)__builtin_ctzll(wm) : wm_hi ? 64ull + (u64)__builtin_ctzll(wm_hi) : 127ull;
+                        if (wm) wm &= wm - 1;
+                        else wm_hi &= wm_hi - 1;
+                    } else {
+                        ln = wm ? (u64)__builtin_ctzll(wm) : 127ull;
+                        wm &= wm - 1;
+                    }
                     lp |= ln << (7 * b);
                 }
             }
@@ -1016,6 +1171,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     n += (u32)__popcll(bal);
                     if (n > (u32)(LCAP - 64)) {
                         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
+                        else if constexpr (POOL) flush_pool<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
                         else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
                         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
@@ -1033,6 +1189,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     }
     if (n) {
         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
+        else if constexpr (POOL) flush_pool<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
         else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
         else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
@@ -1089,7 +1246,7 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (Lanes<S, K>::N <= 64)
+    if constexpr (Lanes<S, K>::N <= 128)
         expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, DYN>(P, PT, B, lo,
                                                                                                      hi);
 }
@@ -1105,7 +1262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 template <int S, int K, int BATCH, bool WS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
 k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (WS && Lanes<S, K>::N <= 64)
+    if constexpr (WS && Lanes<S, K>::N <= 128)
         expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16>(P, PT, B, lo, hi);
     else
         expand_body<S, K, true, BATCH, false, false, false>(P, PT, B, lo, hi);
@@ -1118,12 +1275,20 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4>
+// POOL: the pool flush (flush_pool) with the single-GPU kernel's shape (presorted
+// windows of 16 tiles, early probe loads, the parent's mixes recomputed per lane).
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool POOL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (Lanes<S, K>::N <= 64 && PS && !REP)
+    if constexpr (Lanes<S, K>::N <= 128 && POOL && !REP)
+        expand_body<S, K, false, BATCH, true, false, false, true, true, true, 16, K <= 4 ? 1 : 0, false, true, 0, true>(
+            P, PT, B, lo, hi);
+    else if constexpr (POOL && !REP)  // more than 64 lanes: every lane, the pool flush
+        expand_body<S, K, false, BATCH, true, false, false, false, false, true, 8, 0, false, false, 0, true>(P, PT, B,
+                                                                                                           lo, hi);
+    else if constexpr (Lanes<S, K>::N <= 128 && PS && !REP)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
-    else if constexpr (Lanes<S, K>::N <= 64)
+    else if constexpr (Lanes<S, K>::N <= 128)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
         expand_body<S, K, false, BATCH, true, false, false, false, false, true>(P, PT, B, lo, hi);
@@ -1169,21 +1334,41 @@ __global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64
 // launch size and the expansion grid exactly as the kernel computes it), each
 // counting-sorted by the states' 1-byte classes: word[win + i] = the i-th
 // position of window win in class order.
+// The lanes of the wave holding the same 8-bit class as this one (one ballot
+// per class bit; inactive lanes never match).
+__device__ __forceinline__ u64 match_class8(u32 c, bool act) {
+    u64 peers = __ballot(act);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const u64 on = __ballot(act && ((c >> b) & 1u));
+        peers &= ((c >> b) & 1u) ? on : ~on;
+    }
+    return peers;
+}
+
+// The class counters take one LDS atomic per class present in a wave's 64
+// positions (match_class8), not one per position: a window's states fall in a
+// few classes, and same-address LDS atomics serialise (0.91 bank conflicts per
+// LDS access with per-position atomics, round 4's PMC profile).
 __global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo, u64 nf, u64 wt, uint16_t* word,
                                                       unsigned long long* wnext) {
     __shared__ u32 bins[256];
     __shared__ uint8_t cs[256 * 16];
     const u32 tid = threadIdx.x;
+    const u64 lt = (1ull << __lane_id()) - 1ull;
     if (blockIdx.x == 0 && tid == 0) *wnext = 0;  // the next expansion launch's dynamic work counter
     for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {
         const u32 wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
         __syncthreads();
         bins[tid] = 0;
         __syncthreads();
-        for (u32 p = tid; p < wn; p += 256) {
-            const u32 c = cls[lo + win + p];
-            cs[p] = (uint8_t)c;
-            atomicAdd(&bins[c], 1u);
+        for (u32 p0 = 0; p0 < wn; p0 += 256) {  // block-uniform rounds
+            const u32 p = p0 + tid;
+            const bool act = p < wn;
+            const u32 c = act ? (u32)cls[lo + win + p] : 0u;
+            if (act) cs[p] = (uint8_t)c;
+            const u64 peers = match_class8(c, act);
+            if (act && (peers & lt) == 0) atomicAdd(&bins[c], (u32)__popcll(peers));
         }
         __syncthreads();
         if (tid < 64) {  // exclusive scan of the 256 counters: 4 per lane, then across the wave
@@ -1201,7 +1386,17 @@ __global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo
             for (int q = 0; q < 4; ++q) { bins[tid * 4 + q] = ex; ex += v[q]; }
         }
         __syncthreads();
-        for (u32 p = tid; p < wn; p += 256) word[win + atomicAdd(&bins[cs[p]], 1u)] = (uint16_t)p;
+        for (u32 p0 = 0; p0 < wn; p0 += 256) {  // one cursor atomic per class present in the wave
+            const u32 p = p0 + tid;
+            const bool act = p < wn;
+            const u32 c = act ? (u32)cs[p] : 0u;
+            const u64 peers = match_class8(c, act);
+            const int leader = peers ? __ffsll((long long)peers) - 1 : 0;
+            u32 base = 0;
+            if (act && (peers & lt) == 0) base = atomicAdd(&bins[c], (u32)__popcll(peers));
+            base = (u32)__shfl((int)base, leader);
+            if (act) word[win + base + (u32)__popcll(peers & lt)] = (uint16_t)p;
+        }
     }
 }
 
@@ -1218,19 +1413,27 @@ hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 w
     return hipGetLastError();
 }
 
-// Sharded mode: the count row of one exchange round (launch_pack_counts).
+// Sharded mode: the count row of one exchange round (launch_pack_counts): a
+// block of kRowWords u64 per peer — keys for it, flags, this rank's counters —
+// then novf.
 __global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64* out) {
     const u32 p = threadIdx.x;
     const u64 novf = B.ctr->novf;
+    bool sends = false;
+    for (u32 q = 0; q < B.world; ++q) sends |= q != B.rank && B.ocount[q] != 0;
     // bit 0: more to send this level; bit 1: the parking buffer overflowed (every
-    // rank reads every row and fails alike)
-    const u64 flags = host_more | (novf > ovf_done ? 1ull : 0ull) | (novf > B.ovf_cap ? 2ull : 0ull);
+    // rank reads every row and fails alike); bit 2: keys to some peer this round
+    const u64 flags = host_more | (novf > ovf_done ? 1ull : 0ull) | (novf > B.ovf_cap ? 2ull : 0ull) |
+                      (sends ? 4ull : 0ull);
     if (p < B.world) {
+        u64* r = out + (u64)p * kRowWords;
         const u64 c = B.ocount[p];
-        out[2 * p] = p == B.rank ? 0ull : (c < B.kcap ? c : B.kcap);
-        out[2 * p + 1] = flags;
+        r[0] = p == B.rank ? 0ull : (c < B.kcap ? c : B.kcap);
+        r[1] = flags;
+        const u64* k = reinterpret_cast<const u64*>(B.ctr);
+        for (int i = 0; i < kRowWords - 2; ++i) r[2 + i] = k[i];
     }
-    if (p == 0) out[2 * B.world] = novf;
+    if (p == 0) out[(u64)kRowWords * B.world] = novf;
 }
 
 // Sharded mode: parked keys ovf[a, a + n) back into the outbox (n <= kcap, so
@@ -1251,6 +1454,83 @@ __global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
 
 #endif  // !RMC_SHAPE_S
 
+// Sharded mode, after a pool-flush expansion (k_expand_dist<POOL>): every pool
+// record [0, npool) gets its key (the state's fingerprint: order-free, so equal
+// to the incremental probe key) and owner and goes to that owner's outbox as
+// POOL_TICK | index, one reservation atomic per destination present in a wave;
+// what does not fit is parked as a parent ticket (the pool is reused by the
+// round after next, the parent store is not).
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_route(const Params P, const DevBufs B) {
+    constexpr int NW = 2 * S + K, RW = NW + 4;
+    const int me = (int)__lane_id();
+    const u64 lt = (1ull << me) - 1ull;
+    const u64 np = *B.npool < B.pool_cap ? *B.npool : B.pool_cap;
+    for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < np; t0 += (u64)gridDim.x * 256ull) {  // wave-uniform
+        const u64 t = t0 + threadIdx.x;
+        const bool live = t < np;
+        u64 key = 0, ref = 0;
+        u32 dest = 0xFFFFFFFFu;
+        if (live) {
+            const u32* r = B.pool + t * (u64)RW;
+            u64 w[S];
+            u32 m[K];
+            load_state<S, K>(r, w, m);
+            key = fp_of_materialised<S, K>(w, m, P);
+            dest = owner_state<S>(key, w, B);
+            ref = (u64)r[NW] | ((u64)r[NW + 1] << 32);
+        }
+        u64 slot = ~0ull;
+        u64 pending = __ballot(live);
+        while (pending) {  // wave-uniform: one atomic per destination present
+            const int l = __ffsll((long long)pending) - 1;
+            const u32 dd = (u32)__builtin_amdgcn_readlane((int)dest, l);
+            const u64 bal = __ballot(dest == dd);
+            u64 base = 0;
+            if (me == l) base = atomicAdd(&B.ocount[dd], (unsigned long long)__popcll(bal));
+            base = bcast64(base, l);
+            if (dest == dd) slot = base + (u64)__popcll(bal & lt);
+            pending &= ~bal;
+        }
+        if (!live) continue;
+        if (slot < B.kcap) {
+            B.key_out[(u64)dest * B.kcap + slot] = key;
+            B.tick_out[(u64)dest * B.kcap + slot] = POOL_TICK | t;
+            continue;
+        }
+        // the owner's outbox is full: park it with its parent ticket (a later round sends it)
+        const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
+        if (q < B.ovf_cap) {
+            B.ovf[2 * q] = key;
+            B.ovf[2 * q + 1] = (ref & ((1ull << 40) - 1)) | ((u64)dest << 48) | (((ref >> 40) & 0xFFull) << 56);
+        } else {
+            atomicOr(&B.ctr->overflow, 2u);
+        }
+    }
+}
+// Before k_route: the tickets the expansion itself parked (pool full) carry key
+// 0 until keyed here (k_route's own parked records carry theirs).
+template <int S, int K>
+__global__ __launch_bounds__(256) void k_route_fix(const Params P, const DevBufs B) {
+    constexpr int NW = 2 * S + K;
+    const u64 nov = B.ctr->novf < B.ovf_cap ? B.ctr->novf : B.ovf_cap;
+    for (u64 q = (u64)blockIdx.x * 256ull + threadIdx.x; q < nov; q += (u64)gridDim.x * 256ull) {
+        if (B.ovf[2 * q] != 0) continue;
+        const u64 tk = B.ovf[2 * q + 1];
+        const u64 pidx = tk & ((1ull << 48) - 1);
+        const int lane = (int)(tk >> 56);
+        u64 w[S], wo[S];
+        u32 m[K], mo[K];
+        load_state<S, K>(B.store + pidx * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        materialise<S, K>(w, m, d, wo, mo);
+        const u64 key = fp_of_materialised<S, K>(wo, mo, P);
+        B.ovf[2 * q + 1] = pidx | ((u64)owner_state<S>(key, wo, B) << 48) | ((u64)lane << 56);
+        B.ovf[2 * q] = key;
+    }
+}
+
 // Sharded mode, phase 2, sender side: for every key an owner accepted
 // (reply[d * kcap + i] = 1), re-derive the successor from its ticket and put
 // the record {state, global parent ref | lane << 40} into owner d's state
@@ -1270,11 +1550,18 @@ __global__ __launch_bounds__(256) void k_materialize_remote(const Params P, cons
         const bool seen = !reply[(u64)d * B.kcap + i];
         if (seen && !B.sidx) continue;
         const u64 tick = B.tick_out[(u64)d * B.kcap + i];
-        const u64 pidx = tick & ((1ull << 56) - 1);
+        const u64 pidx = tick & ((1ull << 48) - 1);
         const int lane = (int)(tick >> 56);
         const u64 slot = atomicAdd((unsigned long long*)&B.scount[d], 1ull);
         if (slot >= B.scap) {
             atomicOr(&B.ctr->overflow, 2u);
+            continue;
+        }
+        if (tick & POOL_TICK) {  // a pool record is already the phase-2 record (never REF_SEEN: no verification)
+            const uint2* src = reinterpret_cast<const uint2*>(B.pool + pidx * (u64)RW);
+            uint2* dst = reinterpret_cast<uint2*>(B.st_out + ((u64)d * B.scap + slot) * (u64)RW);
+#pragma unroll
+            for (int q = 0; q < RW / 2; ++q) dst[q] = src[q];
             continue;
         }
         u64 w[S];
@@ -1519,7 +1806,7 @@ __global__ __launch_bounds__(256) void k_pack_rep(const DevBufs B, u64 lo, u64 h
 #pragma unroll
         for (int q = 0; q < NW / 2; ++q) dst[q] = src[q];
         const u64 ref = B.ref_tag | i;
-        const u64 f = Lanes<S, K>::N <= 64 ? B.foot[i] : 0ull;
+        const u64 f = B.foot[i];
         r[RR::REF] = (u32)ref;
         r[RR::REF + 1] = (u32)(ref >> 32);
         r[RR::FOOT] = (u32)f;
@@ -1735,7 +2022,7 @@ static int expand_variant() {
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
-        return e ? atoi(e) : 2;
+        return e ? atoi(e) : 3;
     }();
     return v;
 }
@@ -1747,7 +2034,7 @@ template <int S, int K, bool SYM>
 static hipError_t launch_t(int which, bool verify, const Params& P, const PermTable& PT, const DevBufs& B, u64 a,
                            u64 b, const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st) {
     const u64 n = (which == 0 || which == 3 || which == 5 || which == 7 || which == 12 || which == 13) ? (b - a)
-                : which == 8 ? a * (u64)B.world : which == 10 ? 1 : a;
+                : which == 8 ? a * (u64)B.world : (which == 10 || which == 14) ? 1 : a;
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
@@ -1763,7 +2050,7 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     };
 #define RMC_EXPAND_LAUNCH(KERNEL)                                                                              \
     hipLaunchKernelGGL(KERNEL, dim3(eg(reinterpret_cast<const void*>(&(KERNEL)))), dim3(256), 0, st, P, PT, B, a, b)
-    constexpr bool SORTED = Lanes<S, K>::N <= 64;  // the lane-superset walk needs a 64-bit lane mask
+    constexpr bool SORTED = Lanes<S, K>::N <= 128;  // every shape: the lane-superset walk (LaneMask)
     if (which == 0) {
         if constexpr (SYM) {
             if (verify)
@@ -1810,6 +2097,15 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
+        } else if (dist_kvariant() == 3 && B.pool) {  // the pool flush at the single-GPU kernel's shape
+            if constexpr (SORTED) {
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
+                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, true>));
+            } else {
+                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, false, 4, true>));
+            }
         } else if (dist_kvariant() == 2 && SORTED && B.word) {  // presorted, 6 probes in flight, 5 waves/SIMD
             const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5>));
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
@@ -1819,6 +2115,13 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
         else return hipErrorInvalidValue;
+    } else if (which == 14) {  // the pool's records to the outboxes (after a pool-flush expansion)
+        if constexpr (!SYM) {
+            hipLaunchKernelGGL((k_route_fix<S, K>), dim3(256), dim3(256), 0, st, P, B);
+            hipLaunchKernelGGL((k_route<S, K>), dim3(1024), dim3(256), 0, st, P, B);
+        } else {
+            return hipErrorInvalidValue;
+        }
     } else if (which == 13) {
         hipLaunchKernelGGL((k_pack_rep<S, K>), dim3((unsigned)g), dim3(256), 0, st, B, a, b, out);
     } else if (which == 11) {

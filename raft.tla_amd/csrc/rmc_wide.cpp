@@ -105,10 +105,10 @@ int encode_wide(const rmc_ctx* c, const rmc_state_view& v, WState* out, std::str
         w.dst = (uint8_t)m.mdest;
         switch (m.mtype) {
             case RVQ:
-                if (!byte(m.mlastLogTerm, 0, 127) || !byte(m.mlastLogIndex, 0, 255))
+                if (!byte(m.mlastLogTerm, 0, TMAX) || !byte(m.mlastLogIndex, 0, 255))
                     return bad("RequestVoteRequest field out of range");
-                w.a = (int8_t)m.mlastLogTerm;
-                w.b = (uint8_t)m.mlastLogIndex;
+                w.b = (uint8_t)m.mlastLogTerm;
+                w.c = (uint8_t)m.mlastLogIndex;
                 break;
             case RVP:
                 if (!byte(m.mlog_len, 0, LW)) return bad("mlog too long");
@@ -187,7 +187,7 @@ void decode_wide(const rmc_ctx* c, const WState& s, rmc_state_view* v) {
         m.mdest = w.dst;
         m.count = s.cnt[q];
         switch (w.type) {
-            case RVQ: m.mlastLogTerm = w.a; m.mlastLogIndex = w.b; break;
+            case RVQ: m.mlastLogTerm = w.b; m.mlastLogIndex = w.c; break;
             case RVP:
                 m.mvoteGranted = w.a;
                 m.mlog_len = w.n;

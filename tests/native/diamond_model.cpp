@@ -153,7 +153,7 @@ struct Model {
                 for (int lane = 0; lane < nl; ++lane) {
                     Delta d;
                     lane_delta<S, K>(w, m, lane, P, d);
-                    if (lane < 64) {  // the descriptor path of the sorted kernels gives the same delta
+                    {  // the descriptor path of the sorted kernels gives the same delta
                         Delta dd;
                         lane_delta_desc<S, K>(w, m, P.ldesc[lane], P, dd);
                         if (dd.en != d.en || dd.srv != d.srv || dd.rm != d.rm || dd.has_add != d.has_add ||
@@ -182,7 +182,7 @@ struct Model {
                         delta_fp<S, K>(w, m, h0, d, P, &h2, &nmb);
                         if (diamond_skip<S, K>(m, lane, d, nmb, dm, P) != sk) ++o.mismatch;
                         // the lane-descriptor form the sorted kernels use decides the same
-                        if (lane < 64 && diamond_skip_desc<S, K>(m, lane, P.ldesc[lane], d, nmb, dm) != sk) ++o.mismatch;
+                        if (diamond_skip_desc<S, K>(m, lane, P.ldesc[lane], d, nmb, dm) != sk) ++o.mismatch;
                     }
                     if (sk) {
                         ++o.skipped;

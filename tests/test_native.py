@@ -10,7 +10,7 @@ def test_lane_superset_covers_every_enabled_lane(tmp_path):
     """k_expand_sort / k_expand_sym / k_expand_dist walk only the lanes in the
     OR over a wave of lane_superset (role and slot occupancy): every lane that
     lane_delta enables must be in it, or successors would be silently dropped.
-    Random walks from Init, every shape with <= 64 lanes, |Value| = 1 and 2."""
+    Random walks from Init, every shape (S = 2..5, K = 4 and 8), |Value| = 1 and 2."""
     exe = tmp_path / "lane_mask_check"
     subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-I",
                     os.path.join(ROOT, "raft.tla_amd", "csrc"),

@@ -206,3 +206,44 @@ def test_wide_capacity_edges_are_never_silently_in_the_model():
     assert fams["DuplicateMessage"] == 1       # the message held 255 times
     want = Counter(f for f, _p, t in R.successors(model, s))
     assert sum(want.values()) == len(got)
+
+
+def _state_with_bag(model, rvq_count):
+    """Server 1, a candidate of term 200 whose last log term is 200, has a
+    RequestVote request to server 0 in a 64-message bag (63 stale AEP fillers)."""
+    s = R.init_state(model)
+    s = s._replace(state=(R.FOLLOWER, R.CANDIDATE, R.FOLLOWER), currentTerm=(200, 200, 1),
+                   log=((R.entry(150, 0),), (R.entry(200, 1),), ()))
+    msgs = {R.rec(mtype=R.RVQ, mterm=200, mlastLogTerm=200, mlastLogIndex=1, msource=1, mdest=0): rvq_count}
+    for k in range(63):
+        m = R.rec(mtype=R.AEP, mterm=1, msuccess=False, mmatchIndex=k, msource=(k + 1) % 3, mdest=2)
+        msgs[m] = 1
+    return s._replace(messages=frozenset(msgs.items()))
+
+
+@pytest.mark.parametrize("rvq_count", [1, 2])
+def test_wide_terms_above_127_and_reply_capacity_of_the_net_bag(rvq_count):
+    """(1) a RequestVote request's mlastLogTerm is a term, up to 255:
+    server 0 (last log term 150) must grant a request whose last log term is 200
+    (logOk, raft.tla:249-251) — a signed byte read it as -56; (2) Reply
+    (raft.tla:102-103) removes the request as it adds the response, so in a full
+    64-message bag a count-1 request's reply is in the model (the request's slot
+    is freed) and a count-2 one's is not (a 65th message).  Every in-constraint
+    successor equals the Python restatement's."""
+    model = R.Model()
+    s = _state_with_bag(model, rvq_count)
+    assert len(s.messages) == 64
+    cfg = rmc.make_config(max_term=255, max_log_len=32, max_msgs=64, max_dup=255, max_depth=1, state_capacity=1 << 12)
+    with rmc.Checker(cfg) as ck:
+        got = ck.expand([to_view(model, s)])
+    have = Counter((rmc.FAMILIES[sv.family], from_view(sv.state)) for sv in got if sv.in_constraint)
+    want = Counter((f, t) for f, _p, t in R.successors(model, s) if len(t.messages) <= 64)
+    assert have == want
+    assert sum(1 for _ in got) == sum(1 for _ in R.successors(model, s))
+    granted = [t for f, t in have if f == "Receive" and any(
+        R.rget(m, "mtype") == R.RVP and R.rget(m, "mvoteGranted") for m, _c in t.messages)]
+    assert len(granted) == (1 if rvq_count == 1 else 0)
+    # the request's own sender re-sends: mlastLogTerm 200 decodes as 200
+    rv = [t for f, t in have if f == "RequestVote"]
+    assert rv and all(R.rget(m, "mlastLogTerm") == 200 for t in rv for m, _c in t.messages
+                      if R.rget(m, "mtype") == R.RVQ)

@@ -3,7 +3,7 @@ until a time budget) and print one JSON line per model with distinct/generated/
 depth/time.  Used to calibrate config 3 (5 servers, >= 1e9 distinct states,
 BASELINE.json configs[2]).
 
-    python tools/sizing.py S:V:MaxTerm:MaxLogLen:MaxMsgs:MaxDup[:verify][:spill][:dDEPTH] ... [--budget SECONDS]
+    python tools/sizing.py S:V:MaxTerm:MaxLogLen:MaxMsgs:MaxDup[:verify][:spill][:dDEPTH][:cCAPACITY] ... [--budget SECONDS]
 
 `spill`: expanded levels move to host memory when the device store fills
 (RMC_FLAG_SPILL), so a model larger than HBM still runs to its fixpoint while
@@ -37,9 +37,10 @@ def main():
         verify = "verify" in f[6:]
         spill = "spill" in f[6:]
         depth = max([int(x[1:]) for x in f[6:] if x.startswith("d")] or [0])
+        cap = max([int(x[1:]) for x in f[6:] if x.startswith("c")] or [0])  # cN: state capacity (0: librmc's)
         cfg = rmc.make_config(n_servers=s, n_values=v, max_term=t, max_log_len=l, max_msgs=mm, max_dup=dd,
                               check_deadlock=False, verify_states=verify, max_depth=depth,
-                              spill=spill)
+                              spill=spill, state_capacity=cap)
         t0 = time.time()
         rec = {"model": sp}
         try:
