@@ -4,6 +4,10 @@
 A "step" is one complete breadth-first search of the bounded MCraft model to
 its fixpoint (time-to-fixpoint); `value` = distinct states / seconds per step,
 whole job.  The workload is deterministic: an exhaustive BFS has no input data.
+The default model, specs/MCraftBenchXL.cfg (4.13 G distinct states), is the
+largest bounded model sized so far that one GPU completes: on one GPU its
+expanded levels leave the device window (RMC_FLAG_SPILL with the trace links
+kept in HBM), sharded every rank holds its part resident.
 With N > 1 ranks the state space is sharded over the GPUs inside librmc
 (rmc_shard: owner-routed successors, fingerprint-first two-phase exchange
 over librmc's own RCCL communicator) and the SAME model is searched, so
@@ -36,10 +40,13 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBench.cfg"))
+    ap.add_argument("--config", default=os.path.join(ROOT, "specs", "MCraftBenchXL.cfg"))
     ap.add_argument("--capacity", type=int, default=0,
                     help="state capacity per GPU (0: 1.5e9 / world * 1.3 for MCraftBench.cfg, the table size every "
                          "round measured; any other model: librmc's own sizing, 80%% of free HBM)")
+    ap.add_argument("--spill", default="auto", choices=("auto", "on", "off"),
+                    help="RMC_FLAG_SPILL (expanded levels leave the device window; their trace links stay in "
+                         "HBM): auto = on for a single GPU unless the model is MCraftBench.cfg")
     ap.add_argument("--device", type=int, default=-1, help="-1: LOCAL_RANK modulo the visible GPUs")
     ap.add_argument("--keys-per-dest", type=int, default=0,
                     help="sharded mode: phase-1 keys one chunk may send one owner (0 = librmc's choice)")
@@ -311,12 +318,16 @@ def main(argv=None):
     cfg = rmc.config_from_files(a.config, builtin_raft=True)
     cfg.device = dev
     ranks_per_gpu = max(1, -(-world // ndev)) if sharded else 1
+    small = os.path.basename(a.config) == "MCraftBench.cfg"
     if a.capacity:
         cfg.state_capacity = a.capacity
-    elif os.path.basename(a.config) == "MCraftBench.cfg":
+    elif small:
         cfg.state_capacity = int(1.5e9 / world * (1.3 if sharded else 1.0))
-    else:  # e.g. specs/MCraftBench8.cfg (2.56 G states per rank at 288 GB)
+    else:  # librmc's own sizing (80 % of free HBM)
         cfg.state_capacity = 0
+    spill = (a.spill == "on" or (a.spill == "auto" and not small)) and not sharded
+    if spill:
+        cfg.flags |= rmc.FLAG_SPILL
     W = rmc.native().rmc_state_bytes(cfg)
     # roofline ceiling of the fingerprint set: random 8-B probes over 64 GB
     r_max = None
@@ -416,6 +427,9 @@ def main(argv=None):
                         f"{cfg.max_log_len} MaxMsgs={cfg.max_msgs} MaxDup={cfg.max_dup}, BFS to fixpoint",
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
+            "spill": ({"flag": "RMC_FLAG_SPILL", "trace_links": "device" if last[0].spill_links_on_device else "host",
+                       "spills_per_step": last[0].spills, "states_moved_per_step": last[0].spilled,
+                       "spill_seconds_per_step": last[0].spill_seconds} if spill else None),
             "parallelism": (f"state-space sharded x{world} (librmc two-phase exchange, "
                             f"{'RCCL over xGMI' if transport == 'rccl' else 'host transport over gloo'})")
                            if sharded else "single GPU",

@@ -69,13 +69,16 @@ extern "C" {
                                            /* differences = collisions (no TLC analog;  */
                                            /* single GPU)                               */
 #define RMC_FLAG_SPILL (1u << 4)           /* frontier spill (TLC's states/ directory): */
-                                           /* expanded levels move to pinned host memory */
-                                           /* when the device window fills, so a model  */
-                                           /* whose states outgrow HBM completes while  */
-                                           /* its fingerprints fit.  state_capacity then */
-                                           /* sizes the fingerprint set (all states),   */
-                                           /* device_window the resident states.  Single */
-                                           /* GPU; not with RMC_FLAG_VERIFY_STATES       */
+                                           /* expanded levels leave the device window   */
+                                           /* when it fills, so a model whose states    */
+                                           /* outgrow HBM completes while its           */
+                                           /* fingerprints fit.  Their trace links      */
+                                           /* (parent, lane: 9 B) stay in HBM when they */
+                                           /* fit (else they move to host memory).      */
+                                           /* state_capacity then sizes the fingerprint */
+                                           /* set and links (all states), device_window */
+                                           /* the resident states.  Single GPU; not     */
+                                           /* with RMC_FLAG_VERIFY_STATES               */
 /* A model without a CONSTRAINT on some field (MCraft.cfg as shipped) runs only
  * under a depth bound (max_depth > 0, TLC -depth).  The front-end then gives
  * each unbounded field the wide capacity (RMC_WIDE_MAX_TERM, RMC_WIDE_MAX_LOG,
@@ -154,13 +157,17 @@ typedef struct rmc_result {
                                /* overlapped with the next round's expansion or not        */
     uint64_t stored_here;      /* distinct states this rank stores                         */
     /* RMC_FLAG_SPILL */
-    uint64_t spilled;          /* states moved to host memory (all spills of the run)      */
+    uint64_t spilled;          /* states moved out of the device window (all spills of the run) */
     uint64_t spills;           /* spill events                                              */
     double spill_seconds;      /* wall time of the spills (device-to-host + window shift)   */
     /* sharded mode, continued */
     uint64_t parked;           /* keys parked because an owner's outbox was full; sent in   */
                                /* further rounds of the same level (never dropped)          */
     double exchange_wait_seconds; /* host wall time blocked on count read-backs and level ends */
+    /* RMC_FLAG_SPILL, continued */
+    int32_t spill_links_on_device; /* 1: the trace links (parent, lane) of spilled states stayed */
+                                   /* in HBM and a spill only shifted the window; 0: host      */
+    int32_t pad2;
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */

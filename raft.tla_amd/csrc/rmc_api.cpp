@@ -320,11 +320,13 @@ void spill_rebase(rmc_ctx* c, u64 base) {
     X.base = base;
     const uintptr_t nw = (uintptr_t)c->NW;
     c->B.store = (u32*)((uintptr_t)X.store - (uintptr_t)base * nw * 4);
-    c->B.parent = (u64*)((uintptr_t)X.parent - (uintptr_t)base * 8);
-    c->B.act = (uint8_t*)((uintptr_t)X.act - (uintptr_t)base);
+    const u64 lb = X.dev_links ? 0 : base;  // device links: indexed by global index, never rebased
+    c->B.parent = (u64*)((uintptr_t)X.parent - (uintptr_t)lb * 8);
+    c->B.act = (uint8_t*)((uintptr_t)X.act - (uintptr_t)lb);
     c->B.foot = (u64*)((uintptr_t)X.foot - (uintptr_t)base * 8);
     c->B.cls = (uint8_t*)((uintptr_t)X.cls - (uintptr_t)base);
-    c->B.cap = base + X.win;
+    // device links hold total_cap states: no store index may pass it
+    c->B.cap = X.dev_links ? std::min(base + X.win, X.total_cap) : base + X.win;
 }
 
 // Address space for the trace links of every state the set can hold; pages
@@ -374,6 +376,22 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
     if (!n) return 0;
     const auto t0 = std::chrono::steady_clock::now();
     const u64 W = (u64)c->NW * 4;
+    if (X.dev_links) {  // the links stay in HBM: only the window's states move down
+        const u64 m = count - a;
+        for (u64 off = 0; off < m; off += n) {
+            const u64 k = std::min(n, m - off);
+            HIPCHK(c, hipMemcpyAsync((char*)X.store + off * W, (char*)X.store + (n + off) * W, k * W,
+                                     hipMemcpyDeviceToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync(X.foot + off, X.foot + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync(X.cls + off, X.cls + n + off, k, hipMemcpyDeviceToDevice, c->st));
+        }
+        HIPCHK(c, hipStreamSynchronize(c->st));
+        spill_rebase(c, a);
+        c->res.spilled += n;
+        c->res.spills += 1;
+        c->res.spill_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return 0;
+    }
     u64* hp = X.h_parent + X.base;
     uint8_t* ha = X.h_act + X.base;
     if (X.ahead.joinable()) X.ahead.join();
@@ -418,7 +436,7 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
 
 // The trace link (parent index, action lane) of any stored state.
 int read_link(rmc_ctx* c, u64 idx, u64* parent, uint8_t* act) {
-    if (c->spill.on && idx < c->spill.base) {
+    if (c->spill.on && !c->spill.dev_links && idx < c->spill.base) {
         *parent = c->spill.h_parent[idx];
         *act = c->spill.h_act[idx];
         return 0;
@@ -497,8 +515,14 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     u64 cap = cfg->state_capacity;
     if (cap == 0) {
         // table <= 4 slots per state after pow2 rounding (+ as many sidx words when verifying);
-        // spilling: the set takes 60 % of the budget, the device window the rest
-        cap = spill ? (u64)(budget * 0.6) / 32 : budget / (per_state + (c->sh.verify ? 64 : 32));
+        // spilling: the largest set of at most half the budget, two slots per state
+        if (spill) {
+            u64 sl = 1ull << 20;
+            while (sl * 16 <= budget / 2) sl <<= 1;  // 8 B * (2 sl) <= budget / 2
+            cap = sl / 2;
+        } else {
+            cap = budget / (per_state + (c->sh.verify ? 64 : 32));
+        }
         cap = std::min<u64>(cap, 1ull << 36);
     }
     cap = std::max<u64>(cap, 1024);
@@ -506,15 +530,26 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     while (slots < 2 * cap) slots <<= 1;
     c->table_slots = slots;
     u64 win = cap;  // states resident on the device
+    // spilling: the trace links of every state stay on the device (9 B each) when
+    // that leaves a window of at least a quarter of the states; otherwise, or with
+    // RMC_SPILL_HOST_LINKS=1, they move to the host with the spilled levels
+    bool dev_links = false;
+    u64 link_cap = win;
     if (spill) {
+        const u64 rest = budget - std::min<u64>(budget, slots * 8);
+        const char* hl = getenv("RMC_SPILL_HOST_LINKS");
+        const u64 wbytes = per_state - 9;  // state, footprint, class
+        const u64 need_win = cfg->device_window ? cfg->device_window : cap / 4;
+        dev_links = !(hl && atoi(hl)) && rest > cap * 9 && (rest - cap * 9) / wbytes >= need_win;
         win = cfg->device_window;
-        if (win == 0) win = (budget - std::min<u64>(budget, slots * 8)) / per_state;
+        if (win == 0) win = dev_links ? (rest - cap * 9) / wbytes : rest / per_state;
         win = std::max<u64>(std::min<u64>(win, cap), 1024);
+        link_cap = dev_links ? cap : win;
     }
     c->B.cap = win;
     c->B.tmask = slots - 1;
     if (hipMalloc(&c->B.store, win * (u64)c->NW * 4) != hipSuccess ||
-        hipMalloc(&c->B.parent, win * 8) != hipSuccess || hipMalloc(&c->B.act, win) != hipSuccess ||
+        hipMalloc(&c->B.parent, link_cap * 8) != hipSuccess || hipMalloc(&c->B.act, link_cap) != hipSuccess ||
         hipMalloc(&c->B.foot, win * 8) != hipSuccess || hipMalloc(&c->B.cls, win) != hipSuccess ||
         hipMalloc(&c->B.table, slots * 8) != hipSuccess || hipMalloc(&c->B.ctr, sizeof(Counters)) != hipSuccess ||
         hipMalloc(&c->B.word, (1ull << kMaxLaunchLog2) * 2) != hipSuccess ||  // presorted windows of one launch
@@ -523,6 +558,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         return bail(RMC_E_NOMEM);
     }
     c->spill.on = spill ? 1 : 0;
+    c->spill.dev_links = dev_links ? 1 : 0;
     c->spill.win = win;
     c->spill.total_cap = cap;
     c->spill.store = c->B.store;
@@ -536,7 +572,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         c->err = "hipMemset failed";
         return bail(RMC_E_HIP);
     }
-    if (spill && spill_reserve(c)) return bail(RMC_E_NOMEM);
+    if (spill && !dev_links && spill_reserve(c)) return bail(RMC_E_NOMEM);
     if (c->sh.sym) {  // successors with tied signatures, canonicalised by k_ties after each launch
         // a lane defers at most one tied successor, so launches of at most
         // tie_cap / lanes states cannot overflow it (run_bfs sizes them so):
@@ -613,13 +649,14 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         depth = c->resume_depth;
     } else {
     c->res = rmc_result{};
+    c->res.spill_links_on_device = c->spill.on && c->spill.dev_links;
     c->walked = 0;
     c->level_start.clear();
     if (c->spill.on) {
         spill_rebase(c, 0);
         SpillState& X = c->spill;
         const u64 f1 = std::min(X.total_cap, X.win);  // back the first spill's pages meanwhile
-        if (!X.ahead.joinable() && f1 > X.faulted) {
+        if (!X.dev_links && !X.ahead.joinable() && f1 > X.faulted) {
             const u64 f0 = X.faulted;
             X.faulted = f1;
             X.ahead = std::thread([&X, f0, f1] {
@@ -694,7 +731,12 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 const u64 count = c->h_ctr->count, fit = (c->B.cap - count) / lanes;
                 u64 want = b - a;
                 const u64 old = a - c->spill.base;
-                if (fit < std::min<u64>(want, 1ull << 20) && old && (old * 8 >= count - a || fit == 0))
+                // device links: a spill is a device-to-device shift only, taken as
+                // soon as a whole launch no longer fits (launches keep their size)
+                const bool due = c->spill.dev_links ? (fit < want && old && (old >= count - a || fit == 0))
+                                                    : (fit < std::min<u64>(want, 1ull << 20) && old &&
+                                                       (old * 8 >= count - a || fit == 0));
+                if (due)
                     if (int rc = spill_to(c, a, count)) return rc;
                 want = std::min(want, (c->B.cap - count) / lanes);
                 if (want == 0)
@@ -899,11 +941,12 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     auto put = [&](const void* p, u64 n) {
         if (!rc && n && fwrite(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint write failed");
     };
-    const u64 nd = h.count - base;
-    if (base) put(c->spill.h_parent, base * 8);
-    if (!rc) rc = move_file(c, f, c->B.parent + base, nd * 8, true);
-    if (base) put(c->spill.h_act, base);
-    if (!rc) rc = move_file(c, f, c->B.act + base, nd, true);
+    const u64 lb = c->spill.dev_links ? 0 : base;  // links below lb are on the host
+    const u64 nd = h.count - lb;
+    if (lb) put(c->spill.h_parent, lb * 8);
+    if (!rc) rc = move_file(c, f, c->B.parent + lb, nd * 8, true);
+    if (lb) put(c->spill.h_act, lb);
+    if (!rc) rc = move_file(c, f, c->B.act + lb, nd, true);
     if (!rc) rc = move_file(c, f, c->B.store + h.first * (u64)c->NW, (h.count - h.first) * (u64)c->NW * 4, true);
     if (!rc && h.slots) rc = move_file(c, f, c->B.table, h.slots * 8, true);
     if (fclose(f) != 0 && !rc) rc = fail(c, RMC_E_IO, "checkpoint close failed");
@@ -964,7 +1007,7 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     if (c->spill.on) {
         if (c->spill.ahead.joinable()) c->spill.ahead.join();  // it may be touching [0, s)
         spill_rebase(c, 0);
-        c->spill.faulted = std::max(c->spill.faulted, s);  // fread backs the links it writes
+        if (!c->spill.dev_links) c->spill.faulted = std::max(c->spill.faulted, s);  // fread backs the links it writes
     }
     const u64 NW = (u64)c->NW, W = NW * 4;
     u32* dstore = c->spill.on ? c->spill.store : c->B.store;
@@ -981,10 +1024,11 @@ int rmc_recover(rmc_ctx* c, const char* path) {
                              (c->spill.on ? c->spill.win : c->B.cap) * 8, c->st));
     HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
-    if (s) get(c->spill.h_parent, s * 8);
-    if (!rc) rc = move_file(c, f, dparent, (h.count - s) * 8, false);
-    if (s) get(c->spill.h_act, s);
-    if (!rc) rc = move_file(c, f, dact, h.count - s, false);
+    const u64 ls0 = c->spill.dev_links ? 0 : s;  // links below ls0 go to the host
+    if (ls0) get(c->spill.h_parent, ls0 * 8);
+    if (!rc) rc = move_file(c, f, dparent, (h.count - ls0) * 8, false);
+    if (ls0) get(c->spill.h_act, ls0);
+    if (!rc) rc = move_file(c, f, dact, h.count - ls0, false);
     if (!h.first && s && !rc) {
         // no set in the file: rehash the states below s through the free part
         // of the window (the frontier is loaded after them, at its start)

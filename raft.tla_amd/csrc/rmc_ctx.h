@@ -88,6 +88,12 @@ struct DistState {
 // states by their global index.
 struct SpillState {
     int on = 0;
+    // device links (default when they fit): the trace links of every state stay in
+    // HBM (9 B per state, B.parent / B.act indexed by global index, never rebased)
+    // and a spill only shifts the window's states, footprints and classes — no
+    // PCIe traffic; otherwise (RMC_SPILL_HOST_LINKS=1, or no room) they move to
+    // the host as below
+    int dev_links = 0;
     rmc::u64 base = 0;          // first device-resident global index
     rmc::u64 win = 0;           // device window (states)
     rmc::u64 total_cap = 0;     // all states (fingerprint-set sizing)

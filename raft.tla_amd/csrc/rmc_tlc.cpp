@@ -415,8 +415,9 @@ int main(int argc, char** argv) {
            (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
     printf("The depth of the complete state graph search is %d.\n", r.depth);
     if (r.spills)
-        printf("Spilled %llu expanded states to host memory in %llu spills (%.2fs).\n",
-               (unsigned long long)r.spilled, (unsigned long long)r.spills, r.spill_seconds);
+        printf("Spilled %llu expanded states out of the device window in %llu spills (%.2fs; trace links kept in %s).\n",
+               (unsigned long long)r.spilled, (unsigned long long)r.spills, r.spill_seconds,
+               r.spill_links_on_device ? "HBM" : "host memory");
     if (gpus > 1)
         printf("Exchange (rank 0): %llu rounds, %llu keys and %llu states sent, %llu keys parked, "
                "%.1fms of exchange on the device, %.1fms waited on the host.\n",

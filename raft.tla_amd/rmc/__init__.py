@@ -58,7 +58,8 @@ class Result(C.Structure):
                 ("keys_sent", C.c_uint64), ("states_sent", C.c_uint64), ("chunks", C.c_uint64),
                 ("exchange_seconds", C.c_double), ("stored_here", C.c_uint64),
                 ("spilled", C.c_uint64), ("spills", C.c_uint64), ("spill_seconds", C.c_double),
-                ("parked", C.c_uint64), ("exchange_wait_seconds", C.c_double)]
+                ("parked", C.c_uint64), ("exchange_wait_seconds", C.c_double),
+                ("spill_links_on_device", C.c_int32), ("pad2", C.c_int32)]
 
 
 class LevelStats(C.Structure):

@@ -68,6 +68,10 @@ CONFIGS = {
     # states; the whole 1.23 G-state model exceeds the oracle's memory)
     "bench_prefix22": (3, 2, 2, 1, 3, 1, 0, 1, 0, 22),
     "bench_prefix24": (3, 2, 2, 1, 3, 1, 0, 1, 0, 24),
+    # the round-5 bench model (specs/MCraftBenchXL.cfg: V = 1, MaxLogLen 2; 4.13 G states):
+    # its first 22 and 24 levels (43 M, 87 M states)
+    "benchxl_prefix22": (3, 1, 2, 2, 3, 1, 0, 1, 0, 22),
+    "benchxl_prefix24": (3, 1, 2, 2, 3, 1, 0, 1, 0, 24),
     # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
     "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }

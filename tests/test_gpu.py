@@ -104,19 +104,34 @@ def test_many_launches_per_level_keep_every_count(tmp_path):
     assert out["small"][4] > GOLDEN["small"]["depth"] and out["tiny2_v2"][4] > GOLDEN["tiny2_v2"]["depth"]
 
 
-@pytest.mark.parametrize("prefix", ["bench_prefix22", "bench_prefix24"])
-def test_bench_model_prefix_equals_oracle(prefix):
-    """The bench workload itself (specs/MCraftBench.cfg through the front-end,
-    as bench.py loads it), searched to its fixpoint: its first levels equal the
-    C oracle's level by level (new states per level, and the distinct and
-    generated counts once those levels exist), and the whole search ends with
-    the bench line's counts (1.23 G states: beyond the oracle's memory)."""
+BENCH_MODELS = {  # spec: (final distinct, generated, depth, single-GPU setup)
+    "MCraftBench.cfg": ((1_227_465_177, 21_130_972_267, 56), "resident"),
+    "MCraftBenchXL.cfg": ((4_132_397_327, 68_825_665_094, 75), "spill"),
+}
+
+
+@pytest.mark.parametrize("spec,prefix", [("MCraftBench.cfg", "bench_prefix22"), ("MCraftBench.cfg", "bench_prefix24"),
+                                         ("MCraftBenchXL.cfg", "benchxl_prefix22"),
+                                         ("MCraftBenchXL.cfg", "benchxl_prefix24")])
+def test_bench_model_prefix_equals_oracle(spec, prefix):
+    """The bench workloads themselves (through the front-end, as bench.py loads
+    them), searched to their fixpoint: the first levels equal the C oracle's
+    level by level (new states per level, and the distinct and generated counts
+    once those levels exist), and the whole search ends with the bench line's
+    counts (1.23 G and 4.13 G states: beyond the oracle's memory).  The 4.13 G-state
+    round-5 bench model runs as bench.py runs it on one GPU: RMC_FLAG_SPILL with
+    librmc's own sizing, its trace links in HBM."""
     g = GOLDEN[prefix]
-    cfg = rmc.config_from_files(os.path.join(ROOT, "specs", "MCraftBench.cfg"), builtin_raft=True)
+    final, setup = BENCH_MODELS[spec]
+    cfg = rmc.config_from_files(os.path.join(ROOT, "specs", spec), builtin_raft=True)
     p = g["params"]
     assert (cfg.n_servers, cfg.n_values, cfg.max_term, cfg.max_log_len, cfg.max_msgs, cfg.max_dup) == \
         (p["n_servers"], p["n_values"], p["max_term"], p["max_log_len"], p["max_msgs"], p["max_dup"])
-    cfg.state_capacity = 1_300_000_000
+    if setup == "resident":
+        cfg.state_capacity = 1_300_000_000
+    else:
+        cfg.state_capacity = 0
+        cfg.flags |= rmc.FLAG_SPILL
     with rmc.Checker(cfg) as ck:
         res = ck.run()
         lv = list(ck.levels)
@@ -125,7 +140,9 @@ def test_bench_model_prefix_equals_oracle(prefix):
     assert levels[:d] == g["level_new"]
     at = [x for x in lv if x[2] == g["distinct"]]  # the callback of the level that completed level d
     assert at and at[0][1] == g["generated"]
-    assert (res.distinct, res.generated, res.depth) == (1_227_465_177, 21_130_972_267, 56)
+    assert (res.distinct, res.generated, res.depth) == final
+    if setup == "spill":
+        assert res.spills > 0 and res.spill_links_on_device == 1
 
 
 def test_fingerprint_salt_does_not_change_counts():
@@ -440,12 +457,22 @@ def spill_cfg(name, slack, **kw):
     return g, cfg
 
 
+@pytest.fixture(params=["device", "host"])
+def links(request, monkeypatch):
+    """Where a spilled state's trace links live: in HBM (librmc's default when
+    they fit) or in host memory (RMC_SPILL_HOST_LINKS=1, the fallback)."""
+    if request.param == "host":
+        monkeypatch.setenv("RMC_SPILL_HOST_LINKS", "1")
+    return request.param
+
+
 @pytest.mark.parametrize("name,slack", [("bounded_full", 1 << 22), ("small", 1 << 16), ("small_sym", 1 << 14),
                                         ("tiny2_v2", 4096), ("tiny2", 4096)])
-def test_spill_completes_with_the_oracle_counts(name, slack):
+def test_spill_completes_with_the_oracle_counts(name, slack, links):
     g, cfg = spill_cfg(name, slack)
     assert cfg.device_window < g["distinct"]
     res, levels, _ = run(cfg)
+    assert res.spill_links_on_device == (links == "device")
     assert levels == g["level_new"]
     assert (res.distinct, res.generated, res.depth, res.left_on_queue) == \
         (g["distinct"], g["generated"], g["depth"], g["left_on_queue"])
@@ -454,7 +481,7 @@ def test_spill_completes_with_the_oracle_counts(name, slack):
 
 
 @pytest.mark.parametrize("name", ["bug_one_leader", "messages_small", "sym_bug_one_leader"])
-def test_spill_trace_equals_the_resident_trace(name):
+def test_spill_trace_equals_the_resident_trace(name, links):
     """The counterexample walks parents through host segments and the device
     window; it must be a behaviour of the spec to a violating state at the
     depth the resident run reports (which parent wins a race depends on the
@@ -475,7 +502,7 @@ def test_spill_trace_equals_the_resident_trace(name):
 
 
 @pytest.mark.parametrize("first,second", [("spill", "spill"), ("resident", "spill"), ("spill", "resident")])
-def test_spill_checkpoint_and_recover(first, second, tmp_path):
+def test_spill_checkpoint_and_recover(first, second, tmp_path, links):
     """A spilled search checkpoints its trace links, frontier and fingerprint
     set (the spilled states no longer exist) and recovers into a spilling
     context; a resident checkpoint recovers into a spilling context by
@@ -504,7 +531,7 @@ def test_spill_checkpoint_and_recover(first, second, tmp_path):
     assert r2.spills > r1.spills  # the recovered result carries the checkpointed statistics forward
 
 
-def test_spill_recover_to_the_violation_replays_the_trace(tmp_path):
+def test_spill_recover_to_the_violation_replays_the_trace(tmp_path, links):
     g, cfg = spill_cfg("bug_one_leader", 2048, max_depth=9)
     with rmc.Checker(cfg) as ck:
         ck.run()
@@ -541,7 +568,7 @@ def test_cli_spills_by_default_and_reports_it():
     assert r.returncode == 0, r.stdout + r.stderr
     assert f"{g['generated']} states generated, {g['distinct']} distinct states found, 0 states left on queue." \
         in r.stdout
-    assert "expanded states to host memory" in r.stdout
+    assert "expanded states out of the device window" in r.stdout and "trace links kept in HBM" in r.stdout
 
 
 @pytest.mark.gpu

@@ -2,7 +2,10 @@
 one JSON line per level — level, frontier expanded, new states, generated,
 seconds since the start — for a TLC model file.  Measurement tool.
 
-    python tools/level_times.py specs/MCraftBench.cfg [capacity [max_depth]] > levels.jsonl
+    python tools/level_times.py specs/MCraftBench.cfg [capacity [max_depth [spill]]] > levels.jsonl
+
+capacity 0: librmc's own sizing; `spill`: RMC_FLAG_SPILL (how bench.py runs
+specs/MCraftBenchXL.cfg on one GPU).
 """
 import json
 import os
@@ -16,6 +19,8 @@ cfg = rmc.config_from_files(sys.argv[1], builtin_raft=True)
 cfg.state_capacity = int(sys.argv[2]) if len(sys.argv) > 2 else 1_500_000_000
 if len(sys.argv) > 3:
     cfg.max_depth = int(sys.argv[3])  # a prefix of a model larger than one GPU
+if len(sys.argv) > 4 and sys.argv[4] == "spill":
+    cfg.flags |= rmc.FLAG_SPILL
 with rmc.Checker(cfg) as ck:
     ck.run()  # warm
     r = ck.run()
