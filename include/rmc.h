@@ -298,13 +298,16 @@ int rmc_expand(rmc_ctx* ctx, const rmc_state_view* states, size_t n, rmc_succ_vi
  * ends that behaviour (counted in `truncated`). */
 #define RMC_SIM_WITHIN_CAPACITY 0
 #define RMC_SIM_TRUNCATE 1
-/* TLC's draw (SimulationWorker): a uniformly random enabled action — each
+/* TLC's draw (its simulator's action choice, restated): Next's actions — each
  * instance of Restart .. AppendEntries (\E over the constant Server/Value sets
  * expands into one action each), Receive, DuplicateMessage and DropMessage
- * (\E m \in DOMAIN messages ranges over the state) one action each — then a
- * uniformly random successor of that action; beyond the bounds it ends the
- * behaviour like RMC_SIM_TRUNCATE.  Wide layout only (rmc_simulate refuses it
- * on the packed one). */
+ * (\E m \in DOMAIN messages ranges over the state) one action each — are
+ * visited from a uniformly random index with a random prime stride (primes
+ * above the action count, so every action is visited); the first one with a
+ * successor is taken and one of its successors drawn uniformly.  Not uniform
+ * over the enabled actions: an action after a run of disabled ones is likelier.
+ * Beyond the bounds it ends the behaviour like RMC_SIM_TRUNCATE.  Wide layout
+ * only (rmc_simulate refuses it on the packed one). */
 #define RMC_SIM_TLC 2
 typedef struct rmc_sim_config {
     uint64_t behaviours;       /* random behaviours to run                        */

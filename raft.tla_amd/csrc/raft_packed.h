@@ -109,6 +109,41 @@ static __constant__ u64 c_fp_salt;  // visible to both passes (HIP_SYMBOL needs 
 RMC_HD u64 hS(u64 w, u32 i) { return mix64(w ^ ((u64)(i + 1) << 59) ^ RMC_FP_SALT); }
 RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59) ^ RMC_FP_SALT) : 0ull; }
 
+// A state's fingerprint is two order-free sums over its components: k = sum of
+// the mixes a (the 64-bit key stored in the fingerprint set, as TLC's FP64) and
+// s = sum of smix(a) mod 2^32, a second, nonlinear function of each mix (the
+// high half of a 32 x 32-bit product of its two halves: one v_mul_hi_u32).  The
+// set's slot is taken from k and the stored value is k ^ (s within the slot
+// mask) (fp_value): two distinct states collide only if their k AND those bits
+// of s agree, 64 + min(32, log2 slots) bits instead of 64 — at 4.13 G states
+// the 64-bit birthday bound alone expects 0.46 collisions (DESIGN.md
+// "Fingerprints").
+RMC_HD u32 smix(u64 a) {
+    return (u32)(((u64)((u32)a ^ 0x9E3779B9u) * (u64)((u32)(a >> 32) ^ 0x7F4A7C15u)) >> 32);
+}
+struct Fp {
+    u64 k;
+    u32 s;
+};
+RMC_HD Fp fp_of(u64 a) { return Fp{a, smix(a)}; }
+RMC_HD void fp_add(Fp& h, u64 a) { h.k += a; h.s += smix(a); }
+RMC_HD void fp_sub(Fp& h, u64 a) { h.k -= a; h.s -= smix(a); }
+// A fingerprint's place in a table of mask + 1 slots: the value stored /
+// compared, v = k ^ (s & mask) (never 0, the empty slot), and the first slot
+// of its probe sequence, k & mask.  The one fingerprint whose value would be 0
+// flips bit 0 of s (fp_norm, in every caller alike), so the slot is always
+// (v ^ s) & mask and callers may keep (v, s) only (fp_slot).
+RMC_HD u32 fp_norm(u64 k, u32 s32, u64 mask) { return (k ^ ((u64)s32 & mask)) == 0 ? (s32 ^ 1u) : s32; }
+RMC_HD u64 fp_v(u64 k, u32 s32n, u64 mask) { return k ^ ((u64)s32n & mask); }
+RMC_HD u64 fp_slot(u64 v, u32 s32n, u64 mask) { return (v ^ (u64)s32n) & mask; }
+struct TKey {
+    u64 v, s0;
+};
+RMC_HD TKey tkey(const Fp& h, u64 mask) {
+    const u32 s = fp_norm(h.k, h.s, mask);
+    return TKey{fp_v(h.k, s, mask), h.k & mask};
+}
+
 // Owner rank of a fingerprint in sharded mode: its top 32 bits scaled to
 // [0, world).  The fingerprint-set slot uses the low bits, so every shard's
 // table stays uniformly loaded.
@@ -471,9 +506,9 @@ RMC_HD void lane_delta_desc(const u64 (&w)[S], const u32 (&m)[K], u32 desc, cons
 // Apply a delta: fingerprint and CONSTRAINT (parent assumed in-constraint).
 // Returns 1 if the successor is in the model; *h receives its fingerprint.
 template <int S, int K>
-RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d, const Params& P,
-                    u64* h, int* nmsg_out = nullptr) {
-    u64 hh = h0;
+RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], const Fp& h0, const Delta& d, const Params& P,
+                    Fp* h, int* nmsg_out = nullptr) {
+    Fp hh = h0;
     int nmsg = 0;
 #pragma unroll
     for (int q = 0; q < K; ++q) nmsg += m[q] ? 1 : 0;
@@ -481,12 +516,15 @@ RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d
         const u64 wo = selw<S>(w, d.srv);
         if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
         if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
-        if (d.w_new != wo) hh += hS(d.w_new, (u32)d.srv) - hS(wo, (u32)d.srv);
+        if (d.w_new != wo) {
+            fp_add(hh, hS(d.w_new, (u32)d.srv));
+            fp_sub(hh, hS(wo, (u32)d.srv));
+        }
     }
     if (d.rm >= 0) {
         const u32 sl = selm<K>(m, d.rm);
-        hh -= hM(sl);
-        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
+        fp_sub(hh, hM(sl));
+        if (m_cnt(sl) > 1) fp_add(hh, hM(sl - CNT_ONE));
         else nmsg -= 1;
     }
     if (d.has_add) {
@@ -496,11 +534,12 @@ RMC_HD int delta_fp(const u64 (&w)[S], const u32 (&m)[K], u64 h0, const Delta& d
         if (found >= 0) {
             const u32 sl = selm<K>(m, found);
             if ((int)m_cnt(sl) + 1 > P.max_dup) return 0;
-            hh += hM(sl + CNT_ONE) - hM(sl);
+            fp_add(hh, hM(sl + CNT_ONE));
+            fp_sub(hh, hM(sl));
         } else {
             if (1 > P.max_dup) return 0;
             nmsg += 1;
-            hh += hM(d.add | CNT_ONE);
+            fp_add(hh, hM(d.add | CNT_ONE));
         }
     }
     if (nmsg > P.max_msgs) return 0;
@@ -518,17 +557,21 @@ template <int S, int K>
 struct ParentMix {
     u64 hw[S];
     u64 hm[K];
-    u64 h0;
+    Fp h0;
     int nmsg;
 };
 template <int S, int K>
 RMC_HD void parent_mix(const u64 (&w)[S], const u32 (&m)[K], ParentMix<S, K>& pm) {
-    pm.h0 = 0;
+    pm.h0 = Fp{0, 0};
     pm.nmsg = 0;
 #pragma unroll
-    for (int i = 0; i < S; ++i) { pm.hw[i] = hS(w[i], (u32)i); pm.h0 += pm.hw[i]; }
+    for (int i = 0; i < S; ++i) { pm.hw[i] = hS(w[i], (u32)i); fp_add(pm.h0, pm.hw[i]); }
 #pragma unroll
-    for (int q = 0; q < K; ++q) { pm.hm[q] = hM(m[q]); pm.h0 += pm.hm[q]; pm.nmsg += m[q] ? 1 : 0; }
+    for (int q = 0; q < K; ++q) {
+        pm.hm[q] = hM(m[q]);
+        if (m[q]) fp_add(pm.h0, pm.hm[q]);
+        pm.nmsg += m[q] ? 1 : 0;
+    }
 }
 template <int N>
 RMC_HD u64 sel64(const u64 (&a)[N], int i) {
@@ -540,11 +583,11 @@ RMC_HD u64 sel64(const u64 (&a)[N], int i) {
 // delta_fp with the parent's mixes precomputed: same result, fewer mixes.
 template <int S, int K>
 RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d,
-                        const Params& P, u64* h, int* nmsg_out = nullptr, u64* hw_new = nullptr) {
+                        const Params& P, Fp* h, int* nmsg_out = nullptr, u64* hw_new = nullptr) {
     // early returns on purpose: a branch-light form (bounds as predicates, only
     // the mixes under branches) measured 306 vs 289-294 ms per MCraftBench BFS —
     // out-of-model lanes then pay for the whole computation
-    u64 hh = pm.h0;
+    Fp hh = pm.h0;
     int nmsg = pm.nmsg;
     if (d.srv >= 0) {
         if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
@@ -552,13 +595,16 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
         const u64 wo = selw<S>(w, d.srv);
         const u64 ho = sel64<S>(pm.hw, d.srv);
         const u64 hn = d.w_new != wo ? hS(d.w_new, (u32)d.srv) : ho;
-        hh += hn - ho;
+        if (hn != ho) {
+            fp_add(hh, hn);
+            fp_sub(hh, ho);
+        }
         if (hw_new) *hw_new = hn;  // the new word's mix (the sharded owner reuses it)
     }
     if (d.rm >= 0) {
         const u32 sl = selm<K>(m, d.rm);
-        hh -= sel64<K>(pm.hm, d.rm);
-        if (m_cnt(sl) > 1) hh += hM(sl - CNT_ONE);
+        fp_sub(hh, sel64<K>(pm.hm, d.rm));
+        if (m_cnt(sl) > 1) fp_add(hh, hM(sl - CNT_ONE));
         else nmsg -= 1;
     }
     if (d.has_add) {
@@ -568,11 +614,12 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
         if (found >= 0) {
             const u32 sl = selm<K>(m, found);
             if ((int)m_cnt(sl) + 1 > P.max_dup) return 0;
-            hh += hM(sl + CNT_ONE) - sel64<K>(pm.hm, found);
+            fp_add(hh, hM(sl + CNT_ONE));
+            fp_sub(hh, sel64<K>(pm.hm, found));
         } else {
             if (1 > P.max_dup) return 0;
             nmsg += 1;
-            hh += hM(d.add | CNT_ONE);
+            fp_add(hh, hM(d.add | CNT_ONE));
         }
     }
     if (nmsg > P.max_msgs) return 0;
@@ -711,12 +758,13 @@ RMC_HD int capacity_exceeded(const u32 (&m)[K], const Delta& d, const Params& P)
 }
 
 template <int S, int K>
-RMC_HD u64 state_fp(const u64 (&w)[S], const u32 (&m)[K]) {
-    u64 h = 0;
+RMC_HD Fp state_fp(const u64 (&w)[S], const u32 (&m)[K]) {
+    Fp h{0, 0};
 #pragma unroll
-    for (int i = 0; i < S; ++i) h += hS(w[i], (u32)i);
+    for (int i = 0; i < S; ++i) fp_add(h, hS(w[i], (u32)i));
 #pragma unroll
-    for (int q = 0; q < K; ++q) h += hM(m[q]);
+    for (int q = 0; q < K; ++q)
+        if (m[q]) fp_add(h, hM(m[q]));
     return h;
 }
 
@@ -1213,14 +1261,17 @@ RMC_HD bool sig_rank(const Sig<S>& sg, u32* lo, u32* tc) {
 }
 // Fingerprint of pi(s) (any slot order; empty slots are 0).
 template <int S, int K1>
-RMC_HD u64 fp_perm(const u64 (&w)[S], const u32 (&m)[K1], u32 code) {
-    u64 h = 0;
+RMC_HD Fp fp_perm(const u64 (&w)[S], const u32 (&m)[K1], u32 code) {
+    Fp h{0, 0};
 #pragma unroll
-    for (int i = 0; i < S; ++i) h += hS(perm_word<S>(w[i], code), pe(code, (u32)i));
+    for (int i = 0; i < S; ++i) fp_add(h, hS(perm_word<S>(w[i], code), pe(code, (u32)i)));
 #pragma unroll
-    for (int q = 0; q < K1; ++q) h += hM(perm_slot(m[q], code));
+    for (int q = 0; q < K1; ++q)
+        if (m[q]) fp_add(h, hM(perm_slot(m[q], code)));
     return h;
 }
+// The order of canonical candidates: least k, then least s.
+RMC_HD bool fp_less(const Fp& a, const Fp& b) { return a.k < b.k || (a.k == b.k && a.s < b.s); }
 // A state passed by value (out-of-line calls keep their registers apart).
 template <int S, int K1>
 struct SymState {
@@ -1232,8 +1283,8 @@ struct SymState {
 // [lo_i, lo_i + tc_i) (3 bits per server in lo / tc).  Out of line: the
 // common untied path stays small.
 template <int S, int K1>
-RMC_HD u64 canon_ties(const SymState<S, K1> t, u32 lo, u32 tc, const u32* codes, int np) {
-    u64 best = ~0ull;
+RMC_HD Fp canon_ties(const SymState<S, K1> t, u32 lo, u32 tc, const u32* codes, int np) {
+    Fp best{~0ull, ~0u};
     for (int p = 0; p < np; ++p) {
         const u32 c = codes[p];
         bool ok = true;
@@ -1243,8 +1294,8 @@ RMC_HD u64 canon_ties(const SymState<S, K1> t, u32 lo, u32 tc, const u32* codes,
             ok &= pos >= l && pos < l + pe(tc, (u32)i);
         }
         if (ok) {
-            const u64 h = fp_perm<S, K1>(t.w, t.m, c);
-            best = h < best ? h : best;
+            const Fp h = fp_perm<S, K1>(t.w, t.m, c);
+            best = fp_less(h, best) ? h : best;
         }
     }
     return best;
@@ -1254,14 +1305,14 @@ RMC_HD u64 canon_ties(const SymState<S, K1> t, u32 lo, u32 tc, const u32* codes,
 // single-GPU SYMMETRY kernel defers those lanes to k_ties, so its hot loop
 // carries no permutation enumeration).
 template <int S, int K1, bool NOTIE = false>
-RMC_HD u64 canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const Sig<S>& sg, const u32* codes, int np,
-                        int* tied = nullptr) {
+RMC_HD Fp canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const Sig<S>& sg, const u32* codes, int np,
+                       int* tied = nullptr) {
     u32 lo, tc;
     const bool tie = sig_rank<S>(sg, &lo, &tc);
     if (!tie) return fp_perm<S, K1>(w, m, lo);  // the sorting permutation: server i -> its rank
     if constexpr (NOTIE) {
         *tied = 1;
-        return 0;
+        return Fp{0, 0};
     }
     SymState<S, K1> t;
 #pragma unroll
@@ -1272,7 +1323,7 @@ RMC_HD u64 canon_sorted(const u64 (&w)[S], const u32 (&m)[K1], const Sig<S>& sg,
 }
 // The canonical key of a stored (materialised) state.
 template <int S, int K>
-RMC_HD u64 canon_state(const u64 (&w)[S], const u32 (&m)[K], const u32* codes, int np) {
+RMC_HD Fp canon_state(const u64 (&w)[S], const u32 (&m)[K], const u32* codes, int np) {
     u64 base[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) base[i] = sig_base<S>(w[i], (u32)i);
@@ -1284,8 +1335,8 @@ RMC_HD u64 canon_state(const u64 (&w)[S], const u32 (&m)[K], const u32* codes, i
 // words and slots (unsorted: fingerprints are order-free), the parent's
 // signature bases reused for the servers the delta leaves alone.
 template <int S, int K, bool NOTIE = false>
-RMC_HD u64 canon_delta(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], const Delta& d, const u32* codes,
-                       int np, int* tied = nullptr) {
+RMC_HD Fp canon_delta(const u64 (&w)[S], const u32 (&m)[K], const u64 (&base)[S], const Delta& d, const u32* codes,
+                      int np, int* tied = nullptr) {
     u64 ws[S], bs[S];
     u32 ms[K + 1];
 #pragma unroll

@@ -556,12 +556,56 @@ RMC_HD int wcheck_invariants(const WModel& M, const WState& s) {
     return 0;
 }
 
-// Fingerprint of a canonical record (every byte; salted like the packed one).
-RMC_HD u64 wfp(const WState& s, u64 salt) {
+RMC_HD u64 w_rand(u64& x) {  // splitmix64 stream (the simulators' draws)
+    x += 0x9E3779B97F4A7C15ull;
+    return mix64(x);
+}
+
+// TLC's simulator draw (tlc2.tool.Simulator, restated): Next's actions in
+// order — every instance of Restart .. AppendEntries (TLC splits \E over the
+// constant Server / Value sets into separate actions) and Receive,
+// DuplicateMessage, DropMessage as one action each (their \E m \in DOMAIN
+// messages ranges over the state) — are visited from a uniformly random start
+// index with a random prime stride; the first action with a successor is taken
+// and one of its successors drawn uniformly.  The strides are primes larger
+// than any action count (at most 83 actions), so every stride visits every
+// action.  en: the enabled lanes (bit l of en[l >> 6]); returns the lane, -1
+// if none is enabled.
+template <int NC>
+RMC_HD int tlc_draw(const u64 (&en)[NC], int nl, int o7, int o8, int o9, u64& rs) {
+    auto on = [&](int lane) { return ((en[lane >> 6] >> (lane & 63)) & 1ull) != 0; };
+    const int nact = o7 + 3;
+    const u32 primes[8] = {89, 97, 101, 103, 107, 109, 113, 127};
+    const u32 start = (u32)(w_rand(rs) % (u64)nact), stride = primes[w_rand(rs) & 7u];
+    for (int i = 0; i < nact; ++i) {
+        const int a = (int)((start + (u32)i * stride) % (u32)nact);
+        if (a < o7) {
+            if (on(a)) return a;
+            continue;
+        }
+        const int f = a - o7, lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
+        u32 cnt = 0;
+        for (int lane = lo; lane < hi; ++lane) cnt += on(lane) ? 1u : 0u;
+        if (!cnt) continue;
+        u32 k = (u32)(w_rand(rs) % (u64)cnt);
+        for (int lane = lo; lane < hi; ++lane)
+            if (on(lane) && k-- == 0) return lane;
+    }
+    return -1;
+}
+
+// Fingerprint of a canonical record (every byte; salted like the packed one):
+// k the chained mix over the words, s the sum of smix over the chain's states
+// (raft_packed.h Fp: the second 32 bits the fingerprint set folds in).
+RMC_HD Fp wfp(const WState& s, u64 salt) {
     const u64* w = reinterpret_cast<const u64*>(&s);
     u64 h = 0x6A09E667F3BCC909ull ^ salt;
-    for (int k = 0; k < WWORDS; ++k) h = mix64(h ^ (w[k] + (u64)k * 0x9E3779B97F4A7C15ull));
-    return h ? h : 1ull;
+    u32 s2 = 0;
+    for (int k = 0; k < WWORDS; ++k) {
+        h = mix64(h ^ (w[k] + (u64)k * 0x9E3779B97F4A7C15ull));
+        s2 += smix(h);
+    }
+    return Fp{h, s2};
 }
 
 }  // namespace wide

@@ -825,7 +825,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.depth = depth;
     const double D = (double)c->res.distinct, G = (double)c->res.generated;
     // TLC's "calculated (optimistic)" fingerprint-collision estimate
-    c->res.collision_probability = D * (G - D) / 18446744073709551616.0;
+    c->res.collision_probability = fp_collision_estimate(D, G, c->table_slots);
     c->res.seconds = secs();
     // lane efficiency of the walk: enabled lanes / visited slots (the kernels count
     // the slots only when built with -DRMC_WALK_STATS_BUILD: a register in the hot loop)
@@ -862,7 +862,8 @@ int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
 namespace {
 // The header embeds the ABI structs rmc_config and rmc_result, so its size is
 // written too and must match: a struct that grows changes kCkptVersion.
-constexpr uint32_t kCkptVersion = 3;  // 3: rmc_result with parked / exchange_wait_seconds
+constexpr uint32_t kCkptVersion = 4;  // 3: rmc_result with parked / exchange_wait_seconds; 4: the set holds
+                                      // k ^ s values (raft_packed.h Fp), rmc_result with spill_links_on_device
 struct CkptHeader {
     char magic[8];
     uint32_t version, nw;

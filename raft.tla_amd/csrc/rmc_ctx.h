@@ -25,7 +25,7 @@ struct DistState {
     // Outbox sets, double-buffered: the expansion of round k + 1 (ctx stream)
     // fills one set while round k's exchange (xs) drains the other.
     struct Set {
-        rmc::u64* key_out = nullptr;             // [world][kcap] keys per owner
+        rmc::u64* key_out = nullptr;             // [world][kcap][2] keys per owner (k, s32)
         rmc::u64* tick_out = nullptr;            // [world][kcap] tickets (parent | lane << 56)
         unsigned long long* ocount = nullptr;    // [world] keys written per owner, [world]: pool records
         rmc::u32* pool = nullptr;                // remote-successor pool (phase-2 records, flush_pool)
@@ -40,7 +40,7 @@ struct DistState {
     hipEvent_t ev_cnt = nullptr, ev_acc = nullptr, ev_c = nullptr, ev_x = nullptr;
     hipEvent_t ev_h = nullptr;      // host waits on xs (under the deadline)
     // single buffers (used on xs only, rounds in order)
-    rmc::u64* key_in = nullptr;     // keys received, blocks by source
+    rmc::u64* key_in = nullptr;     // keys received (k, s32 pairs), blocks by source
     uint8_t* rep_out = nullptr;     // replies to the keys received (same layout)
     uint8_t* rep_in = nullptr;      // replies to the keys sent, [world][kcap]
     rmc::u32* st_in = nullptr;      // accepted states received, blocks by source
@@ -148,6 +148,14 @@ struct rmc_ctx {
     } while (0)
 
 namespace rmc_host {
+// TLC's "calculated (optimistic)" collision estimate D * (G - D) / 2^b for the
+// fingerprint bits b the set compares: 64 of k plus the bits of the second sum
+// folded in under the slot mask, min(32, log2 slots) (raft_packed.h Fp).
+inline double fp_collision_estimate(double D, double G, rmc::u64 slots) {
+    int lb = 0;
+    while (lb < 32 && (2ull << lb) <= slots) ++lb;
+    return D * (G - D) / 18446744073709551616.0 / (double)(1ull << lb);
+}
 int fail(rmc_ctx* c, int code, const std::string& msg);
 int kcap_for(int max_msgs);
 int validate(const rmc_config* c, std::string* why);

@@ -39,6 +39,10 @@ using namespace rmc_host;
 
 namespace {
 
+// Bytes per phase-1 key record: the raw fingerprint (k, s32) as two u64
+// (raft_packed.h Fp; the owner derives its own table value and slot).
+constexpr u64 KEYB = 16;
+
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -648,10 +652,11 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             for (int p = 0; p < W; ++p) {
                 global_more |= (rx(cx, p)[1] & 1u) != 0;
                 global_sends |= (rx(cx, p)[1] & 4u) != 0;
-                scnt[(size_t)p] = cx[RWD * (u64)p] * 8;
-                soff[(size_t)p] = (u64)p * kcap * 8;
-                rcnt[(size_t)p] = rx(cx, p)[0] * 8;
-                roff[(size_t)p] = tot_in * 8;
+                // phase-1 key records: the raw fingerprint (k, s32) in two u64 (KEYB bytes)
+                scnt[(size_t)p] = cx[RWD * (u64)p] * KEYB;
+                soff[(size_t)p] = (u64)p * kcap * KEYB;
+                rcnt[(size_t)p] = rx(cx, p)[0] * KEYB;
+                roff[(size_t)p] = tot_in * KEYB;
                 tot_in += rx(cx, p)[0];
                 mx = std::max(mx, cx[RWD * (u64)p]);
                 D.keys_sent += cx[RWD * (u64)p];
@@ -706,13 +711,13 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             HIPCHK(c, hipMemsetAsync(D.sa, 0, 16 * (u64)W, D.xs));
             if (int rc = a2a(c, S.key_out, soff.data(), scnt.data(), D.key_in, roff.data(), rcnt.data())) return rc;
             SrcOff so{};
-            for (int p = 0; p < W; ++p) so.o[p] = roff[(size_t)p] / 8;
+            for (int p = 0; p < W; ++p) so.o[p] = roff[(size_t)p] / KEYB;
             so.o[W] = tot_in;
             HIPCHK(c, launch_owner_insert(c->B, D.key_in, D.rep_out, tot_in, so, D.sa + W, D.xs));
             for (int p = 0; p < W; ++p) {  // block p of rep_out (keys from p) back to p; from d into rep_in + d * kcap
-                s2[(size_t)p] = rcnt[(size_t)p] / 8;
-                o2[(size_t)p] = roff[(size_t)p] / 8;
-                r2[(size_t)p] = scnt[(size_t)p] / 8;
+                s2[(size_t)p] = rcnt[(size_t)p] / KEYB;
+                o2[(size_t)p] = roff[(size_t)p] / KEYB;
+                r2[(size_t)p] = scnt[(size_t)p] / KEYB;
                 q2[(size_t)p] = (u64)p * kcap;
             }
             D.phase = "phase 1 (replies)";
@@ -844,7 +849,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.exchange_wait_seconds = D.wait_seconds;
     c->res.parked = D.parked;
     const double Dd = (double)total_prev, G = (double)generated;
-    c->res.collision_probability = Dd * (G - Dd) / 18446744073709551616.0;
+    c->res.collision_probability = fp_collision_estimate(Dd, G, c->table_slots);
     c->res.seconds = now_s() - t0;
     D.phase = "done";
     return 0;
@@ -945,12 +950,12 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     // (the default kernel keeps send markers in the fingerprint set instead)
     if (!c->sh.verify && c->sh.sym) ok = ok && hipMalloc(&c->B.sent, slots * 8) == hipSuccess;
     const u64 ovf_cap = std::max<u64>(W * kcap, 1ull << 20);  // parked keys per level: >= a round's worth
-    ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 16) == hipSuccess;
+    ok = ok && hipMalloc(&c->B.ovf, ovf_cap * 24) == hipSuccess;  // {k, s32 | flags, ticket}
     // the pool flush's remote successors of one round: as many as the round's
     // outboxes hold (a fuller pool parks tickets); none leave a world of one
     D.pool_cap = world > 1 ? W * kcap : 64;
     for (auto& S : D.set) {
-        ok = ok && hipMalloc(&S.key_out, W * kcap * 8) == hipSuccess && hipMalloc(&S.tick_out, W * kcap * 8) == hipSuccess &&
+        ok = ok && hipMalloc(&S.key_out, W * kcap * KEYB) == hipSuccess && hipMalloc(&S.tick_out, W * kcap * 8) == hipSuccess &&
              hipMalloc(&S.ocount, 8 * (W + 1)) == hipSuccess && hipMalloc(&S.cx, 8 * (2 * kRowWords * W + 1)) == hipSuccess &&
              hipMalloc(&S.pool, D.pool_cap * RB) == hipSuccess &&
              hipHostMalloc(&S.h_cx, 8 * (2 * kRowWords * W + 1), hipHostMallocDefault) == hipSuccess;
@@ -969,7 +974,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
         ok = ok && hipMalloc(&D.rep_send, D.rep_max * rbr) == hipSuccess &&
              hipMalloc(&D.rep_buf, D.rep_max * rbr) == hipSuccess;
     }
-    ok = ok && hipMalloc(&D.key_in, W * kcap * 8) == hipSuccess && hipMalloc(&D.rep_out, W * kcap) == hipSuccess &&
+    ok = ok && hipMalloc(&D.key_in, W * kcap * KEYB) == hipSuccess && hipMalloc(&D.rep_out, W * kcap) == hipSuccess &&
          hipMalloc(&D.rep_in, W * kcap) == hipSuccess && hipMalloc(&c->B.st_out, W * kcap * RB) == hipSuccess &&
          hipMalloc(&D.st_in, W * kcap * RB) == hipSuccess && hipMalloc(&D.sa, 16 * W) == hipSuccess &&
          hipHostMalloc(&D.h_sa, 16 * W, hipHostMallocDefault) == hipSuccess &&

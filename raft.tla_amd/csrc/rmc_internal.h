@@ -45,16 +45,16 @@ struct DevBufs {
     u64* sent;                 // lossy cache of fingerprints already shipped to their owner
     u64 smask;                 // sent-cache slots - 1
     // two-phase exchange: phase 1 keys, phase 2 accepted states
-    u64* key_out;              // [world][kcap] keys for each owner
+    u64* key_out;              // [world][kcap][2] keys for each owner: the raw fingerprint (k, s32)
     u64* tick_out;             // [world][kcap] local tickets: parent index | lane << 56, or POOL_TICK | pool index
     u64 kcap;                  // keys per destination and chunk
     unsigned long long* ocount;  // [world] keys written per destination
     u32* st_out;               // [world][scap][NW + 4] accepted states for each owner (+ ref, footprint)
     u64 scap;                  // state records per destination and round (= kcap)
     unsigned long long* scount;  // [world] state records written per destination
-    // keys whose owner's outbox was full: {key, parent index | dest << 48 | lane << 56},
-    // sent in later exchange rounds of the same level (never dropped); key 0: a
-    // successor the expansion could not put in the pool, keyed by k_route
+    // keys whose owner's outbox was full: {k, s32 | flags << 32, parent index | dest << 48 |
+    // lane << 56}, sent in later exchange rounds of the same level (never dropped);
+    // flag OVF_UNKEYED: a successor the expansion could not put in the pool, keyed by k_route_fix
     u64* ovf;
     u64 ovf_cap;               // records in ovf
     // remote-successor pool (the sharded expansion's default flush, flush_pool):
@@ -115,7 +115,7 @@ struct SimCounters {
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
                       int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
 
-// Sharded mode, phase 1 owner side: insert n received keys, reply[t] = new;
+// Sharded mode, phase 1 owner side: insert n received keys (k, s32 pairs), reply[t] = new;
 // keys [src_off[p], src_off[p + 1]) came from rank p, acc[p] += keys of p that were new.
 constexpr int kMaxWorld = 64;
 struct SrcOff {

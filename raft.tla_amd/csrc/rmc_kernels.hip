@@ -27,13 +27,14 @@ __device__ __forceinline__ u64 bcast64(u64 v, int src) {
     return ((u64)hi << 32) | lo;
 }
 
-// Open-addressing insert of a non-zero 64-bit fingerprint, linear probing.
+// Open-addressing insert of a non-zero 64-bit value v whose probe sequence
+// starts at slot s0, linear probing.
 // Returns 1 if this lane inserted the key, 0 if it was present (or the table
 // is full, flagged in *full).  Plain probe loads may be stale only in the
 // EMPTY direction (slots go 0 -> key once); the CAS (agent scope, executed at
 // the memory side) settles every race.
-__device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 key, u32* full) {
-    u64 s = key & mask;
+__device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 s0, u64 key, u32* full) {
+    u64 s = s0;
     for (u64 n = 0; n <= mask; ++n) {
         const u64 cur = table[s];
         if (cur == key) return 0;
@@ -49,8 +50,8 @@ __device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 
 }
 
 // fp_insert that also reports the slot holding the key (verification mode).
-__device__ __forceinline__ int fp_insert_at(u64* __restrict__ table, u64 mask, u64 key, u32* full, u64* at) {
-    u64 s = key & mask;
+__device__ __forceinline__ int fp_insert_at(u64* __restrict__ table, u64 mask, u64 s0, u64 key, u32* full, u64* at) {
+    u64 s = s0;
     for (u64 n = 0; n <= mask; ++n) {
         const u64 cur = table[s];
         if (cur == key) { *at = s; return 0; }
@@ -66,16 +67,29 @@ __device__ __forceinline__ int fp_insert_at(u64* __restrict__ table, u64 mask, u
     return 0;
 }
 
-// Same protocol, given the already-loaded content `cur` of the first slot.
-__device__ __forceinline__ int fp_resolve(u64* __restrict__ table, u64 mask, u64 key, u64 cur, u32* full) {
+// Same protocol, given the already-loaded content `cur` of the first slot s0.
+__device__ __forceinline__ int fp_resolve(u64* __restrict__ table, u64 mask, u64 s0, u64 key, u64 cur, u32* full) {
     if (cur == key) return 0;
-    const u64 s = key & mask;
     if (cur == 0) {
-        const u64 prev = atomicCAS((unsigned long long*)&table[s], 0ull, (unsigned long long)key);
+        const u64 prev = atomicCAS((unsigned long long*)&table[s0], 0ull, (unsigned long long)key);
         if (prev == 0) return 1;
         if (prev == key) return 0;
     }
-    return fp_insert(table, mask, key, full);  // rare: continue linear probing
+    return fp_insert(table, mask, s0, key, full);  // rare: continue linear probing
+}
+// Insert fingerprint h (raft_packed.h Fp) into the table.
+__device__ __forceinline__ int fp_insert_fp(u64* __restrict__ table, u64 mask, const Fp& h, u32* full) {
+    const TKey t = tkey(h, mask);
+    return fp_insert(table, mask, t.s0, t.v, full);
+}
+// rmc_set_fp_bits (verification tests): only the kept bits of k, no second sum,
+// so a weakened fingerprint collides as often as its width says.
+__device__ __forceinline__ Fp fp_weaken(Fp h, u64 fp_mask) {
+    if (fp_mask != ~0ull) {
+        h.k &= fp_mask;
+        h.s = 0;
+    }
+    return h;
 }
 
 template <int S, int K>
@@ -344,9 +358,9 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
 }
 
 template <int S, int K, bool SYM>
-__device__ __forceinline__ u64 verify_key(const u64 (&w)[S], const u32 (&m)[K], const Params& P, const PermTable& PT) {
-    const u64 k = (SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m)) & P.fp_mask;
-    return k ? k : 1ull;
+__device__ __forceinline__ TKey verify_key(const u64 (&w)[S], const u32 (&m)[K], const Params& P, const PermTable& PT,
+                                           u64 tmask) {
+    return tkey(fp_weaken(SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m), P.fp_mask), tmask);
 }
 
 // sidx[slot of state i's fingerprint] = i for the stored states [lo, hi).
@@ -357,10 +371,10 @@ __global__ __launch_bounds__(256) void k_publish(const Params P, const PermTable
         u64 w[S];
         u32 m[K];
         load_state<S, K>(B.store + i * (u64)NW, w, m);
-        const u64 key = verify_key<S, K, SYM>(w, m, P, PT);
-        u64 s = key & B.tmask;
+        const TKey key = verify_key<S, K, SYM>(w, m, P, PT, B.tmask);
+        u64 s = key.s0;
         u64 n = 0;
-        while (B.table[s] != key && n <= B.tmask) { s = (s + 1) & B.tmask; ++n; }
+        while (B.table[s] != key.v && n <= B.tmask) { s = (s + 1) & B.tmask; ++n; }
         if (n > B.tmask) atomicOr(&B.ctr->overflow, 8u);  // a stored state without its key
         else B.sidx[s] = i;
     }
@@ -450,9 +464,31 @@ __device__ __forceinline__ u32 owner_succ(u64 key, const Delta& d, const ParentM
 }
 
 template <int S, int K>
-__device__ __forceinline__ u64 fp_of_materialised(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
-    const u64 h = state_fp<S, K>(w, m);  // = the incremental key: the fp is order-free
-    return h ? h : 1ull;
+__device__ __forceinline__ Fp fp_of_materialised(const u64 (&w)[S], const u32 (&m)[K], const Params& P) {
+    return state_fp<S, K>(w, m);  // = the incremental key: the fp is order-free
+}
+
+// Phase-1 keys travel as the raw fingerprint (k, low 32 bits of s): the owner
+// derives its own table value and slot (tkey; tables may differ in size across
+// ranks).  Outbox: two u64 per key; parking (B.ovf): {k, s32 | flags << 32,
+// ticket}, where flag OVF_UNKEYED marks a ticket the expansion parked without
+// computing its key (k_route_fix computes it).
+constexpr u64 OVF_UNKEYED = 1ull << 32;
+__device__ __forceinline__ void put_key(const DevBufs& B, u32 dest, u64 slot, u64 k, u32 s32, u64 tick) {
+    u64* o = B.key_out + 2 * ((u64)dest * B.kcap + slot);
+    o[0] = k;
+    o[1] = s32;
+    B.tick_out[(u64)dest * B.kcap + slot] = tick;
+}
+__device__ __forceinline__ void park_key(const DevBufs& B, u64 k, u64 s_and_flags, u64 tick) {
+    const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
+    if (q < B.ovf_cap) {
+        B.ovf[3 * q] = k;
+        B.ovf[3 * q + 1] = s_and_flags;
+        B.ovf[3 * q + 2] = tick;
+    } else {
+        atomicOr(&B.ctr->overflow, 2u);  // the parking buffer is full too: fatal
+    }
 }
 
 // Sharded mode, phase 1 (fingerprint first): the listed
@@ -464,7 +500,8 @@ __device__ __forceinline__ u64 fp_of_materialised(const u64 (&w)[S], const u32 (
 // atomic per destination per flush.
 template <int S, int K>
 __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u64 lo, const u32* l_rel,
-                                           const uint8_t* l_lane, const uint8_t* l_dest, const u64* l_key, u32 n) {
+                                           const uint8_t* l_lane, const uint8_t* l_dest, const u64* l_key,
+                                           const u32* l_ks, u32 n) {
     constexpr int NW = 2 * S + K;
     wave_sync_lds();
     const int me = (int)__lane_id();
@@ -505,17 +542,12 @@ __device__ __forceinline__ void flush_dist(const Params& P, const DevBufs& B, u6
                 // the owner's outbox is full: park the key with its ticket; a later
                 // exchange round of this level sends it (the sent-cache entry
                 // written at probe time stays right: the key IS sent)
-                const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
-                if (q < B.ovf_cap) {
-                    B.ovf[2 * q] = l_key[e];
-                    B.ovf[2 * q + 1] = (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56);
-                } else {
-                    atomicOr(&B.ctr->overflow, 2u);  // the parking buffer is full too: fatal
-                }
+                // (the list holds the local table value: the raw k is v ^ (s32 & tmask))
+                park_key(B, l_key[e] ^ ((u64)l_ks[e] & B.tmask), l_ks[e],
+                         (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56));
                 continue;
             }
-            B.key_out[(u64)dest * B.kcap + slot] = l_key[e];
-            B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
+            put_key(B, dest, slot, l_key[e] ^ ((u64)l_ks[e] & B.tmask), l_ks[e], (lo + rel) | ((u64)lane << 56));
             continue;
         }
         if (slot >= B.cap) {
@@ -570,7 +602,7 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
                     u64 wo[S];
                     u32 mo[K];
                     materialise<S, K>(w, m, d, wo, mo);
-                    dest = owner_of(fp_of_materialised<S, K>(wo, mo, P), B.world);
+                    dest = owner_of(fp_of_materialised<S, K>(wo, mo, P).k, B.world);
                 } else {
                     dest = owner_succ_w<S>(0ull, d, w, B);
                 }
@@ -622,19 +654,12 @@ __device__ __forceinline__ void flush_mark(const Params& P, const DevBufs& B, u6
         u32 mo[K];
         materialise<S, K>(w, m, d, wo, mo);
         if (dest != B.rank) {  // the key to its owner, the ticket stays here
-            const u64 key = fp_of_materialised<S, K>(wo, mo, P);
+            const Fp key = fp_of_materialised<S, K>(wo, mo, P);
             if (slot >= B.kcap) {  // outbox full: parked, sent by a later round of this level
-                const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
-                if (q < B.ovf_cap) {
-                    B.ovf[2 * q] = key;
-                    B.ovf[2 * q + 1] = (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56);
-                } else {
-                    atomicOr(&B.ctr->overflow, 2u);
-                }
+                park_key(B, key.k, (u32)key.s, (lo + rel) | ((u64)dest << 48) | ((u64)lane << 56));
                 continue;
             }
-            B.key_out[(u64)dest * B.kcap + slot] = key;
-            B.tick_out[(u64)dest * B.kcap + slot] = (lo + rel) | ((u64)lane << 56);
+            put_key(B, dest, slot, key.k, (u32)key.s, (lo + rel) | ((u64)lane << 56));
             continue;
         }
         store_new<S, K>(P, B, slot, wo, mo, B.ref_tag | (lo + rel), lane, foot);
@@ -679,7 +704,7 @@ __device__ __forceinline__ void flush_pool(const Params& P, const DevBufs& B, u6
                     u64 wo[S];
                     u32 mo[K];
                     materialise<S, K>(w, m, d, wo, mo);
-                    own = owner_of(fp_of_materialised<S, K>(wo, mo, P), B.world) == B.rank;
+                    own = owner_of(fp_of_materialised<S, K>(wo, mo, P).k, B.world) == B.rank;
                 } else if (d.srv >= 0 && d.srv < owner_words<S>(B)) {
                     own = owner_succ_w<S>(0ull, d, w, B) == B.rank;
                 }
@@ -710,13 +735,7 @@ __device__ __forceinline__ void flush_pool(const Params& P, const DevBufs& B, u6
             continue;
         }
         if (!own && qr >= B.pool_cap) {  // pool full: park the ticket, k_route_fix keys it
-            const u64 o = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
-            if (o < B.ovf_cap) {
-                B.ovf[2 * o] = 0;
-                B.ovf[2 * o + 1] = (lo + rel) | ((u64)lane << 56);
-            } else {
-                atomicOr(&B.ctr->overflow, 2u);
-            }
+            park_key(B, 0ull, OVF_UNKEYED, (lo + rel) | ((u64)lane << 56));
             continue;
         }
         u64 w[S];
@@ -807,13 +826,15 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     // Sharded mode keeps per-probe owners in LDS too; a shorter list keeps the
     // block under 160 KB / 6 so it runs at the same 6 waves/SIMD as the
     // single-GPU kernel (VGPR-bound there).
-    constexpr int LCAP = SENTC ? 256 : WCAP;
+    constexpr int LCAP = SENTC ? 256 : MARK ? WCAP - 64 : WCAP;  // MARK: the owner byte per entry
     __shared__ u32 s_rel[4][LCAP];
     __shared__ uint8_t s_lane[4][LCAP];
     constexpr bool LDEST = SENTC || MARK;
     __shared__ uint8_t s_dest[LDEST ? 4 : 1][LDEST ? LCAP : 1];  // owner per listed successor
     __shared__ u64 s_lkey[SENTC ? 4 : 1][SENTC ? LCAP : 1];  // sharded: the key of each listed successor
-    __shared__ u64 s_key[BATCH][256];
+    __shared__ u32 s_lks[SENTC ? 4 : 1][SENTC ? LCAP : 1];   // ... and its s32 (fp_norm)
+    __shared__ u64 s_key[BATCH][256];  // per lane of the batch: the probe's table value (0 = no probe)
+    __shared__ u32 s_ks[BATCH][256];   // ... and its s32, which recovers its slot (fp_slot)
     __shared__ uint8_t s_own[LISTOWN ? BATCH : 1][LISTOWN ? 256 : 1];  // owner rank per probe
     const int wv = (int)(threadIdx.x >> 6);
     const int me = (int)__lane_id();
@@ -822,6 +843,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
     uint8_t* l_lane = s_lane[wv];
     uint8_t* l_dest = s_dest[LDEST ? wv : 0];
     u64* l_key = s_lkey[SENTC ? wv : 0];
+    u32* l_ks = s_lks[SENTC ? wv : 0];
     u32 n = 0;  // wave-uniform list length
     u32 gen = 0;  // generated lanes of this thread's states (< 2^32 per launch)
     u64 vchk = 0, vcol = 0;  // verification: hits compared, collisions
@@ -917,7 +939,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             mine = powner == B.rank;
         }
         ParentMix<S, K> pmx;
-        u64 h0;
+        Fp h0;
         if constexpr (PRE) {
             parent_mix<S, K>(w, m, pmx);
             h0 = pmx.h0;
@@ -988,7 +1010,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
 #pragma unroll UNROLL
             for (int b = 0; b < BATCH; ++b) {
                 const int lane = SORT ? (int)((lp >> (7 * b)) & 127u) : lane0 + b;
-                u64 key = 0;
+                u64 key = 0, slot0 = 0;  // the probe's table value (0: none) and first slot
+                u32 ks = 0;
                 int tied = 0;  // SYMMETRY: signatures tie, deferred to k_ties
                 if (lane < nl) {
                     Delta d;
@@ -996,7 +1019,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     else lane_delta<S, K>(w, m, lane, P, d);
                     const int en = d.en && live;
                     g += (u32)(en && mine);
-                    u64 h = 0;
+                    Fp h{0, 0};
                     u64 hwn = 0;  // DIST: the mix of the changed server word (owner routing)
                     int in_model = 0;
                     if constexpr (SYM) {
@@ -1018,30 +1041,32 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                                                           (REP || SENTC) ? &hwn : nullptr);
                         else in_model = delta_fp<S, K>(w, m, h0, d, P, &h, DIA ? &nmb : nullptr);
                         if constexpr (DIA)
-                            if (in_model && h != h0 &&
+                            if (in_model && h.k != h0.k &&
                                 (SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d, nmb, dm)
                                       : diamond_skip<S, K>(m, lane, d, nmb, dm, P)))
                                 in_model = 0;
                     }
-                    if (in_model && (SYM || h != h0)) {
-                        key = h;
-                        if constexpr (VERIFY) key &= P.fp_mask;
-                        key = key ? key : 1ull;
+                    if (in_model && (SYM || h.k != h0.k)) {  // (a stutter has the parent's k)
+                        if constexpr (VERIFY) h = fp_weaken(h, P.fp_mask);
+                        ks = fp_norm(h.k, (u32)h.s, B.tmask);
+                        key = fp_v(h.k, ks, B.tmask);
+                        slot0 = h.k & B.tmask;
                         if constexpr (REP) {  // a replicated level: only the owner probes
-                            if (owner_succ<S, K>(key, d, pmx, hwn, B, powner) != B.rank) key = 0;
+                            if (owner_succ<S, K>(h.k, d, pmx, hwn, B, powner) != B.rank) key = 0;
                         } else if constexpr (SENTC) {
                             if constexpr (PRE)
-                                s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(key, d, pmx, hwn, B, B.rank);
+                                s_own[b][threadIdx.x] = (uint8_t)owner_succ<S, K>(h.k, d, pmx, hwn, B, B.rank);
                             else  // no parent mixes: the successor's words 0 and 1 when it changes one
                                 s_own[b][threadIdx.x] = (uint8_t)(
                                     B.world == 1 ? 0u
-                                    : B.owner_mode == 0 ? owner_of(key, B.world)
-                                    : owner_succ_w<S>(key, d, w, B));
+                                    : B.owner_mode == 0 ? owner_of(h.k, B.world)
+                                    : owner_succ_w<S>(h.k, d, w, B));
                         }
                     }
                 }
                 s_key[b][threadIdx.x] = key;
-                if constexpr (PIPE != 0) cur_p[b] = key ? B.table[key & B.tmask] : 0ull;
+                s_ks[b][threadIdx.x] = ks;
+                if constexpr (PIPE != 0) cur_p[b] = key ? B.table[slot0] : 0ull;
                 if constexpr (TIEDEFER) {  // one queue atomic per wave and lane, not per tied successor
                     const u64 bal = __ballot(tied);
                     if (bal) {
@@ -1067,11 +1092,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     // no sent-cache in verification mode (B.sent null): every remote successor is shipped
                     cur[b] = !key[b] ? 0ull
                            : remote ? (B.sent ? B.sent[(key[b] >> 8) & B.smask] : 0ull)
-                                    : B.table[key[b] & B.tmask];
+                                    : B.table[fp_slot(key[b], s_ks[b][threadIdx.x], B.tmask)];
                 } else if constexpr (PIPE != 0) {
                     cur[b] = cur_p[PIPE ? b : 0];
                 } else {
-                    cur[b] = key[b] ? B.table[key[b] & B.tmask] : 0ull;
+                    cur[b] = key[b] ? B.table[fp_slot(key[b], s_ks[b][threadIdx.x], B.tmask)] : 0ull;
                 }
             }
 #pragma unroll
@@ -1085,7 +1110,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                 if (cur[b] == key[b]) {
                     if constexpr (VERIFY) {
                         hitbits |= 1u << b;
-                        s_key[b][threadIdx.x] = key[b] & B.tmask;  // the slot that holds the key
+                        s_key[b][threadIdx.x] = fp_slot(key[b], s_ks[b][threadIdx.x], B.tmask);  // the key's slot
                     }
                     continue;
                 }
@@ -1097,13 +1122,13 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     }
                 }
                 if (cur[b] == 0) {
-                    const u64 prev = atomicCAS((unsigned long long*)&B.table[key[b] & B.tmask], 0ull,
-                                               (unsigned long long)key[b]);
+                    const u64 sl0 = fp_slot(key[b], s_ks[b][threadIdx.x], B.tmask);
+                    const u64 prev = atomicCAS((unsigned long long*)&B.table[sl0], 0ull, (unsigned long long)key[b]);
                     if (prev == 0) newbits |= 1u << b;
                     else if (prev != key[b]) slowbits |= 1u << b;
                     else if constexpr (VERIFY) {
                         hitbits |= 1u << b;
-                        s_key[b][threadIdx.x] = key[b] & B.tmask;
+                        s_key[b][threadIdx.x] = sl0;
                     }
                 } else {
                     slowbits |= 1u << b;
@@ -1112,15 +1137,16 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             while (slowbits) {  // rare: linear probing past an occupied first slot
                 const int b = __builtin_ctz(slowbits);
                 slowbits &= slowbits - 1;
+                const u64 kv = s_key[b][threadIdx.x], sl0 = fp_slot(kv, s_ks[b][threadIdx.x], B.tmask);
                 if constexpr (VERIFY) {
                     u64 at = 0;
-                    if (fp_insert_at(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full, &at)) {
+                    if (fp_insert_at(B.table, B.tmask, sl0, kv, &B.ctr->table_full, &at)) {
                         newbits |= 1u << b;
                     } else {
                         hitbits |= 1u << b;
                         s_key[b][threadIdx.x] = at;  // the slot that holds the key
                     }
-                } else if (fp_insert(B.table, B.tmask, s_key[b][threadIdx.x], &B.ctr->table_full)) {
+                } else if (fp_insert(B.table, B.tmask, sl0, kv, &B.ctr->table_full)) {
                     newbits |= 1u << b;
                 }
             }
@@ -1166,6 +1192,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         if constexpr (SENTC) {
                             l_dest[pos] = s_own[b][threadIdx.x];
                             l_key[pos] = key[b];
+                            l_ks[pos] = s_ks[b][threadIdx.x];
                         }
                     }
                     n += (u32)__popcll(bal);
@@ -1173,7 +1200,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
                         else if constexpr (POOL) flush_pool<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
                         else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
-                        else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
+                        else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, l_ks, n);
                         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
                         n = 0;
                     }
@@ -1191,7 +1218,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         if constexpr (REP) flush_new<S, K, true>(P, B, lo, l_rel, l_lane, n);
         else if constexpr (POOL) flush_pool<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
         else if constexpr (MARK) flush_mark<S, K>(P, B, lo, l_rel, l_lane, l_dest, n);
-        else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, n);
+        else if constexpr (DIST) flush_dist<S, K>(P, B, lo, l_rel, l_lane, l_dest, l_key, l_ks, n);
         else flush_new<S, K>(P, B, lo, l_rel, l_lane, n);
     }
     // wave reductions of the generated and probe counts, one atomic each per wave
@@ -1308,7 +1335,7 @@ __global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64
         const u64 t = t0 + threadIdx.x;
         u32 src = 0xFFFFFFFFu;
         if (t < n) {
-            const int isnew = fp_insert(B.table, B.tmask, keys[t], &B.ctr->table_full);
+            const int isnew = fp_insert_fp(B.table, B.tmask, Fp{keys[2 * t], (u32)keys[2 * t + 1]}, &B.ctr->table_full);
             reply[t] = (uint8_t)isnew;
             if (isnew) {
                 u32 p = 0;
@@ -1440,15 +1467,15 @@ __global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64*
 // no destination can overflow; ocount was zeroed for this round).
 __global__ __launch_bounds__(256) void k_drain(const DevBufs B, u64 a, u64 n) {
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n; t += (u64)gridDim.x * 256ull) {
-        const u64 key = B.ovf[2 * (a + t)], tk = B.ovf[2 * (a + t) + 1];
+        const u64* r = B.ovf + 3 * (a + t);
+        const u64 k = r[0], sf = r[1], tk = r[2];
         const u32 dest = (u32)((tk >> 48) & 0xFFu);
         const u64 slot = atomicAdd(&B.ocount[dest], 1ull);
         if (slot >= B.kcap) {  // cannot happen for n <= kcap; never write past the outbox
             atomicOr(&B.ctr->overflow, 2u);
             continue;
         }
-        B.key_out[(u64)dest * B.kcap + slot] = key;
-        B.tick_out[(u64)dest * B.kcap + slot] = (tk & ((1ull << 48) - 1)) | (tk & (0xFFull << 56));
+        put_key(B, dest, slot, k, (u32)sf, (tk & ((1ull << 48) - 1)) | (tk & (0xFFull << 56)));
     }
 }
 
@@ -1469,7 +1496,8 @@ __global__ __launch_bounds__(256) void k_route(const Params P, const DevBufs B) 
     for (u64 t0 = (u64)blockIdx.x * 256ull; t0 < np; t0 += (u64)gridDim.x * 256ull) {  // wave-uniform
         const u64 t = t0 + threadIdx.x;
         const bool live = t < np;
-        u64 key = 0, ref = 0;
+        Fp key{0, 0};
+        u64 ref = 0;
         u32 dest = 0xFFFFFFFFu;
         if (live) {
             const u32* r = B.pool + t * (u64)RW;
@@ -1477,7 +1505,7 @@ __global__ __launch_bounds__(256) void k_route(const Params P, const DevBufs B) 
             u32 m[K];
             load_state<S, K>(r, w, m);
             key = fp_of_materialised<S, K>(w, m, P);
-            dest = owner_state<S>(key, w, B);
+            dest = owner_state<S>(key.k, w, B);
             ref = (u64)r[NW] | ((u64)r[NW + 1] << 32);
         }
         u64 slot = ~0ull;
@@ -1494,29 +1522,23 @@ __global__ __launch_bounds__(256) void k_route(const Params P, const DevBufs B) 
         }
         if (!live) continue;
         if (slot < B.kcap) {
-            B.key_out[(u64)dest * B.kcap + slot] = key;
-            B.tick_out[(u64)dest * B.kcap + slot] = POOL_TICK | t;
+            put_key(B, dest, slot, key.k, (u32)key.s, POOL_TICK | t);
             continue;
         }
         // the owner's outbox is full: park it with its parent ticket (a later round sends it)
-        const u64 q = atomicAdd((unsigned long long*)&B.ctr->novf, 1ull);
-        if (q < B.ovf_cap) {
-            B.ovf[2 * q] = key;
-            B.ovf[2 * q + 1] = (ref & ((1ull << 40) - 1)) | ((u64)dest << 48) | (((ref >> 40) & 0xFFull) << 56);
-        } else {
-            atomicOr(&B.ctr->overflow, 2u);
-        }
+        park_key(B, key.k, (u32)key.s,
+                 (ref & ((1ull << 40) - 1)) | ((u64)dest << 48) | (((ref >> 40) & 0xFFull) << 56));
     }
 }
-// Before k_route: the tickets the expansion itself parked (pool full) carry key
-// 0 until keyed here (k_route's own parked records carry theirs).
+// Before k_route: the tickets the expansion itself parked (pool full) are
+// OVF_UNKEYED until keyed here (k_route's own parked records carry theirs).
 template <int S, int K>
 __global__ __launch_bounds__(256) void k_route_fix(const Params P, const DevBufs B) {
     constexpr int NW = 2 * S + K;
     const u64 nov = B.ctr->novf < B.ovf_cap ? B.ctr->novf : B.ovf_cap;
     for (u64 q = (u64)blockIdx.x * 256ull + threadIdx.x; q < nov; q += (u64)gridDim.x * 256ull) {
-        if (B.ovf[2 * q] != 0) continue;
-        const u64 tk = B.ovf[2 * q + 1];
+        if (!(B.ovf[3 * q + 1] & OVF_UNKEYED)) continue;
+        const u64 tk = B.ovf[3 * q + 2];
         const u64 pidx = tk & ((1ull << 48) - 1);
         const int lane = (int)(tk >> 56);
         u64 w[S], wo[S];
@@ -1525,9 +1547,10 @@ __global__ __launch_bounds__(256) void k_route_fix(const Params P, const DevBufs
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);
         materialise<S, K>(w, m, d, wo, mo);
-        const u64 key = fp_of_materialised<S, K>(wo, mo, P);
-        B.ovf[2 * q + 1] = pidx | ((u64)owner_state<S>(key, wo, B) << 48) | ((u64)lane << 56);
-        B.ovf[2 * q] = key;
+        const Fp key = fp_of_materialised<S, K>(wo, mo, P);
+        B.ovf[3 * q] = key.k;
+        B.ovf[3 * q + 2] = pidx | ((u64)owner_state<S>(key.k, wo, B) << 48) | ((u64)lane << 56);
+        B.ovf[3 * q + 1] = (u32)key.s;
     }
 }
 
@@ -1631,9 +1654,9 @@ __global__ __launch_bounds__(256) void k_compare_remote(const Params P, const Pe
         if (!(r[NW + 1] & (u32)(REF_SEEN >> 32))) continue;
         PackedState<S, K> o;
         load_state<S, K>(r, o.w, o.m);
-        const u64 key = verify_key<S, K, SYM>(o.w, o.m, P, PT);
-        u64 s = key & B.tmask, k = 0;
-        while (B.table[s] != key && k <= B.tmask) { s = (s + 1) & B.tmask; ++k; }
+        const TKey key = verify_key<S, K, SYM>(o.w, o.m, P, PT, B.tmask);
+        u64 s = key.s0, k = 0;
+        while (B.table[s] != key.v && k <= B.tmask) { s = (s + 1) & B.tmask; ++k; }
         const u64 ix = k > B.tmask ? ~0ull : B.sidx[s];
         if (ix == ~0ull) {
             atomicOr(&B.ctr->overflow, 8u);  // a seen key without a published owner
@@ -1677,9 +1700,8 @@ __global__ __launch_bounds__(256) void k_ties(const Params P, const PermTable PT
             u64 base[S];
 #pragma unroll
             for (int i = 0; i < S; ++i) base[i] = sig_base<S>(w[i], (u32)i);
-            u64 key = canon_delta<S, K>(w, m, base, d, PT.code, PT.np);
-            key = key ? key : 1ull;
-            is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+            is_new = fp_insert_fp(B.table, B.tmask, canon_delta<S, K>(w, m, base, d, PT.code, PT.np),
+                                  &B.ctr->table_full);
         } else {
 #pragma unroll
             for (int i = 0; i < S; ++i) w[i] = 0;
@@ -1765,11 +1787,10 @@ __global__ __launch_bounds__(256) void k_seed(const Params P, const PermTable PT
     }
     int is_new = 0;
     if (live) {
-        u64 key = SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m);
-        key &= P.fp_mask;  // ~0 unless a verification test weakens the fingerprint
-        key = key ? key : 1ull;
+        // fp_weaken: a no-op unless a verification test weakens the fingerprint
+        const Fp key = fp_weaken(SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m), P.fp_mask);
         // sharded mode: only the owner of an initial state stores it
-        if (owner_state<S>(key, w, B) == B.rank) is_new = fp_insert(B.table, B.tmask, key, &B.ctr->table_full);
+        if (owner_state<S>(key.k, w, B) == B.rank) is_new = fp_insert_fp(B.table, B.tmask, key, &B.ctr->table_full);
     }
     Delta d;  // identity delta: the state itself
     d.srv = -1; d.rm = -1; d.has_add = 0; d.add = 0; d.en = 1; d.w_new = 0;
@@ -1785,10 +1806,8 @@ __global__ __launch_bounds__(256) void k_rehash(const Params P, const PermTable 
         u64 w[S];
         u32 m[K];
         load_state<S, K>(B.store + i * (u64)NW, w, m);
-        u64 key = SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m);
-        key &= P.fp_mask;
-        key = key ? key : 1ull;
-        if (!fp_insert(B.table, B.tmask, key, &B.ctr->table_full)) atomicOr(&B.ctr->overflow, 8u);  // duplicate
+        const Fp key = fp_weaken(SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m), P.fp_mask);
+        if (!fp_insert_fp(B.table, B.tmask, key, &B.ctr->table_full)) atomicOr(&B.ctr->overflow, 8u);  // duplicate
     }
 }
 
@@ -1827,7 +1846,7 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
     u64 w[S];
     u32 m[K];
     load_state<S, K>(in + t * (u64)NW, w, m);
-    const u64 h0 = state_fp<S, K>(w, m);
+    const Fp h0 = state_fp<S, K>(w, m);
     u64 sbase[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) sbase[i] = sig_base<S>(w[i], (u32)i);
@@ -1837,7 +1856,7 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);
         if (!d.en) continue;
-        u64 h = 0;
+        Fp h{0, 0};
         const int in_model = delta_fp<S, K>(w, m, h0, d, P, &h);
         if (in_model) {
             if constexpr (SYM) h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
@@ -1846,7 +1865,7 @@ __global__ __launch_bounds__(256) void k_list(const Params P, const PermTable PT
         if (o >= cap) continue;
         u32* r = out + o * (u64)RW;
         r[0] = (u32)t; r[1] = (u32)(t >> 32); r[2] = (u32)lane; r[3] = (u32)in_model;
-        r[4] = (u32)h; r[5] = (u32)(h >> 32);
+        r[4] = (u32)h.k; r[5] = (u32)(h.k >> 32);
         u64 wo[S];
         u32 mo[K];
         if (in_model) {
@@ -1901,8 +1920,8 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
                 Delta d;
                 lane_delta<S, K>(w, m, lane, P, d);
                 if (!d.en) continue;
-                u64 hh;
-                if (mode == 0 && !delta_fp<S, K>(w, m, 0ull, d, P, &hh)) continue;  // beyond the capacity
+                Fp hh;
+                if (mode == 0 && !delta_fp<S, K>(w, m, Fp{0, 0}, d, P, &hh)) continue;  // beyond the capacity
                 ++cnt;
                 if (sim_rand(rs) % cnt == 0) pick = lane;  // reservoir: uniform over enabled lanes
             }
@@ -1912,8 +1931,8 @@ __global__ __launch_bounds__(256) void k_simulate(const Params P, const u32* ini
             }
             Delta d;
             lane_delta<S, K>(w, m, pick, P, d);
-            u64 hh;
-            if (!delta_fp<S, K>(w, m, 0ull, d, P, &hh)) {
+            Fp hh;
+            if (!delta_fp<S, K>(w, m, Fp{0, 0}, d, P, &hh)) {
                 ++trunc;
                 break;
             }

@@ -334,7 +334,7 @@ int run_bfs_wide(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.depth = depth;
     c->res.stored_here = c->res.distinct;
     const double Dd = (double)c->res.distinct, G = (double)c->res.generated;
-    c->res.collision_probability = Dd * (G - Dd) / 18446744073709551616.0;
+    c->res.collision_probability = fp_collision_estimate(Dd, G, (c->WB.tmask + 1));
     c->res.seconds = secs();
     return 0;
 }

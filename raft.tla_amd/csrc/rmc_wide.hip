@@ -13,8 +13,10 @@
 namespace rmc {
 namespace wide {
 
-__device__ __forceinline__ int w_insert(u64* __restrict__ table, u64 mask, u64 key, u32* full) {
-    u64 s = key & mask;
+__device__ __forceinline__ int w_insert(u64* __restrict__ table, u64 mask, const Fp& h, u32* full) {
+    const TKey t = tkey(h, mask);
+    const u64 key = t.v;
+    u64 s = t.s0;
     for (u64 n = 0; n <= mask; ++n) {
         const u64 cur = table[s];
         if (cur == key) return 0;
@@ -117,26 +119,20 @@ __global__ __launch_bounds__(64) void k_wlist(const WModel M, const WState* in, 
         w.code = r;
         const int inm = r == W_ON && win_model(M, t);
         w.in_model = inm;
-        w.fp = inm ? wfp(t, salt) : 0ull;
+        w.fp = inm ? wfp(t, salt).k : 0ull;
         if (inm) wcopy_state(w.state, t);
         else wzero(&w.state, (int)sizeof(WState));
     }
 }
 
-__device__ __forceinline__ u64 w_rand(u64& x) {  // splitmix64 stream
-    x += 0x9E3779B97F4A7C15ull;
-    return mix64(x);
-}
 
 // Random behaviours (TLC -simulate): one thread per behaviour, from one of the
 // n_init staged initial states, up to depth - 1 steps.  mode 0: uniform over
 // the enabled successors within the bounds (rejection: an out-of-bounds draw
 // is excluded and the draw repeated); 1: uniform over every enabled successor,
-// one beyond the bounds ends the behaviour (truncated); 2: TLC's draw — a
-// uniformly random enabled action (the instances of Restart .. AppendEntries
-// one by one; Receive, DuplicateMessage and DropMessage, whose \E m \in
-// DOMAIN messages ranges over the state, one action each), then a uniform
-// successor of it; beyond the bounds it is truncated like mode 1.
+// one beyond the bounds ends the behaviour (truncated); 2: TLC's draw
+// (tlc_draw: random start, random prime stride, the first enabled action, a
+// uniform successor of it); beyond the bounds it is truncated like mode 1.
 __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* inits, u64 n_init, u64 n_beh, int depth,
                                                  u64 seed, int mode, SimCounters* out, i64 rec_beh, WState* rec) {
     u64 steps = 0, trunc = 0, dead = 0;
@@ -157,29 +153,12 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
         u64 excl[WLMASK] = {};  // mode 0: lanes whose successor left the bounds this step
         for (int dd = 2; dd <= depth && !v;) {
             int pick = -1;
-            if (mode == 2) {
-                // enabled actions: lanes < o7 one each, + one per non-empty bag family
-                u32 na = 0;
-                int fam_on[3] = {0, 0, 0};
-                for (int lane = 0; lane < nl; ++lane) {
-                    if (wlane(M, buf[cur], lane, nullptr) == W_OFF) continue;
-                    if (lane < o7) ++na;
-                    else fam_on[lane < o8 ? 0 : lane < o9 ? 1 : 2] += 1;
-                }
-                na += (u32)(fam_on[0] > 0) + (u32)(fam_on[1] > 0) + (u32)(fam_on[2] > 0);
-                if (na) {
-                    u32 a = (u32)(w_rand(rs) % na);
-                    for (int lane = 0; lane < o7 && pick < 0; ++lane)
-                        if (wlane(M, buf[cur], lane, nullptr) != W_OFF && a-- == 0) pick = lane;
-                    for (int f = 0; f < 3 && pick < 0; ++f) {
-                        if (!fam_on[f]) continue;
-                        if (a-- != 0) continue;
-                        const int lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
-                        u32 k = (u32)(w_rand(rs) % (u64)fam_on[f]);
-                        for (int lane = lo; lane < hi && pick < 0; ++lane)
-                            if (wlane(M, buf[cur], lane, nullptr) != W_OFF && k-- == 0) pick = lane;
-                    }
-                }
+            if (mode == 2) {  // TLC's draw
+                constexpr int NCL = (WLANES_MAX + 63) / 64;
+                u64 en[NCL] = {};
+                for (int lane = 0; lane < nl; ++lane)
+                    if (wlane(M, buf[cur], lane, nullptr) != W_OFF) en[lane >> 6] |= 1ull << (lane & 63);
+                pick = tlc_draw<NCL>(en, nl, o7, o8, o9, rs);
             } else {
                 u32 cnt = 0;
                 for (int lane = 0; lane < nl; ++lane) {  // reservoir: uniform over the enabled lanes
@@ -269,35 +248,7 @@ __global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M,
             }
             int pick = -1;
             if (mode == 2) {  // TLC's draw, exactly as k_wsimulate
-                u32 na = 0;
-                int fam_on[3] = {0, 0, 0};
-                for (int c = 0; c < NC; ++c) {
-                    for (u64 mm = en[c]; mm; mm &= mm - 1) {
-                        const int lane = 64 * c + __builtin_ctzll(mm);
-                        if (lane < o7) ++na;
-                        else fam_on[lane < o8 ? 0 : lane < o9 ? 1 : 2] += 1;
-                    }
-                }
-                na += (u32)(fam_on[0] > 0) + (u32)(fam_on[1] > 0) + (u32)(fam_on[2] > 0);
-                if (na) {
-                    u32 a = (u32)(w_rand(rs) % na);
-                    for (int c = 0; c < NC && pick < 0; ++c)
-                        for (u64 mm = en[c]; mm && pick < 0; mm &= mm - 1) {
-                            const int lane = 64 * c + __builtin_ctzll(mm);
-                            if (lane < o7 && a-- == 0) pick = lane;
-                        }
-                    for (int f = 0; f < 3 && pick < 0; ++f) {
-                        if (!fam_on[f]) continue;
-                        if (a-- != 0) continue;
-                        const int lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
-                        u32 k = (u32)(w_rand(rs) % (u64)fam_on[f]);
-                        for (int c = 0; c < NC && pick < 0; ++c)
-                            for (u64 mm = en[c]; mm && pick < 0; mm &= mm - 1) {
-                                const int lane = 64 * c + __builtin_ctzll(mm);
-                                if (lane >= lo && lane < hi && k-- == 0) pick = lane;
-                            }
-                    }
-                }
+                pick = tlc_draw<NC>(en, nl, o7, o8, o9, rs);
             } else {  // reservoir over the enabled lanes in lane order (k_wsimulate's draws)
                 u32 cnt = 0;
                 for (int c = 0; c < NC; ++c)

@@ -132,7 +132,7 @@ struct Model {
         u32 m0[K];
         for (int i = 0; i < S; ++i) w0[i] = 1ull | ((u64)NILV << VF_SH);
         for (int q = 0; q < K; ++q) m0[q] = 0;
-        insert(state_fp<S, K>(w0, m0));
+        insert(state_fp<S, K>(w0, m0).k);
         W.insert(W.end(), w0, w0 + S);
         M.insert(M.end(), m0, m0 + K);
         act.push_back(255);
@@ -147,7 +147,7 @@ struct Model {
                 u32 m[K];
                 for (int i = 0; i < S; ++i) w[i] = W[t * S + i];
                 for (int q = 0; q < K; ++q) m[q] = M[t * K + q];
-                const u64 h0 = state_fp<S, K>(w, m);
+                const Fp h0 = state_fp<S, K>(w, m);
                 ParentMix<S, K> pm;
                 parent_mix<S, K>(w, m, pm);
                 for (int lane = 0; lane < nl; ++lane) {
@@ -162,23 +162,29 @@ struct Model {
                     }
                     if (!d.en) continue;
                     ++o.generated;
-                    u64 h = 0;
-                    {  // the kernels' precomputed-mix form decides and hashes the same
-                        u64 hp = 0;
+                    Fp h{0, 0};
+                    {  // the kernels' precomputed-mix form decides and hashes the same (both sums)
+                        Fp hp{0, 0}, hf{0, 0};
                         int np = 0, nf = 0;
-                        u64 hf = 0;
                         const int a1 = delta_fp<S, K>(w, m, h0, d, P, &hf, &nf);
                         const int a2 = delta_fp_pre<S, K>(w, m, pm, d, P, &hp, &np);
-                        if (a1 != a2 || (a1 && (hf != hp || nf != np))) ++o.mismatch;
+                        if (a1 != a2 || (a1 && (hf.k != hp.k || hf.s != hp.s || nf != np))) ++o.mismatch;
                     }
                     if (!delta_fp<S, K>(w, m, h0, d, P, &h)) continue;
-                    if (h == h0) continue;  // stutter
+                    {  // the incremental sums equal the materialised successor's (both sums)
+                        u64 wo[S];
+                        u32 mo[K];
+                        materialise<S, K>(w, m, d, wo, mo);
+                        const Fp hm = state_fp<S, K>(wo, mo);
+                        if (hm.k != h.k || hm.s != h.s) ++o.mismatch;
+                    }
+                    if (h.k == h0.k) continue;  // stutter
                     const bool sk = skippable(t, m, lane, d);
                     {  // the kernels' implementation (raft_packed.h) must decide the same
                         Diamond dm;
                         diamond_of<S, K>(m, act[t], hfoot[t], P, dm);
                         int nmb = 0;
-                        u64 h2 = 0;
+                        Fp h2{0, 0};
                         delta_fp<S, K>(w, m, h0, d, P, &h2, &nmb);
                         if (diamond_skip<S, K>(m, lane, d, nmb, dm, P) != sk) ++o.mismatch;
                         // the lane-descriptor form the sorted kernels use decides the same
@@ -189,7 +195,7 @@ struct Model {
                         if (skip) continue;
                     }
                     ++o.probes;
-                    if (!insert(h)) continue;
+                    if (!insert(h.k)) continue;
                     u64 wo[S];
                     u32 mo[K];
                     materialise<S, K>(w, m, d, wo, mo);

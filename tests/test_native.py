@@ -44,3 +44,20 @@ def test_diamond_skipping_keeps_every_level_count(tmp_path):
         assert rec["same_levels"] and rec["kernel_rule_mismatches"] == 0, rec
         assert (rec["with_skip"]["distinct"], rec["with_skip"]["generated"]) == (g["distinct"], g["generated"]), case
         assert rec["skippable_frac"] > 0.15, rec  # worth a kernel change
+
+
+def test_tlc_draw_follows_the_random_start_prime_stride_rule(tmp_path):
+    """RMC_SIM_TLC (raft_wide.h tlc_draw, both wide simulators): for random sets
+    of enabled lanes, every lane is drawn with the exact probability of TLC's
+    simulator rule — random start among Next's actions, random prime stride,
+    the first action with a successor, a uniform successor of it — within 6
+    standard deviations over 200,000 draws per set; the rule is measurably not
+    "uniform over the enabled actions" (VERDICT r04 missing item 4)."""
+    exe = tmp_path / "tlc_draw_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-I",
+                    os.path.join(ROOT, "raft.tla_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "native", "tlc_draw_check.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "30", "200000", "5"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok "), r.stdout
+    assert float(r.stdout.split("max |P(action) - 1/(enabled actions)| ")[1]) > 0.01
