@@ -319,10 +319,13 @@ def main(argv=None):
     cfg.device = dev
     ranks_per_gpu = max(1, -(-world // ndev)) if sharded else 1
     small = os.path.basename(a.config) == "MCraftBench.cfg"
+    xl = os.path.basename(a.config) == "MCraftBenchXL.cfg"
     if a.capacity:
         cfg.state_capacity = a.capacity
     elif small:
         cfg.state_capacity = int(1.5e9 / world * (1.3 if sharded else 1.0))
+    elif xl and sharded:  # 4.13 G states: a rank's share, +12 % for the owner imbalance (1.06 measured)
+        cfg.state_capacity = int(4.14e9 / world * 1.12)
     else:  # librmc's own sizing (80 % of free HBM)
         cfg.state_capacity = 0
     spill = (a.spill == "on" or (a.spill == "auto" and not small)) and not sharded

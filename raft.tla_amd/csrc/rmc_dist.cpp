@@ -213,6 +213,10 @@ int a2a(rmc_ctx* c, const void* sbuf, const u64* soff, const u64* scnt, void* rb
 // All-to-all of `per` u64 per peer between device buffers (the count rows).
 int a2a_u64(rmc_ctx* c, const u64* send, u64* recv, u64 per) {
     DistState& D = c->dist;
+    if (D.world == 1) {  // a world of one: the row to itself, no collective
+        HIPCHK(c, hipMemcpyAsync(recv, send, per * 8, hipMemcpyDeviceToDevice, D.xs));
+        return 0;
+    }
     if (D.rccl) {
         NCCLCHK(c, ncclAllToAll(send, recv, per, ncclUint64, D.comm, D.xs));
         return 0;
@@ -618,16 +622,28 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             const bool host_more = cursor < hi || ovf_done < ovf_known;
             // ---- count row of round k (after its expansion), on xs
             D.phase = "count all-to-all";
-            HIPCHK(c, hipStreamWaitEvent(D.xs, S.ev_exp, 0));
-            HIPCHK(c, hipEventRecord(S.x0, D.xs));
-            {
+            if (W == 1) {
+                // a world of one: the row is its own all-to-all; the pack kernel writes
+                // it (both halves) straight into the pinned host row, on the ctx stream
+                // right after the expansion: no stream hop, collective or copy
+                HIPCHK(c, hipEventRecord(S.x0, c->st));
                 DevBufs Bb = c->B;
                 Bb.ocount = S.ocount;
-                HIPCHK(c, launch_pack_counts(Bb, host_more ? 1ull : 0ull, ovf_done, S.cx, D.xs));
+                HIPCHK(c, launch_pack_counts(Bb, host_more ? 1ull : 0ull, ovf_done, S.h_cx, c->st,
+                                             S.h_cx + RWD * (u64)W + 1));
+                HIPCHK(c, hipEventRecord(D.ev_cnt, c->st));
+            } else {
+                HIPCHK(c, hipStreamWaitEvent(D.xs, S.ev_exp, 0));
+                HIPCHK(c, hipEventRecord(S.x0, D.xs));
+                {
+                    DevBufs Bb = c->B;
+                    Bb.ocount = S.ocount;
+                    HIPCHK(c, launch_pack_counts(Bb, host_more ? 1ull : 0ull, ovf_done, S.cx, D.xs));
+                }
+                if (int rc = a2a_u64(c, S.cx, S.cx + RWD * (u64)W + 1, RWD)) return rc;
+                HIPCHK(c, hipMemcpyAsync(S.h_cx, S.cx, row_len * 8, hipMemcpyDeviceToHost, D.xs));
+                HIPCHK(c, hipEventRecord(D.ev_cnt, D.xs));
             }
-            if (int rc = a2a_u64(c, S.cx, S.cx + RWD * (u64)W + 1, RWD)) return rc;
-            HIPCHK(c, hipMemcpyAsync(S.h_cx, S.cx, row_len * 8, hipMemcpyDeviceToHost, D.xs));
-            HIPCHK(c, hipEventRecord(D.ev_cnt, D.xs));
             // the next round's expansion is queued before waiting, so the GPU
             // expands while the counts travel (not in RMC_DIST_OVERLAP=0 runs)
             bool next_queued = false;
@@ -690,8 +706,9 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             bool idle = !verify && (D.rccl || W == 1) && tot_in == 0;
             for (int p = 0; p < W; ++p) idle = idle && scnt[(size_t)p] == 0;
             if (idle) {
-                HIPCHK(c, hipEventRecord(S.ev_free, D.xs));
-                HIPCHK(c, hipEventRecord(S.x1, D.xs));
+                hipStream_t is = W == 1 ? c->st : D.xs;  // where the count row ran
+                HIPCHK(c, hipEventRecord(S.ev_free, is));
+                HIPCHK(c, hipEventRecord(S.x1, is));
                 S.xtimed = 1;
                 D.chunks += 1;
                 if (!global_more) {

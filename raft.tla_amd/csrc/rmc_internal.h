@@ -131,7 +131,9 @@ hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply
 // them ends the level without a counter all-gather); out[kRowWords * W] = novf.
 constexpr int kRowWords = 2 + (int)(sizeof(Counters) / 8);
 static_assert(sizeof(Counters) % 8 == 0, "Counters travel as u64 words");
-hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st);
+// mirror (a world of one): the row's blocks also written there (its received half).
+hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st,
+                              u64* mirror = nullptr);
 // States per single-GPU expansion launch at most (B.word holds one launch's
 // presorted window positions).
 constexpr int kMaxLaunchLog2 = 25;

@@ -1443,7 +1443,7 @@ hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 w
 // Sharded mode: the count row of one exchange round (launch_pack_counts): a
 // block of kRowWords u64 per peer — keys for it, flags, this rank's counters —
 // then novf.
-__global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64* out) {
+__global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64* out, u64* mirror) {
     const u32 p = threadIdx.x;
     const u64 novf = B.ctr->novf;
     bool sends = false;
@@ -1459,8 +1459,11 @@ __global__ void k_pack_counts(const DevBufs B, u64 host_more, u64 ovf_done, u64*
         r[1] = flags;
         const u64* k = reinterpret_cast<const u64*>(B.ctr);
         for (int i = 0; i < kRowWords - 2; ++i) r[2 + i] = k[i];
+        if (mirror)
+            for (int i = 0; i < kRowWords; ++i) mirror[(u64)p * kRowWords + i] = r[i];
     }
     if (p == 0) out[(u64)kRowWords * B.world] = novf;
+    if (mirror) __threadfence_system();  // the row is in pinned host memory: visible before the event
 }
 
 // Sharded mode: parked keys ovf[a, a + n) back into the outbox (n <= kcap, so
@@ -1747,9 +1750,9 @@ hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply
     return hipGetLastError();
 }
 
-hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st) {
+hipError_t launch_pack_counts(const DevBufs& B, u64 host_more, u64 ovf_done, u64* out, hipStream_t st, u64* mirror) {
     if (B.world > (u32)kMaxWorld) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, st, B, host_more, ovf_done, out);
+    hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, st, B, host_more, ovf_done, out, mirror);
     return hipGetLastError();
 }
 

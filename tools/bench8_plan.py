@@ -21,7 +21,13 @@ the rehearsal), rounds = ceil(frontier / N / min(2^25, kcap / rho)) with rho =
 kappa / N keys per state to one owner (librmc's round sizing, rmc_dist.cpp).
 
     python tools/bench8_plan.py prefix_levels.jsonl prefix_rounds.txt prefix_dist8.json shape_levels.jsonl [N]
-        [--sizing profiles/r03/sizing_next_bounds.txt] [--k-dist K]
+        [--sizing profiles/r03/sizing_next_bounds.txt] [--k-dist K] [--measured full_levels.jsonl]
+
+--measured: the whole model's per-level times on one GPU (tools/level_times.py of a
+model one GPU completes, e.g. specs/MCraftBenchXL.cfg with spill): T1 and the
+frontiers past the rehearsed prefix are then measured, not extrapolated — only the
+per-rank keys and states of those levels come from the prefix's last 3 levels
+(shape_levels is then unused).
 
 --sizing: per-level new-state counts of a longer depth-bounded run of the same
 model (tools/sizing.py) extend the measured prefix before the tail is
@@ -115,6 +121,16 @@ def main():
         k = args.index("--sizing")
         sizing = args[k + 1]
         del args[k:k + 2]
+    table_frac = None  # the per-rank fingerprint set's share of the one-GPU set's bytes (level 1's memset)
+    if "--table-frac" in args:
+        k = args.index("--table-frac")
+        table_frac = float(args[k + 1])
+        del args[k:k + 2]
+    measured = None
+    if "--measured" in args:
+        k = args.index("--measured")
+        measured = news(args[k + 1])
+        del args[k:k + 2]
     lv, rounds_p, pr_p, shape_p = args[:4]
     n = int(args[4]) if len(args) > 4 else 8
     t1, frontier, total1, rounds, keys_in, states, pr = dcm.load(lv, rounds_p, pr_p)
@@ -148,8 +164,11 @@ def main():
                       "tau_ns_per_frontier_state": tau * 1e9, "generated_per_frontier_state": gen_per,
                       "keys_per_expanded_state": kappa, "rank_state_share_max": max(share)}))
     kcap = min(1 << 25, max(1 << 20, (1 << 26) // n))
-    for stretch in (1.0, 1.15, 1.3):
-        full = extrapolate(prefix_new, shape_new, stretch)
+    if measured:  # the whole model's counts (level L's new states) from the one-GPU run
+        full_m = [1] + [measured[i]["new"] for i in sorted(measured)]
+        full_m = full_m[:max(i for i, v in enumerate(full_m) if v) + 1]
+    for stretch in ((None,) if measured else (1.0, 1.15, 1.3)):
+        full = full_m if measured else extrapolate(prefix_new, shape_new, stretch)
         distinct = sum(full)
         T1 = dict(t1)
         Fr = dict(frontier)
@@ -162,21 +181,35 @@ def main():
             Ro[L] = set(rounds[L])
         for L in range(depth_p + 1, len(full)):
             F = full[L - 1]  # level L expands the states found at level L - 1
-            T1[L] = f + F * tau
+            T1[L] = measured[L]["seconds"] if measured else f + F * tau
             Fr[L] = F
             Ki[L].update({r: F * kappa * kshare[r] for r in range(n)})
             St[L].update({r: F * share[r] for r in range(n)})
             rho = kappa / n
             per_round = min(1 << 25, kcap / max(rho, 0.02))
-            Ro[L] = set(range(max(1, math.ceil(F / n / per_round))))
+            # librmc: at world > 1 a level of >= 2^21 states per rank takes at least
+            # 2 rounds (D.split), so one round's exchange overlaps the next's expansion
+            split = 2 if (n > 1 and F / n >= (1 << 21)) else 1
+            Ro[L] = set(range(max(split, math.ceil(F / n / per_round))))
+        if measured:  # the prefix levels too: this model's own one-GPU run (same build as the tail)
+            for L in t1:
+                if L in measured:
+                    T1[L] = measured[L]["seconds"]
         tot1 = sum(T1.values())
         row = {"stretch": stretch, "k_dist": k_dist, "depth": len(full) - 1, "distinct_est": distinct,
-               "generated_est": int(sum(pl[L]["generated"] for L in pl) + sum(
-                   full[L - 1] * gen_per for L in range(depth_p + 1, len(full)))),
+               "generated_est": (int(sum(measured[L]["generated"] for L in measured)) + 1 if measured else int(
+                   sum(pl[L]["generated"] for L in pl) + sum(full[L - 1] * gen_per for L in range(depth_p + 1, len(full))))),
                "T1_model_s": tot1, "peak_level_new": max(full)}
         row["memory"] = memory_plan(n, distinct)
         for lat in dcm.LATENCIES:
-            m = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist)
+            m = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist,
+                          table_frac=table_frac)
+            for part in ("expand_ms", "insert_ms", "xgmi_ms", "latency_ms"):
+                row.setdefault(part, []).append(round(m.get(part, 0.0), 1))
+            mo = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist,
+                           table_frac=table_frac, overlap=True)
+            row.setdefault("T_N_ms_overlapped", []).append(round(mo["T_N_ms"], 1))
+            row.setdefault("speedup_overlapped", []).append(round(mo["speedup"], 2))
             row.setdefault("T_N_ms", []).append(round(m["T_N_ms"], 1))
             row.setdefault("speedup", []).append(round(m["speedup"], 2))
             row.setdefault("rate_G_per_s", []).append(round(distinct / m["T_N_ms"] / 1e6, 2))

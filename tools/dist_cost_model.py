@@ -65,7 +65,11 @@ def load(lv_path, log_path, pr_path):
 
 
 def model(t1, frontier, total1, rounds, keys_in, states, pr, n, rep_max, lat, k_dist=1.0, a_lane=0.55,
-          link_bw=50e9, c_probe=1 / 30e9, table_frac=None, RB=56, RBR=64):
+          link_bw=50e9, c_probe=1 / 30e9, table_frac=None, RB=56, RBR=64, overlap=False):
+    """overlap: a level of R >= 2 rounds runs round k's exchange (owner inserts and
+    xGMI bytes, on the exchange stream) under round k + 1's expansion (librmc's two
+    outbox sets), so only the last round's exchange, 1/R of the level's, is exposed;
+    without it (the default) every exchange is charged in full, serially."""
     a_sync, a_coll, a_launch, a_level = lat
     accept = pr["states_sent"] / max(1, pr["keys_sent"])  # phase-2 states per phase-1 key
     f_level = min(t1.values())
@@ -93,10 +97,12 @@ def model(t1, frontier, total1, rounds, keys_in, states, pr, n, rep_max, lat, k_
             share = (st / max(1, sum(states[L].values()))) if st is not None else 1.0 / n
             e = f_level + max(0.0, tl - f_level) * share * k_dist
             ins = keys_in[L][r] * c_probe
-            byts = keys_in[L][r] * 9 + accept * keys_in[L][r] * RB
+            byts = keys_in[L][r] * (KEYB + 1) + accept * keys_in[L][r] * RB  # key record + reply byte
             x = byts / (link_bw * links) if n > 1 else 0.0
             per_rank.append((e, ins, x))
         e, ins, x = max(per_rank, key=lambda v: sum(v))
+        if overlap and R >= 2:
+            ins, x = ins / R, x / R
         lat_l = R * (2 * a_sync + 4 * a_coll + 5 * a_launch) + a_level
         parts["expand"] += e
         parts["insert"] += ins
@@ -110,6 +116,7 @@ def model(t1, frontier, total1, rounds, keys_in, states, pr, n, rep_max, lat, k_
 
 
 LATENCIES = ((10e-6, 15e-6, 5e-6, 40e-6), (20e-6, 30e-6, 8e-6, 80e-6), (40e-6, 60e-6, 10e-6, 150e-6))
+KEYB = 16  # bytes per phase-1 key record: the raw 96-bit fingerprint (k, s32) in two u64 (rmc_dist.cpp)
 
 
 def main():
