@@ -431,7 +431,9 @@ def main(argv=None):
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
             "spill": ({"flag": "RMC_FLAG_SPILL", "trace_links": "device" if last[0].spill_links_on_device else "host",
-                       "spills_per_step": last[0].spills, "states_moved_per_step": last[0].spilled,
+                       "window": ("ring (slot reuse, nothing copied)" if last[0].spill_links_on_device
+                                  else "shifted (links to host memory)"),
+                       "spills_per_step": last[0].spills, "states_out_of_window_per_step": last[0].spilled,
                        "spill_seconds_per_step": last[0].spill_seconds} if spill else None),
             "parallelism": (f"state-space sharded x{world} (librmc two-phase exchange, "
                             f"{'RCCL over xGMI' if transport == 'rccl' else 'host transport over gloo'})")

@@ -157,16 +157,18 @@ typedef struct rmc_result {
                                /* overlapped with the next round's expansion or not        */
     uint64_t stored_here;      /* distinct states this rank stores                         */
     /* RMC_FLAG_SPILL */
-    uint64_t spilled;          /* states moved out of the device window (all spills of the run) */
-    uint64_t spills;           /* spill events                                              */
-    double spill_seconds;      /* wall time of the spills (device-to-host + window shift)   */
+    uint64_t spilled;          /* states that left the device window (all spills of the run) */
+    uint64_t spills;           /* spill events; with the links in HBM (a ring window whose  */
+                               /* slots are reused, nothing copied) the passes of the ring  */
+    double spill_seconds;      /* wall time of the spills (device-to-host + window shift;   */
+                               /* 0 for the ring)                                           */
     /* sharded mode, continued */
     uint64_t parked;           /* keys parked because an owner's outbox was full; sent in   */
                                /* further rounds of the same level (never dropped)          */
     double exchange_wait_seconds; /* host wall time blocked on count read-backs and level ends */
     /* RMC_FLAG_SPILL, continued */
     int32_t spill_links_on_device; /* 1: the trace links (parent, lane) of spilled states stayed */
-                                   /* in HBM and a spill only shifted the window; 0: host      */
+                                   /* in HBM and the window was a ring; 0: links on the host   */
     int32_t pad2;
 } rmc_result;
 

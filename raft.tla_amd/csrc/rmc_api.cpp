@@ -318,6 +318,15 @@ int read_counters(rmc_ctx* c) {
 void spill_rebase(rmc_ctx* c, u64 base) {
     SpillState& X = c->spill;
     X.base = base;
+    if (X.dev_links) {  // the ring window (DevBufs.wmask): nothing moves, base = the oldest resident state
+        c->B.store = X.store;
+        c->B.parent = X.parent;
+        c->B.act = X.act;
+        c->B.foot = X.foot;
+        c->B.cls = X.cls;
+        c->B.cap = X.total_cap;
+        return;
+    }
     const uintptr_t nw = (uintptr_t)c->NW;
     c->B.store = (u32*)((uintptr_t)X.store - (uintptr_t)base * nw * 4);
     const u64 lb = X.dev_links ? 0 : base;  // device links: indexed by global index, never rebased
@@ -369,29 +378,14 @@ static void prefault(void* p, size_t n) {
 }
 
 // Move the trace links of the device-resident states [base, a) to the host
-// and shift [a, count) to the start of the window.
+// and shift [a, count) to the start of the window.  (With the links in HBM the
+// window is a ring and nothing ever moves: see the launch loop.)
 int spill_to(rmc_ctx* c, u64 a, u64 count) {
     SpillState& X = c->spill;
     const u64 n = a - X.base;
     if (!n) return 0;
     const auto t0 = std::chrono::steady_clock::now();
     const u64 W = (u64)c->NW * 4;
-    if (X.dev_links) {  // the links stay in HBM: only the window's states move down
-        const u64 m = count - a;
-        for (u64 off = 0; off < m; off += n) {
-            const u64 k = std::min(n, m - off);
-            HIPCHK(c, hipMemcpyAsync((char*)X.store + off * W, (char*)X.store + (n + off) * W, k * W,
-                                     hipMemcpyDeviceToDevice, c->st));
-            HIPCHK(c, hipMemcpyAsync(X.foot + off, X.foot + n + off, k * 8, hipMemcpyDeviceToDevice, c->st));
-            HIPCHK(c, hipMemcpyAsync(X.cls + off, X.cls + n + off, k, hipMemcpyDeviceToDevice, c->st));
-        }
-        HIPCHK(c, hipStreamSynchronize(c->st));
-        spill_rebase(c, a);
-        c->res.spilled += n;
-        c->res.spills += 1;
-        c->res.spill_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        return 0;
-    }
     u64* hp = X.h_parent + X.base;
     uint8_t* ha = X.h_act + X.base;
     if (X.ahead.joinable()) X.ahead.join();
@@ -544,10 +538,18 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
         win = cfg->device_window;
         if (win == 0) win = dev_links ? (rest - cap * 9) / wbytes : rest / per_state;
         win = std::max<u64>(std::min<u64>(win, cap), 1024);
+        if (dev_links) {
+            // the window is a ring of a power of two states (DevBufs.wmask): a
+            // given window rounds up, librmc's own sizing down
+            u64 p2 = 1024;
+            while (p2 < win) p2 <<= 1;
+            win = (cfg->device_window || p2 == win) ? p2 : p2 >> 1;
+        }
         link_cap = dev_links ? cap : win;
     }
     c->B.cap = win;
     c->B.tmask = slots - 1;
+    c->B.wmask = dev_links ? win - 1 : ~0ull;
     if (hipMalloc(&c->B.store, win * (u64)c->NW * 4) != hipSuccess ||
         hipMalloc(&c->B.parent, link_cap * 8) != hipSuccess || hipMalloc(&c->B.act, link_cap) != hipSuccess ||
         hipMalloc(&c->B.foot, win * 8) != hipSuccess || hipMalloc(&c->B.cls, win) != hipSuccess ||
@@ -721,7 +723,21 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         const u64 even = (hi - lo + nlaunch - 1) / nlaunch;  // <= chunk
         for (u64 a = lo, b = 0; a < hi; a = b) {
             b = std::min(hi, a + even);
-            if (c->spill.on) {
+            if (c->spill.on && c->spill.dev_links) {
+                // the ring window: [a, count) is live (the rest of the frontier and
+                // the level being built); every lane yields at most one new state, so
+                // a launch of n states cannot overwrite a live state when
+                // count + n * lanes <= a + win — nothing is ever moved
+                const u64 lanes = (u64)c->P.off[10], count = c->h_ctr->count, win = c->spill.win;
+                const u64 room = count - a < win ? a + win - count : 0;
+                const u64 want = std::min(b - a, room / lanes);
+                if (want == 0)
+                    return fail(c, RMC_E_CAPACITY,
+                                "spill: the device window (" + std::to_string(win) +
+                                    " states) cannot hold the frontier and the level being built; raise "
+                                    "rmc_config.device_window");
+                b = a + want;
+            } else if (c->spill.on) {
                 // every lane yields at most one new state: a launch of n states
                 // stays inside the window when n * lanes <= room.  Launches
                 // shrink as the window fills; below 2^20 states the expanded
@@ -731,11 +747,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 const u64 count = c->h_ctr->count, fit = (c->B.cap - count) / lanes;
                 u64 want = b - a;
                 const u64 old = a - c->spill.base;
-                // device links: a spill is a device-to-device shift only, taken as
-                // soon as a whole launch no longer fits (launches keep their size)
-                const bool due = c->spill.dev_links ? (fit < want && old && (old >= count - a || fit == 0))
-                                                    : (fit < std::min<u64>(want, 1ull << 20) && old &&
-                                                       (old * 8 >= count - a || fit == 0));
+                const bool due = fit < std::min<u64>(want, 1ull << 20) && old && (old * 8 >= count - a || fit == 0);
                 if (due)
                     if (int rc = spill_to(c, a, count)) return rc;
                 want = std::min(want, (c->B.cap - count) / lanes);
@@ -769,6 +781,12 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 if (c->h_ctr->count > c->spill.total_cap)
                     return fail(c, RMC_E_CAPACITY, "spill: more states than rmc_config.state_capacity (" +
                                                        std::to_string(c->spill.total_cap) + ")");
+                if (c->spill.dev_links) {  // the ring: states below count - win are overwritten
+                    const u64 cnt = c->h_ctr->count, win = c->spill.win;
+                    c->spill.base = cnt > win ? cnt - win : 0;
+                    c->res.spilled = c->spill.base;
+                    c->res.spills = cnt / win;  // passes of the ring
+                }
             }
         }
         HIPCHK(c, hipEventRecord(c->ev1, c->st));
@@ -948,7 +966,11 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (!rc) rc = move_file(c, f, c->B.parent + lb, nd * 8, true);
     if (lb) put(c->spill.h_act, lb);
     if (!rc) rc = move_file(c, f, c->B.act + lb, nd, true);
-    if (!rc) rc = move_file(c, f, c->B.store + h.first * (u64)c->NW, (h.count - h.first) * (u64)c->NW * 4, true);
+    for (u64 i = h.first; !rc && i < h.count;) {  // the ring window: in up to two pieces
+        const u64 sl = wslot(c->B, i), n = std::min(h.count - i, c->B.wmask == ~0ull ? h.count - i : c->spill.win - sl);
+        rc = move_file(c, f, c->B.store + sl * (u64)c->NW, n * (u64)c->NW * 4, true);
+        i += n;
+    }
     if (!rc && h.slots) rc = move_file(c, f, c->B.table, h.slots * 8, true);
     if (fclose(f) != 0 && !rc) rc = fail(c, RMC_E_IO, "checkpoint close failed");
     return rc;
@@ -1040,11 +1062,21 @@ int rmc_recover(rmc_ctx* c, const char* path) {
             rc = move_file(c, f, area, k * W, false);
             DevBufs T = c->B;
             T.store = (u32*)((uintptr_t)area - (uintptr_t)(p * W));
+            T.wmask = ~0ull;  // indexed through the biased pointer, not the ring
             if (!rc) HIPCHK(c, launch(c->sh, 7, c->P, c->PT, T, p, p + k, nullptr, nullptr, 0, nullptr, c->st));
             if (!rc) HIPCHK(c, hipStreamSynchronize(c->st));
         }
     }
-    if (!rc) rc = move_file(c, f, dstore, (h.count - s) * W, false);
+    if (c->spill.on && c->spill.dev_links) {  // the ring window: state i at slot i & wmask
+        const u64 win = c->spill.win;
+        for (u64 i = s; !rc && i < h.count;) {
+            const u64 sl = i & (win - 1), n = std::min(h.count - i, win - sl);
+            rc = move_file(c, f, dstore + sl * NW, n * W, false);
+            i += n;
+        }
+    } else if (!rc) {
+        rc = move_file(c, f, dstore, (h.count - s) * W, false);
+    }
     if (!rc && h.slots) rc = move_file(c, f, c->B.table, h.slots * 8, false);
     fclose(f);
     if (rc) return rc;
@@ -1093,7 +1125,7 @@ int rmc_trace(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* in
     int rc = 0;
     for (size_t q = 0; q < chain.size() && !rc; ++q) {
         if (!c->spill.on || chain[q] >= c->spill.base) {
-            HIPCHK(c, hipMemcpy(cur.data(), c->B.store + chain[q] * NW, NW * 4, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(cur.data(), c->B.store + wslot(c->B, chain[q]) * NW, NW * 4, hipMemcpyDeviceToHost));
         } else if (q == 0) {  // Init (raft.tla:125-129), the one initial state
             rmc_state_view iv;
             init_view(c->cfg, &iv);

@@ -501,7 +501,8 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     int depth = resume ? c->resume_depth : 1;
     // Replicated levels: the plain kernel (every shape), models with a
     // CONSTRAINT on every field (the capacity pass reads the store)
-    const bool rep_ok = !verify && !c->sh.sym && !c->P.unbounded && D.rep_max > 0;
+    // (a world of one has nothing to gather: its levels run as plain rounds)
+    const bool rep_ok = W > 1 && !verify && !c->sh.sym && !c->P.unbounded && D.rep_max > 0;
     // Round sizing: rho = most keys one round sends one owner, per expanded
     // state, from the previous rounds (it varies along a frontier: states
     // received from other ranks are appended after the local ones).  A round

@@ -37,6 +37,10 @@ struct DevBufs {
     u64* table;      // fingerprint set, power-of-two slots, 0 = empty
     u64 tmask;       // slots - 1
     u64 cap;         // state store capacity
+    // ring window (RMC_FLAG_SPILL with the trace links in HBM): store / foot / cls hold
+    // state i at slot i & wmask, the last wmask + 1 states; ~0 (resident, host-link
+    // spill, sharded): slot = index.  parent / act are indexed by the index itself.
+    u64 wmask;
     Counters* ctr;
     // sharded mode (rank/world > 1 GPU processes; single mode: rank 0, world 1)
     u32 rank, world;
@@ -140,6 +144,8 @@ constexpr int kMaxLaunchLog2 = 25;
 // Presorted windows: k_window_order over the launch [lo, hi) for an expansion
 // grid of `grid` blocks and windows of at most wt_max tiles (B.word).
 hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st);
+// The slot of state index i in the store / foot / cls arrays (DevBufs.wmask).
+__host__ __device__ __forceinline__ u64 wslot(const DevBufs& B, u64 i) { return i & B.wmask; }
 // Sharded mode: move parked keys ovf[a, a + n) into the (emptied) outbox; n <= kcap.
 hipError_t launch_drain(const DevBufs& B, u64 a, u64 n, hipStream_t st);
 // Outbox ticket of a pool record (bit 48: a parent ticket's index is < 2^48 and

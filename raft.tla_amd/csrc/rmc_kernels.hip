@@ -129,11 +129,12 @@ __device__ __forceinline__ void store_state(u32* __restrict__ base, const u64 (&
 template <int S, int K>
 __device__ __forceinline__ void store_new(const Params& P, const DevBufs& B, u64 ni, const u64 (&wo)[S],
                                           const u32 (&mo)[K], u64 parent, int lane, u64 foot) {
-    store_state<S, K>(B.store + ni * (u64)(2 * S + K), wo, mo);
+    const u64 sl = wslot(B, ni);  // the ring window's slot (= ni unless spilling with links in HBM)
+    store_state<S, K>(B.store + sl * (u64)(2 * S + K), wo, mo);
     B.parent[ni] = parent;
     B.act[ni] = (uint8_t)lane;
-    B.foot[ni] = foot;
-    B.cls[ni] = (uint8_t)state_class_fine<S, K>(wo, mo);
+    B.foot[sl] = foot;
+    B.cls[sl] = (uint8_t)state_class_fine<S, K>(wo, mo);
     const int v = check_invariants<S, K>(wo, mo, P);
     if (v) atomicMin((unsigned long long*)&B.ctr->viol, (unsigned long long)((ni << 4) | (u64)(v - 1)));
 }
@@ -209,7 +210,7 @@ __device__ __forceinline__ void flush_new(const Params& P, const DevBufs& B, u64
         }
         u64 w[S];
         u32 m[K];
-        const u32* pr = REP ? B.rep + (lo + rel) * (u64)RR::RR : B.store + (lo + rel) * (u64)NW;
+        const u32* pr = REP ? B.rep + (lo + rel) * (u64)RR::RR : B.store + wslot(B, lo + rel) * (u64)NW;
         load_state<S, K>(pr, w, m);
         Delta d;
         u64 foot;
@@ -879,7 +880,8 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             const u32 p = (u32)k * 256u + threadIdx.x;
             if (p < wn) {
                 // the stored 1-byte class (B.cls / the record's class byte), not the state
-                const u32 c = REP ? (fr[(lo + win + p) * (u64)FW + RR::ACT] >> 8) & 0xFFu : (u32)B.cls[lo + win + p];
+                const u32 c = REP ? (fr[(lo + win + p) * (u64)FW + RR::ACT] >> 8) & 0xFFu
+                                  : (u32)B.cls[wslot(B, lo + win + p)];
                 s_wcls[p] = (uint8_t)c;
                 atomicAdd(&s_wbin[c], 1u);
             }
@@ -921,7 +923,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
         }
         u64 w[S];
         u32 m[K];
-        const u32* rec = fr + (lo + rel) * (u64)FW;
+        const u32* rec = fr + (REP ? lo + rel : wslot(B, lo + rel)) * (u64)FW;
         if (live) {
             load_state<S, K>(rec, w, m);
         } else {
@@ -963,7 +965,7 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                     foot = (u64)rec[RR::FOOT] | ((u64)rec[RR::FOOT + 1] << 32);
                 } else {
                     act = (int)B.act[lo + rel];
-                    foot = B.foot[lo + rel];
+                    foot = B.foot[wslot(B, lo + rel)];
                 }
             }
             diamond_of<S, K>(m, act, foot, P, dm);
@@ -1251,7 +1253,7 @@ __global__ __launch_bounds__(256) void k_capacity_check(const Params P, const De
     for (u64 t = lo + (u64)blockIdx.x * 256 + threadIdx.x; t < hi; t += (u64)gridDim.x * 256) {
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + t * (u64)NW, w, m);
+        load_state<S, K>(B.store + wslot(B, t) * (u64)NW, w, m);
         for (int lane = 0; lane < nl; ++lane) {
             Delta d;
             lane_delta<S, K>(w, m, lane, P, d);
@@ -1377,8 +1379,8 @@ __device__ __forceinline__ u64 match_class8(u32 c, bool act) {
 // positions (match_class8), not one per position: a window's states fall in a
 // few classes, and same-address LDS atomics serialise (0.91 bank conflicts per
 // LDS access with per-position atomics, round 4's PMC profile).
-__global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo, u64 nf, u64 wt, uint16_t* word,
-                                                      unsigned long long* wnext) {
+__global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 wmask, u64 lo, u64 nf, u64 wt,
+                                                      uint16_t* word, unsigned long long* wnext) {
     __shared__ u32 bins[256];
     __shared__ uint8_t cs[256 * 16];
     const u32 tid = threadIdx.x;
@@ -1392,7 +1394,7 @@ __global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 lo
         for (u32 p0 = 0; p0 < wn; p0 += 256) {  // block-uniform rounds
             const u32 p = p0 + tid;
             const bool act = p < wn;
-            const u32 c = act ? (u32)cls[lo + win + p] : 0u;
+            const u32 c = act ? (u32)cls[(lo + win + p) & wmask] : 0u;
             if (act) cs[p] = (uint8_t)c;
             const u64 peers = match_class8(c, act);
             if (act && (peers & lt) == 0) atomicAdd(&bins[c], (u32)__popcll(peers));
@@ -1435,7 +1437,7 @@ hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 w
     const u64 per_block = (nf + grid * 256ull - 1) / (grid * 256ull);
     const u64 wt = per_block < wt_max ? (per_block ? per_block : 1ull) : wt_max;
     const u64 nwin = (nf + 256ull * wt - 1) / (256ull * wt);
-    hipLaunchKernelGGL(k_window_order, dim3((unsigned)(nwin < grid ? nwin : grid)), dim3(256), 0, st, B.cls, lo, nf,
+    hipLaunchKernelGGL(k_window_order, dim3((unsigned)(nwin < grid ? nwin : grid)), dim3(256), 0, st, B.cls, B.wmask, lo, nf,
                        wt, B.word, (unsigned long long*)&B.ctr->wnext);
     return hipGetLastError();
 }
@@ -1698,7 +1700,7 @@ __global__ __launch_bounds__(256) void k_ties(const Params P, const PermTable PT
             const u64 rec = B.ties[t];
             pidx = rec & ((1ull << 56) - 1);
             lane = (int)(rec >> 56);
-            load_state<S, K>(B.store + pidx * (u64)NW, w, m);
+            load_state<S, K>(B.store + wslot(B, pidx) * (u64)NW, w, m);
             lane_delta<S, K>(w, m, lane, P, d);
             u64 base[S];
 #pragma unroll
@@ -1808,7 +1810,7 @@ __global__ __launch_bounds__(256) void k_rehash(const Params P, const PermTable 
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + i * (u64)NW, w, m);
+        load_state<S, K>(B.store + wslot(B, i) * (u64)NW, w, m);
         const Fp key = fp_weaken(SYM ? canon_state<S, K>(w, m, PT.code, PT.np) : state_fp<S, K>(w, m), P.fp_mask);
         if (!fp_insert_fp(B.table, B.tmask, key, &B.ctr->table_full)) atomicOr(&B.ctr->overflow, 8u);  // duplicate
     }

@@ -477,18 +477,26 @@ def test_spill_completes_with_the_oracle_counts(name, slack, links):
     assert (res.distinct, res.generated, res.depth, res.left_on_queue) == \
         (g["distinct"], g["generated"], g["depth"], g["left_on_queue"])
     assert res.spills > 0
-    assert res.distinct - res.spilled <= cfg.device_window
+    # resident at the end: at most the window (the ring of device links rounds it up to a power of two)
+    assert res.distinct - res.spilled <= (cfg.device_window if links == "host" else 2 * cfg.device_window)
 
 
-@pytest.mark.parametrize("name", ["bug_one_leader", "messages_small", "sym_bug_one_leader"])
-def test_spill_trace_equals_the_resident_trace(name, links):
-    """The counterexample walks parents through host segments and the device
-    window; it must be a behaviour of the spec to a violating state at the
-    depth the resident run reports (which parent wins a race depends on the
-    launch sizes, so the two traces may differ state by state)."""
+# (with the links in HBM the window is a ring of a power of two states: the cases
+# whose ring still wraps before the violation — a violation search usually ends at
+# its largest level)
+@pytest.mark.parametrize("name,mode", [("bug_one_leader", "host"), ("messages_small", "host"),
+                                       ("sym_bug_one_leader", "host"), ("messages_small", "device"),
+                                       ("bug_votes_granted", "device"), ("bug_quorum_log", "device")])
+def test_spill_trace_equals_the_resident_trace(name, mode, monkeypatch):
+    """The counterexample walks parents through spilled states (replayed from
+    Init) and the device window; it must be a behaviour of the spec to a
+    violating state at the depth the resident run reports (which parent wins a
+    race depends on the launch sizes, so the two traces may differ state by state)."""
+    if mode == "host":
+        monkeypatch.setenv("RMC_SPILL_HOST_LINKS", "1")
     g, cfg = spill_cfg(name, 2048)
     res, _, trace = run(cfg)
-    assert res.spills > 0
+    assert res.spills > 0 and res.spill_links_on_device == (mode == "device")
     base, _, trace0 = run(cfg_from(g["params"]))
     assert (res.violated_inv, res.violation_depth, res.distinct, res.generated) == \
         (base.violated_inv, base.violation_depth, base.distinct, base.generated) == \
@@ -531,22 +539,27 @@ def test_spill_checkpoint_and_recover(first, second, tmp_path, links):
     assert r2.spills > r1.spills  # the recovered result carries the checkpointed statistics forward
 
 
-def test_spill_recover_to_the_violation_replays_the_trace(tmp_path, links):
-    g, cfg = spill_cfg("bug_one_leader", 2048, max_depth=9)
+@pytest.mark.parametrize("name,stop,mode", [("bug_one_leader", 9, "host"), ("bug_quorum_log", 15, "device")])
+def test_spill_recover_to_the_violation_replays_the_trace(tmp_path, name, stop, mode, monkeypatch):
+    if mode == "host":
+        monkeypatch.setenv("RMC_SPILL_HOST_LINKS", "1")
+    g, cfg = spill_cfg(name, 2048, max_depth=stop)
     with rmc.Checker(cfg) as ck:
         ck.run()
         ck.checkpoint(str(tmp_path / "ck"))
-    _, cfg = spill_cfg("bug_one_leader", 2048)
+    _, cfg = spill_cfg(name, 2048)
     with rmc.Checker(cfg) as ck:
         ck.recover(str(tmp_path / "ck"))
         res = ck.run()
         trace = ck.trace()
-    assert res.spills > 0  # levels 10-11 outgrow the window: the trace replays spilled states
+    assert res.spills > 0  # the last levels outgrow the window: the trace replays spilled states
+    assert res.spill_links_on_device == (mode == "device")
     assert (res.violated_inv, res.violation_depth, res.distinct, res.generated) == \
         (g["violated_inv"], g["violation_depth"], g["distinct"], g["generated"])
     p = g["params"]
     model = R.Model(n_servers=p["n_servers"], n_values=p["n_values"], max_term=p["max_term"],
-                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"], bug_quorum=True)
+                    max_log=p["max_log_len"], max_msgs=p["max_msgs"], max_dup=p["max_dup"],
+                    bug_quorum=bool(p["bug_quorum"]))
     check_trace(model, trace, res.violated_inv, res.violation_depth)
 
 
