@@ -1,18 +1,20 @@
 # rocprofv3 evidence for the bench command (the build in the tree):
 # a kernel trace with stats, then one PMC pass per counter group (separate
 # runs: FETCH_SIZE and WRITE_SIZE alone, instruction mix, waits, LDS).
-#   OUT=gpurun_out/<tag> [ENVS="RMC_EXPAND_VARIANT=7"] bash tools/gpu/pmc.sh
+#   OUT=gpurun_out/<tag> [ENVS="RMC_EXPAND_VARIANT=7"] [CMD="raft.tla_amd/bin/rmc-tlc ..."] bash tools/gpu/pmc.sh
+# (CMD replaces the bench command; it must be the program itself, no wrapper)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 P=${OUT:-gpurun_out/pmc}
 mkdir -p $P
 B="--steps 1 --warmup 0 --no-cpu --no-probe-ceiling ${BENCH_ARGS}"
+C=${CMD:-python3 bench.py $B}
 for v in $ENVS; do export $v; done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py $B > $P/kt.json 2> $P/kt.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- $C > $P/kt.json 2> $P/kt.err || exit 1
 find $P/kt -name "*.db" -delete
 pass() {  # name counters...
   local name=$1; shift
-  timeout -s KILL 150 rocprofv3 --pmc "$@" -d $P/$name -o $name -- python3 bench.py $B > $P/$name.json 2> $P/$name.err || exit 1
+  timeout -s KILL 150 rocprofv3 --pmc "$@" -d $P/$name -o $name -- $C > $P/$name.json 2> $P/$name.err || exit 1
   python3 tools/pmc_totals.py $P/$name $name >> $P/totals.jsonl || exit 1
 }
 pass fetch FETCH_SIZE

@@ -8,8 +8,3 @@ python3 tools/pmc_summary.py $O/pmc_xl $O/summary MCraftBenchXL || exit 1
 ls $O/summary
 timeout -k 10 300 python -u tools/level_times.py specs/MCraftBenchXL.cfg 0 0 spill > $O/levels_MCraftBenchXL.jsonl 2> $O/levels.err || exit 1
 tail -1 $O/levels_MCraftBenchXL.jsonl
-for r in 1 2; do
-  timeout -k 10 200 python -u bench.py --config specs/MCraftBench.cfg --no-cpu --no-probe-ceiling --steps 5 --warmup 1 > $O/b_plain_$r.json 2> $O/b_plain_$r.err || exit 1
-  timeout -k 10 200 python -u bench.py --config specs/MCraftBench.cfg --no-cpu --no-probe-ceiling --steps 5 --warmup 1 --force-dist > $O/b_dist_$r.json 2> $O/b_dist_$r.err || exit 1
-done
-for f in $O/b_*.json; do python -c "import json; d=json.load(open('$f')); print('$f', round(d['ms_per_step'],2), round(d['roofline']['kernel_ms_per_step'],2), d['config']['distinct'], (d.get('sharded') or {}).get('host_wait_s_rank0'))"; done

@@ -53,7 +53,8 @@ def main():
         "command": "tools/gpu/pmc.sh: rocprofv3 --kernel-trace --stats, then one --pmc pass per counter group "
                    "(FETCH_SIZE | WRITE_SIZE | SQ instruction mix | SQ waits | LDS) -- python3 bench.py --steps 1 "
                    "--warmup 0 --no-cpu --no-probe-ceiling; per-kernel totals by tools/pmc_totals.py",
-        "workload": f"specs/{stem}.cfg, BFS to fixpoint (bench step + the untimed fingerprint-salt re-run)",
+        "workload": os.environ.get("PMC_WORKLOAD",
+                                   f"specs/{stem}.cfg, BFS to fixpoint (bench step + the untimed fingerprint-salt re-run)"),
         "kernel": k,
         "pmc_launches": n,
         "fetch_size_kb_total": c["FETCH_SIZE"]["total"],
