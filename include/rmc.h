@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 5
+#define RMC_ABI_VERSION 6 /* 6: rmc_result.spill_links_on_device (round 5) */
 
 /* Capacity of the packed encoding (DESIGN.md "Packed state"): the layout the
  * BFS kernels run on when every bound fits it. */

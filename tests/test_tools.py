@@ -1,8 +1,8 @@
 """The measurement tools behind DESIGN.md §e's numbers, run on the committed
-round-4 inputs (profiles/r04/dist8/): the 8-GPU cost model of the bench model
-and the plan of specs/MCraftBench8.cfg reproduce the figures DESIGN quotes,
-and the sharded kernel's measured rate (--k-dist) enters the expansion term.
-CPU only."""
+inputs: the 8-GPU plan of the XL bench workload (profiles/r05/dist8/), the cost
+model of the old bench model (profiles/r04/dist8/) and the plan of
+specs/MCraftBench8.cfg reproduce the figures DESIGN quotes, and the sharded
+kernel's measured rate (--k-dist) enters the expansion term.  CPU only."""
 import json
 import os
 import subprocess
@@ -12,6 +12,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 D8 = os.path.join(ROOT, "profiles", "r04", "dist8")
+X8 = os.path.join(ROOT, "profiles", "r05", "dist8")
 
 
 def _run(args):
@@ -30,10 +31,24 @@ def test_cost_model_reproduces_the_design_table():
     assert head["levels"] == 56 and head["rounds_total"] == 54
     assert head["T1_s"] == pytest.approx(0.2380, abs=1e-3)
     assert mid["replicated_levels"] == 23
-    # 53.3 / 60.8 / 74.1 ms at the three latency rows
-    for row, t8 in ((fast, 53.3), (mid, 60.8), (slow, 74.1)):
+    # 55.8 / 63.2 / 76.6 ms at the three latency rows (16-B key records)
+    for row, t8 in ((fast, 55.8), (mid, 63.2), (slow, 76.6)):
         assert row["T_N_ms"] == pytest.approx(t8, abs=0.1)
         assert row["expand_ms"] == pytest.approx(35.7, abs=0.1)
+
+
+def test_xl_plan_reproduces_the_design_table():
+    rows = _run(["tools/bench8_plan.py", os.path.join(X8, "levels_MCraftBenchXL_depth36.jsonl"),
+                 os.path.join(X8, "rounds_MCraftBenchXL_depth36.txt"),
+                 os.path.join(X8, "dist8_MCraftBenchXL_depth36.json"), os.path.join(D8, "levels_MCraftBench.jsonl"),
+                 "8", "--k-dist", "1.04", "--measured", os.path.join(X8, "levels_MCraftBenchXL.jsonl")])
+    head, plan = rows[0], rows[-1]
+    assert head["prefix_depth"] == 35 and head["counted_distinct"] == 1_223_708_472
+    assert plan["distinct_est"] == 4_132_397_328 and plan["T1_model_s"] == pytest.approx(0.855, abs=1e-3)
+    # serial 187.4 / 197.8 / 216.6 ms, overlapped 164.5 / 175.0 / 193.8 ms
+    assert plan["T_N_ms"] == pytest.approx([187.4, 197.8, 216.6], abs=0.11)
+    assert plan["T_N_ms_overlapped"] == pytest.approx([164.5, 175.0, 193.8], abs=0.11)
+    assert plan["expand_ms"][0] == pytest.approx(128.9, abs=0.11)
 
 
 def test_cost_model_prices_the_sharded_kernel_rate():
