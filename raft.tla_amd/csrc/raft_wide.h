@@ -189,11 +189,28 @@ RMC_HD void wbag_remove_at(WState& s, int k) {
     s.cnt[s.nmsg] = 0;
 }
 
+// The bag operations a lane applies: one thread at a time (SerialBag), or the
+// whole wave on a record in LDS (WaveBag, rmc_wide.hip: every lane calls with
+// the same arguments, each compares / moves one message).
+struct SerialBag {
+    static RMC_HD int fits(const WState& s, const WMsg& m) { return wbag_fits(s, m); }
+    static RMC_HD int reply_fits(const WState& s, const WMsg& r, int x) { return wreply_fits(s, r, x); }
+    static RMC_HD int add(WState& s, const WMsg& m) { return wbag_add(s, m); }
+    static RMC_HD void remove_at(WState& s, int k) { wbag_remove_at(s, k); }
+};
+
 // Lane `lane` on s (raft.tla:136-417, one action instance): W_OFF when the
 // instance is not enabled, W_ON when it is (*t = the successor, if t is
 // given), else the field its successor overflows (W_TERM .. W_DUP; *t is not
-// written).  t == nullptr only evaluates the guard (the simulation's draw);
-// pre: *t already holds a copy of s (a wave that copied it cooperatively).
+// written).  t == nullptr only evaluates the guard (the simulation's draw): W_OFF
+// or not — a nonzero code may then be W_ON for a successor that would not fit,
+// which the draw treats alike (it is decided when the drawn lane is applied);
+// pre: *t already holds a copy of s (a wave that copied it cooperatively), or
+// t == &s (every field of s is read before the same field of *t is written).
+// Scalar fields of *t are written from s (never read-modify-written), so a
+// wave whose lanes all apply the same lane to a shared record writes the same
+// values.
+template <class Bag = SerialBag>
 RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre = false) {
     const int S = M.S;
     const int f = M.L.family(lane), x = lane - M.L.off[f];
@@ -228,6 +245,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
     case 2: {  // RequestVote(i, j) :157-166 (no i /= j guard)
         const int i = x / S, j = x % S;
         if (s.st[i] != CANDIDATE || ((s.vR[i] >> j) & 1u)) return W_OFF;
+        if (!t) return W_ON;
         WMsg m;
         wmsg_zero(m);
         m.type = RVQ;
@@ -236,10 +254,10 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
         m.c = s.len[i];
         m.src = (uint8_t)i;
         m.dst = (uint8_t)j;
-        const int fit = wbag_fits(s, m);
-        if (fit != W_ON || !t) return fit;
+        const int fit = Bag::fits(s, m);
+        if (fit != W_ON) return fit;
         if (!pre) wcopy_state(*t, s);
-        return wbag_add(*t, m);
+        return Bag::add(*t, m);
     }
     case 3: {  // BecomeLeader(i) :195-203
         const int i = x;
@@ -283,6 +301,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
     case 6: {  // AppendEntries(i, j) :171-192
         const int i = x / S, j = x % S;
         if (i == j || s.st[i] != LEADER) return W_OFF;
+        if (!t) return W_ON;
         const int nidx = s.ni[i][j], len = s.len[i];
         const int prev = nidx - 1;
         const int last = len < nidx ? len : nidx;  // Min({Len(log[i]), nextIndex[i][j]})
@@ -299,10 +318,10 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
         m.c = (uint8_t)(s.ci[i] < last ? s.ci[i] : last);
         m.src = (uint8_t)i;
         m.dst = (uint8_t)j;
-        const int fit = wbag_fits(s, m);
-        if (fit != W_ON || !t) return fit;
+        const int fit = Bag::fits(s, m);
+        if (fit != W_ON) return fit;
         if (!pre) wcopy_state(*t, s);
-        return wbag_add(*t, m);
+        return Bag::add(*t, m);
     }
     case 7: {  // Receive(m) :388-403 for bag slot x
         if (x >= s.nmsg) return W_OFF;
@@ -317,6 +336,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
             return W_ON;
         }
         if (m.type == RVQ) {  // HandleRequestVoteRequest :244-263
+            if (!t) return W_ON;
             const int lt = wlast_term(s, i);
             const int logok = m.b > lt || (m.b == lt && m.c >= s.len[i]);
             const int grant = m.term == ct && logok && (s.vf[i] == NIL || s.vf[i] == j);
@@ -330,22 +350,22 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
             r.n = s.len[i];
             for (int e = 0; e < s.len[i]; ++e) r.e[e] = s.log[i][e];
             // Reply :102-103 (response added, request removed): the capacity of the net bag
-            const int fit = wreply_fits(s, r, x);
-            if (fit != W_ON || !t) return fit;
+            const int fit = Bag::reply_fits(s, r, x);
+            if (fit != W_ON) return fit;
             if (!pre) wcopy_state(*t, s);
             if (grant) t->vf[i] = (uint8_t)j;
-            wbag_remove_at(*t, x);
-            wbag_add(*t, r);
+            Bag::remove_at(*t, x);
+            Bag::add(*t, r);
             return W_ON;
         }
         if (m.type == RVP) {
             if (!t) return W_ON;
             if (!pre) wcopy_state(*t, s);
             if (m.term == ct) {  // HandleRequestVoteResponse :267-279
-                t->vR[i] |= (uint8_t)(1u << j);
-                if (m.a) t->vG[i] |= (uint8_t)(1u << j);
+                t->vR[i] = (uint8_t)(s.vR[i] | (1u << j));
+                if (m.a) t->vG[i] = (uint8_t)(s.vG[i] | (1u << j));
             }  // else DropStaleResponse :382-385
-            wbag_remove_at(*t, x);
+            Bag::remove_at(*t, x);
             return W_ON;
         }
         if (m.type == AEQ) {  // HandleAppendEntriesRequest :347-356
@@ -358,11 +378,12 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
             r.src = (uint8_t)i;
             r.dst = (uint8_t)j;
             if (m.term < ct || (s.st[i] == FOLLOWER && !logok)) {  // Reject :281-293
-                const int fit = wreply_fits(s, r, x);
-                if (fit != W_ON || !t) return fit;
+                if (!t) return W_ON;
+                const int fit = Bag::reply_fits(s, r, x);
+                if (fit != W_ON) return fit;
                 if (!pre) wcopy_state(*t, s);
-                wbag_remove_at(*t, x);
-                wbag_add(*t, r);
+                Bag::remove_at(*t, x);
+                Bag::add(*t, r);
                 return W_ON;
             }
             if (s.st[i] == CANDIDATE) {  // ReturnToFollowerState :295-299 — m stays
@@ -377,13 +398,14 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
                 // AppendEntriesAlreadyDone :301-317: UNCHANGED logVars after binding
                 // commitIndex' is an equality test under TLC
                 if (m.c != s.ci[i]) return W_OFF;
+                if (!t) return W_ON;
                 r.a = 1;
                 r.b = (uint8_t)(pidx + m.n);
-                const int fit = wreply_fits(s, r, x);
-                if (fit != W_ON || !t) return fit;
+                const int fit = Bag::reply_fits(s, r, x);
+                if (fit != W_ON) return fit;
                 if (!pre) wcopy_state(*t, s);
-                wbag_remove_at(*t, x);
-                wbag_add(*t, r);
+                Bag::remove_at(*t, x);
+                Bag::add(*t, r);
                 return W_ON;
             }
             if (len >= index) {  // ConflictAppendEntriesRequest :319-325 — drops the LAST entry, m stays
@@ -416,7 +438,7 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
                 t->ni[i][j] = (uint8_t)(v < 1 ? 1 : v);
             }
         }  // else DropStaleResponse
-        wbag_remove_at(*t, x);
+        Bag::remove_at(*t, x);
         return W_ON;
     }
     case 8: {  // DuplicateMessage(m) :410-412
@@ -424,14 +446,14 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
         if (s.cnt[x] >= CMAX) return W_DUP;
         if (!t) return W_ON;
         if (!pre) wcopy_state(*t, s);
-        t->cnt[x] += 1;
+        t->cnt[x] = (uint8_t)(s.cnt[x] + 1);
         return W_ON;
     }
     default: {  // DropMessage(m) :415-417
         if (x >= s.nmsg) return W_OFF;
         if (!t) return W_ON;
         if (!pre) wcopy_state(*t, s);
-        wbag_remove_at(*t, x);
+        Bag::remove_at(*t, x);
         return W_ON;
     }
     }
@@ -590,6 +612,26 @@ RMC_HD int tlc_draw(const u64 (&en)[NC], int nl, int o7, int o8, int o9, u64& rs
         u32 k = (u32)(w_rand(rs) % (u64)cnt);
         for (int lane = lo; lane < hi; ++lane)
             if (on(lane) && k-- == 0) return lane;
+    }
+    return -1;
+}
+
+// The uniform draws (RMC_SIM_WITHIN_CAPACITY / RMC_SIM_TRUNCATE): one of the
+// enabled lanes not excluded, uniformly, with one random number.
+template <int NC>
+RMC_HD int uniform_draw(const u64 (&en)[NC], const u64 (&excl)[NC], u64& rs) {
+    u32 cnt = 0;
+    for (int c = 0; c < NC; ++c) cnt += (u32)__builtin_popcountll(en[c] & ~excl[c]);
+    if (!cnt) return -1;
+    u32 k = (u32)(w_rand(rs) % (u64)cnt);
+    for (int c = 0; c < NC; ++c) {
+        u64 mm = en[c] & ~excl[c];
+        const u32 p = (u32)__builtin_popcountll(mm);
+        if (k < p) {
+            for (; k; --k) mm &= mm - 1;
+            return 64 * c + __builtin_ctzll(mm);
+        }
+        k -= p;
     }
     return -1;
 }

@@ -126,10 +126,148 @@ __global__ __launch_bounds__(64) void k_wlist(const WModel M, const WState* in, 
 }
 
 
+// ---- one wave on one record in LDS (k_wsimulate_w) ----------------------------------
+// Every lane of the wave calls these with the same arguments; lane q handles
+// message q (KW = 64 = the wave), so a bag search is one compare per lane and a
+// ballot, and an insert / removal moves every later message at once.
+__device__ __forceinline__ void w_wsync() {  // the wave's LDS writes seen by the whole wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+static_assert(KW <= 64, "WaveBag: one message per lane of the wave");
+struct WaveBag {
+    // slot of m in the sorted bag (-1: absent); *pos = the messages below m
+    static __device__ int find(const WState& s, const WMsg& m, int* pos) {
+        const int ln = (int)__lane_id();
+        const int n = s.nmsg;
+        const int c = ln < n ? wmsg_cmp(s.msg[ln], m) : 1;
+        const u64 eq = __ballot(c == 0), lt = __ballot(c < 0);
+        *pos = (int)__popcll(lt);
+        return eq ? (int)__builtin_ctzll(eq) : -1;
+    }
+    static __device__ int fits(const WState& s, const WMsg& m) {
+        int pos;
+        const int k = find(s, m, &pos);
+        if (k >= 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
+        return s.nmsg >= KW ? W_MSGS : W_ON;
+    }
+    static __device__ int reply_fits(const WState& s, const WMsg& r, int x) {
+        int pos;
+        const int k = find(s, r, &pos);
+        if (k >= 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
+        return (s.nmsg >= KW && s.cnt[x] > 1) ? W_MSGS : W_ON;
+    }
+    static __device__ int add(WState& s, const WMsg& m) {  // wbag_add
+        const int ln = (int)__lane_id();
+        w_wsync();
+        int k;
+        const int e = find(s, m, &k);
+        const int n = s.nmsg;
+        if (e >= 0) {
+            const int c = s.cnt[e];
+            if (c >= CMAX) return W_DUP;
+            w_wsync();
+            if (ln == 0) s.cnt[e] = (uint8_t)(c + 1);
+            w_wsync();
+            return W_ON;
+        }
+        if (n >= KW) return W_MSGS;
+        const bool mv = ln >= k && ln < n;  // messages k .. n-1 move up one slot
+        WMsg mine;
+        uint8_t c = 0;
+        if (mv) {
+            mine = s.msg[ln];
+            c = s.cnt[ln];
+        }
+        w_wsync();
+        if (mv) {
+            s.msg[ln + 1] = mine;
+            s.cnt[ln + 1] = c;
+        }
+        if (ln == 0) {
+            s.msg[k] = m;
+            s.cnt[k] = 1;
+            s.nmsg = (uint8_t)(n + 1);
+        }
+        w_wsync();
+        return W_ON;
+    }
+    static __device__ void remove_at(WState& s, int k) {  // wbag_remove_at
+        const int ln = (int)__lane_id();
+        w_wsync();
+        const int c = s.cnt[k], n = s.nmsg;
+        if (c > 1) {
+            w_wsync();
+            if (ln == 0) s.cnt[k] = (uint8_t)(c - 1);
+            w_wsync();
+            return;
+        }
+        const bool mv = ln > k && ln < n;  // messages k+1 .. n-1 move down one slot
+        WMsg mine;
+        uint8_t cm = 0;
+        if (mv) {
+            mine = s.msg[ln];
+            cm = s.cnt[ln];
+        }
+        w_wsync();
+        if (mv) {
+            s.msg[ln - 1] = mine;
+            s.cnt[ln - 1] = cm;
+        }
+        if (ln == n - 1) {  // the freed last slot (also written by no mover: n - 1 > ln - 1)
+            wmsg_zero(s.msg[n - 1]);
+            s.cnt[n - 1] = 0;
+        }
+        if (ln == 0) s.nmsg = (uint8_t)(n - 1);
+        w_wsync();
+    }
+};
+
+// win_model with lane q checking message q's count.
+__device__ __forceinline__ int w_in_model_wave(const WModel& M, const WState& t) {
+    const int ln = (int)__lane_id();
+    bool bad = ln < t.nmsg && t.cnt[ln] > M.max_dup;
+    if (ln < M.S) bad = bad || t.ct[ln] > M.max_term || t.len[ln] > M.max_log;
+    if (ln == 0) bad = bad || t.nmsg > M.max_msgs;
+    return __ballot(bad) == 0;
+}
+
+// TypeOK (raft.tla:482-492, wtype_ok) with lane i checking server i and lane q
+// message q.
+__device__ __forceinline__ int w_type_ok_wave(const WModel& M, const WState& s) {
+    const int ln = (int)__lane_id();
+    bool bad = false;
+    if (ln < M.S) {
+        const int i = ln;
+        bad = s.st[i] > LEADER || (s.vf[i] != NIL && s.vf[i] >= M.S) || ((s.vR[i] | s.vG[i]) >> M.S) != 0;
+        for (int j = 0; j < M.S; ++j) bad = bad || s.ni[i][j] < 1;
+        for (int x = 0; x < s.len[i]; ++x) bad = bad || s.log[i][x].value >= M.V;
+    }
+    if (ln < s.nmsg) {
+        const WMsg& m = s.msg[ln];
+        bad = bad || s.cnt[ln] < 1 || m.src >= M.S || m.dst >= M.S;
+        for (int x = 0; x < m.n; ++x) bad = bad || m.e[x].value >= M.V;
+    }
+    return __ballot(bad) == 0;
+}
+
+// wcheck_invariants for the whole wave (every lane gets the result): TypeOK
+// lane-parallel, the other named invariants on lane 0 in wcheck_invariants'
+// order.
+__device__ __forceinline__ int w_check_invariants_wave(const WModel& M, const WState& s) {
+    if ((M.inv_mask & 1) && !w_type_ok_wave(M, s)) return 1;
+    if (!(M.inv_mask & ~1)) return 0;
+    WModel M2 = M;
+    M2.inv_mask &= ~1;
+    const int v = __lane_id() == 0 ? wcheck_invariants(M2, s) : 0;
+    return __shfl(v, 0);
+}
+
 // Random behaviours (TLC -simulate): one thread per behaviour, from one of the
 // n_init staged initial states, up to depth - 1 steps.  mode 0: uniform over
 // the enabled successors within the bounds (rejection: an out-of-bounds draw
-// is excluded and the draw repeated); 1: uniform over every enabled successor,
+// is excluded and the draw repeated; uniform_draw); 1: uniform over every enabled successor,
 // one beyond the bounds ends the behaviour (truncated); 2: TLC's draw
 // (tlc_draw: random start, random prime stride, the first enabled action, a
 // uniform successor of it); beyond the bounds it is truncated like mode 1.
@@ -152,22 +290,11 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
         if (v) atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 44) | ((u64)(v - 1) << 40) | b));
         u64 excl[WLMASK] = {};  // mode 0: lanes whose successor left the bounds this step
         for (int dd = 2; dd <= depth && !v;) {
-            int pick = -1;
-            if (mode == 2) {  // TLC's draw
-                constexpr int NCL = (WLANES_MAX + 63) / 64;
-                u64 en[NCL] = {};
-                for (int lane = 0; lane < nl; ++lane)
-                    if (wlane(M, buf[cur], lane, nullptr) != W_OFF) en[lane >> 6] |= 1ull << (lane & 63);
-                pick = tlc_draw<NCL>(en, nl, o7, o8, o9, rs);
-            } else {
-                u32 cnt = 0;
-                for (int lane = 0; lane < nl; ++lane) {  // reservoir: uniform over the enabled lanes
-                    if ((excl[lane >> 6] >> (lane & 63)) & 1ull) continue;
-                    if (wlane(M, buf[cur], lane, nullptr) == W_OFF) continue;
-                    ++cnt;
-                    if (w_rand(rs) % cnt == 0) pick = lane;
-                }
-            }
+            u64 en[WLMASK] = {};
+            for (int lane = 0; lane < nl; ++lane)
+                if (wlane(M, buf[cur], lane, nullptr) != W_OFF) en[lane >> 6] |= 1ull << (lane & 63);
+            const int pick = mode == 2 ? tlc_draw<WLMASK>(en, nl, o7, o8, o9, rs)  // TLC's draw
+                                       : uniform_draw<WLMASK>(en, excl, rs);
             if (pick < 0) {
                 u64 any = 0;
                 for (int q = 0; q < WLMASK; ++q) any |= excl[q];
@@ -202,15 +329,17 @@ __global__ __launch_bounds__(64) void k_wsimulate(const WModel M, const WState* 
 // The same walks, one WAVE per behaviour (RMC_WSIM=1, the default): the two
 // 5-KB records live in LDS instead of one lane's private memory, the 64 lanes
 // evaluate the action guards in parallel (a ballot per 64 lanes of the lane
-// table), copy the record together, and lane 0 applies the drawn action and
-// checks the invariants.  The draws are the thread kernel's (the same random
-// stream per behaviour), so both give the same behaviours.
+// table), copy the record together, apply the drawn action together (the
+// scalar fields by every lane alike, the bag one message per lane: WaveBag)
+// and check TypeOK and the CONSTRAINT one server / message per lane.  The
+// draws are the thread kernel's (the same random stream per behaviour), so
+// both give the same behaviours.
 constexpr int WSIM_WAVES = 4;  // behaviours per 256-thread block (2 x 5,080 B of LDS each)
-__global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M, const WState* inits, u64 n_init,
+__global__ __launch_bounds__(64 * WSIM_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_wsimulate_w(const WModel M, const WState* inits, u64 n_init,
                                                                 u64 n_beh, int depth, u64 seed, int mode,
-                                                                SimCounters* out, i64 rec_beh, WState* rec) {
+                                                                SimCounters* out, i64 rec_beh, WState* rec,
+                                                                int inplace) {
     __shared__ WState s_buf[WSIM_WAVES][2];
-    __shared__ int s_res[WSIM_WAVES];
     const int wv = (int)(threadIdx.x >> 6), ln = (int)(threadIdx.x & 63);
     u64 steps = 0, trunc = 0, dead = 0;  // lane 0's tallies
     const int nl = M.L.off[10];
@@ -231,8 +360,7 @@ __global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M,
         copy(s_buf[wv][0], inits[w_rand(rs) % n_init]);
         const bool record = (i64)b == rec_beh;
         if (record && ln == 0) wcopy_state(rec[0], s_buf[wv][0]);
-        int v = ln == 0 ? wcheck_invariants(M, s_buf[wv][0]) : 0;
-        v = __shfl(v, 0);
+        int v = w_check_invariants_wave(M, s_buf[wv][0]);
         if (v && ln == 0)
             atomicMin((unsigned long long*)&out->viol, (unsigned long long)((1ull << 44) | ((u64)(v - 1) << 40) | b));
         u64 excl[WLMASK] = {};  // mode 0: lanes whose successor left the bounds this step (uniform)
@@ -246,19 +374,9 @@ __global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M,
                 const bool on = lane < nl && wlane(M, s, lane, nullptr) != W_OFF;
                 en[c] = __ballot(on);
             }
-            int pick = -1;
-            if (mode == 2) {  // TLC's draw, exactly as k_wsimulate
-                pick = tlc_draw<NC>(en, nl, o7, o8, o9, rs);
-            } else {  // reservoir over the enabled lanes in lane order (k_wsimulate's draws)
-                u32 cnt = 0;
-                for (int c = 0; c < NC; ++c)
-                    for (u64 mm = en[c]; mm; mm &= mm - 1) {
-                        const int lane = 64 * c + __builtin_ctzll(mm);
-                        if ((excl[lane >> 6] >> (lane & 63)) & 1ull) continue;
-                        ++cnt;
-                        if (w_rand(rs) % cnt == 0) pick = lane;
-                    }
-            }
+            static_assert(NC == WLMASK, "one mask word per 64 lanes");
+            const int pick = mode == 2 ? tlc_draw<NC>(en, nl, o7, o8, o9, rs)  // k_wsimulate's draws exactly
+                                       : uniform_draw<NC>(en, excl, rs);
             if (pick < 0) {
                 u64 any = 0;
                 for (int q = 0; q < WLMASK; ++q) any |= excl[q];
@@ -266,16 +384,16 @@ __global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M,
                 else ++dead;
                 break;
             }
-            WState& t = s_buf[wv][cur ^ 1];
-            copy(t, s);
-            if (ln == 0) {
-                const int r = wlane(M, s, pick, &t, true);
-                s_res[wv] = (r != W_ON || !win_model(M, t)) ? 1 : 0;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (s_res[wv]) {
+            // mode 0 may redraw from s: the successor goes to the other record.
+            // Otherwise a failed draw ends the behaviour, so the successor is
+            // written over s in place (wlane reads every field of s before it
+            // writes it) and the 5-KB copy is skipped.
+            const bool inp = inplace && mode != 0;
+            WState& t = s_buf[wv][inp ? cur : cur ^ 1];
+            if (!inp) copy(t, s);
+            const int r = wlane<WaveBag>(M, s, pick, &t, true);  // every lane: the same r
+            w_wsync();
+            if (r != W_ON || !w_in_model_wave(M, t)) {
                 if (mode == 0) {
                     excl[pick >> 6] |= 1ull << (pick & 63);
                     continue;
@@ -283,12 +401,11 @@ __global__ __launch_bounds__(64 * WSIM_WAVES) void k_wsimulate_w(const WModel M,
                 ++trunc;
                 break;
             }
-            cur ^= 1;
+            if (!inp) cur ^= 1;
             for (int q = 0; q < WLMASK; ++q) excl[q] = 0;
             ++steps;
             if (record && ln == 0) wcopy_state(rec[dd - 1], t);
-            v = ln == 0 ? wcheck_invariants(M, t) : 0;
-            v = __shfl(v, 0);
+            v = w_check_invariants_wave(M, t);
             if (v && ln == 0)
                 atomicMin((unsigned long long*)&out->viol, (unsigned long long)(((u64)dd << 44) | ((u64)(v - 1) << 40) | b));
             ++dd;
@@ -329,9 +446,13 @@ hipError_t launch_wsimulate(const WModel& M, const WState* inits, u64 n_init, u6
         const char* e = getenv("RMC_WSIM");
         return e ? atoi(e) : 1;
     }();
+    static const int inplace = [] {  // RMC_WSIM_INPLACE=0: every successor to the other record (A/B)
+        const char* e = getenv("RMC_WSIM_INPLACE");
+        return e ? atoi(e) : 1;
+    }();
     if (wave)
         hipLaunchKernelGGL(k_wsimulate_w, dim3(grid_for(n_beh, WSIM_WAVES, 8192)), dim3(64 * WSIM_WAVES), 0, st, M,
-                           inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec);
+                           inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, inplace);
     else
         hipLaunchKernelGGL(k_wsimulate, dim3(grid_for(n_beh, 64, 16384)), dim3(64), 0, st, M, inits, n_init, n_beh,
                            depth, seed, mode, out, rec_beh, rec);

@@ -247,3 +247,43 @@ def test_wide_terms_above_127_and_reply_capacity_of_the_net_bag(rvq_count):
     rv = [t for f, t in have if f == "RequestVote"]
     assert rv and all(R.rget(m, "mlastLogTerm") == 200 for t in rv for m, _c in t.messages
                       if R.rget(m, "mtype") == R.RVQ)
+
+
+_SIM_PROBE = r"""
+import hashlib, json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "raft.tla_amd"))
+sys.path.insert(0, sys.argv[1])
+import rmc
+from tests.convert import from_view
+c, _, _ = rmc.model_from_files(os.path.join(sys.argv[1], "tests", "golden", "models", "SmokeFixture.cfg"),
+                               builtin_raft=True, simulate=True)
+c.state_capacity = 1 << 12
+out = {}
+with rmc.Checker(c) as ck:
+    for mode in (rmc.SIM_WITHIN_CAPACITY, rmc.SIM_TRUNCATE, rmc.SIM_TLC):
+        r = ck.simulate(behaviours=4096, depth=100, smoke_k=2, seed=5, mode=mode)
+        views = ck.sim_replay(77, behaviours=4096, depth=100, smoke_k=2, seed=5, mode=mode)
+        h = hashlib.sha256(repr([from_view(v) for v in views]).encode()).hexdigest()
+        out[mode] = [r.steps, r.truncated, r.deadlocked, r.violated_inv, len(views), h]
+print(json.dumps(out))
+"""
+
+
+def test_wave_simulator_draws_the_thread_simulators_behaviours():
+    """k_wsimulate_w (one wave per behaviour: guards, apply, TypeOK and the
+    CONSTRAINT spread over the lanes, the bag moved one message per lane) walks
+    exactly the behaviours of k_wsimulate (one thread per behaviour, the serial
+    lane code) from the same seeds: equal step, truncation, deadlock and
+    violation tallies in every draw mode, and an identical replayed behaviour."""
+    import subprocess
+    import sys
+    res = []
+    for wsim in ("0", "1"):
+        env = dict(os.environ, RMC_WSIM=wsim, PYTHONHASHSEED="0")  # frozenset reprs in one order
+        p = subprocess.run([sys.executable, "-c", _SIM_PROBE, ROOT], env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        res.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    assert res[0] == res[1]
+    for mode, (steps, _t, _d, viol, nviews, _h) in res[1].items():
+        assert steps > 4096 * 50 and viol == 0 and nviews >= 2, (mode, res[1][mode])
