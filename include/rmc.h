@@ -276,7 +276,8 @@ int rmc_checkpoint(rmc_ctx* ctx, const char* path);
 int rmc_recover(rmc_ctx* ctx, const char* path);
 
 /* ---- codec and successor enumeration (tests, Java driver printing) -------
- * rmc_state_bytes: bytes of one packed state for this config.
+ * rmc_state_bytes: bytes of one stored state for this config (packed, or the
+ * wide layout's BFS record: 904 B compact or 5,080 B).
  * rmc_expand: run the SAME device successor code as the BFS on n caller
  * states (no dedup) and return every enabled lane's successor.  *n_out
  * receives the number of successors even if it exceeds cap. */

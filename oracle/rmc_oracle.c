@@ -34,8 +34,12 @@
 #include <time.h>
 
 #define OS 5  /* max servers */
-#define OL 4  /* max log length held (bounds are <= 3, +1 overshoot) */
-#define OK_ 9 /* max distinct messages held (bounds are <= 8, +1 overshoot) */
+#ifndef OL
+#define OL 4  /* max log length held (bounds are <= 3, +1 overshoot); liboracle_wide.so: 9 */
+#endif
+#ifndef OK_
+#define OK_ 9 /* max distinct messages held (bounds are <= 8, +1 overshoot); liboracle_wide.so: 13 */
+#endif
 
 enum { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 enum { NIL = 15 };

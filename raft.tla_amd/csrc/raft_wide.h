@@ -28,35 +28,49 @@ namespace wide {
 constexpr int WS = 5;    // servers held (= the packed layout's)
 constexpr int LW = 32;   // log entries per server (rmc.h RMC_WIDE_MAX_LOG)
 constexpr int KW = 64;   // distinct messages in the bag (rmc.h RMC_WIDE_MAX_MSGS)
+// The compact record (DESIGN.md "Wide state"): 16 log entries and 16 messages,
+// 904 bytes instead of 5,080 — enough for any state of a BFS bounded at depth
+// 17 or less (each step adds at most one log entry and one distinct message)
+// and for CONSTRAINTs of at most 16 entries and messages.
+constexpr int LWC = 16, KWC = 16;
 constexpr int TMAX = 255, CMAX = 255;  // largest term / count a field holds
 constexpr uint8_t NIL = 255;           // votedFor = Nil
 
 struct WEnt {
     uint8_t term, value;
 };
-// One message record (raft.tla:443-475): 8 + 2 LW bytes, fields a type does not use 0.
-struct alignas(8) WMsg {
+// One message record (raft.tla:443-475): 8 + 2 L bytes, fields a type does not use 0.
+template <int L>
+struct alignas(8) WMsgT {
     uint8_t type, term, src, dst;  // mtype, mterm, msource, mdest
     int8_t a;    // RVP mvoteGranted | AEQ mprevLogIndex (-1: Smokeraft.tla:35) | AEP msuccess
     uint8_t b;   // RVQ mlastLogTerm | AEQ mprevLogTerm | AEP mmatchIndex (unsigned: terms up to TMAX)
     uint8_t c;   // RVQ mlastLogIndex | AEQ mcommitIndex
     uint8_t n;   // AEQ Len(mentries) (<= 1) | RVP Len(mlog)
-    WEnt e[LW];  // AEQ mentries | RVP mlog (= log[i], raft.tla:259)
+    WEnt e[L];   // AEQ mentries | RVP mlog (= log[i], raft.tla:259)
 };
-static_assert(sizeof(WMsg) == 8 + 2 * LW && sizeof(WMsg) % 8 == 0, "WMsg layout");
-constexpr int WMWORDS = (int)(sizeof(WMsg) / 8);
-// The ten variables of raft.tla:31-74.
-struct WState {
+// The ten variables of raft.tla:31-74, with L log entries per server and K
+// distinct messages (kLW / kKW: the record's capacity, Msg: its message type).
+template <int L, int K>
+struct WStateT {
+    static constexpr int kLW = L, kKW = K;
+    typedef WMsgT<L> Msg;
     uint8_t ct[WS], st[WS], vf[WS], ci[WS], len[WS], vR[WS], vG[WS];
     uint8_t nmsg;
     uint8_t ni[WS][WS], mi[WS][WS];
     uint8_t pad[2];
-    WEnt log[WS][LW];
-    uint8_t cnt[KW];
-    WMsg msg[KW];
+    WEnt log[WS][L];
+    uint8_t cnt[K];
+    Msg msg[K];
 };
+typedef WMsgT<LW> WMsg;
+typedef WStateT<LW, KW> WState;     // the full record (5,080 B): simulation, rmc_expand, deep BFS
+typedef WStateT<LWC, KWC> WStateC;  // the compact record (904 B): BFS of depth <= 17
+static_assert(sizeof(WMsg) == 8 + 2 * LW && sizeof(WMsg) % 8 == 0, "WMsg layout");
+static_assert(sizeof(WState) == 5080 && sizeof(WStateC) == 904, "wide record sizes");
+static_assert(sizeof(WState) % 8 == 0 && sizeof(WStateC) % 8 == 0, "records are read as u64 words");
+constexpr int WMWORDS = (int)(sizeof(WMsg) / 8);
 constexpr int WWORDS = (int)(sizeof(WState) / 8);
-static_assert(sizeof(WState) % 8 == 0, "WState is read as u64 words");
 
 // Lane table with KW message lanes per bag family; WLMASK u64
 // words hold a mask over every lane of the largest shape (S = 5).
@@ -101,30 +115,35 @@ RMC_HD void wcopy(void* d, const void* s, int n) {
     const uint8_t* y = (const uint8_t*)s;
     for (int k = 0; k < n; ++k) x[k] = y[k];
 }
-RMC_HD void wcopy_state(WState& d, const WState& s) {
+template <class St>
+RMC_HD void wcopy_state(St& d, const St& s) {
     u64* x = reinterpret_cast<u64*>(&d);
     const u64* y = reinterpret_cast<const u64*>(&s);
-    for (int k = 0; k < WWORDS; ++k) x[k] = y[k];
+    for (int k = 0; k < (int)(sizeof(St) / 8); ++k) x[k] = y[k];
 }
 
 // Message order of the canonical bag: the record as WMWORDS u64 words compared in
 // turn (a total order; byte equality = record equality).  Host and device sort by it.
-RMC_HD int wmsg_cmp(const WMsg& a, const WMsg& b) {
+template <class Mg>
+RMC_HD int wmsg_cmp(const Mg& a, const Mg& b) {
     const u64* x = reinterpret_cast<const u64*>(&a);
     const u64* y = reinterpret_cast<const u64*>(&b);
-    for (int k = 0; k < WMWORDS; ++k)
+    for (int k = 0; k < (int)(sizeof(Mg) / 8); ++k)
         if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
     return 0;
 }
-RMC_HD void wmsg_zero(WMsg& m) {
+template <class Mg>
+RMC_HD void wmsg_zero(Mg& m) {
     u64* x = reinterpret_cast<u64*>(&m);
-    for (int k = 0; k < WMWORDS; ++k) x[k] = 0;
+    for (int k = 0; k < (int)(sizeof(Mg) / 8); ++k) x[k] = 0;
 }
 
 RMC_HD int wquorum(const WModel& M, unsigned set) { return 2 * __builtin_popcount(set) > M.S; }  // raft.tla:81
-RMC_HD int wlast_term(const WState& s, int i) { return s.len[i] ? s.log[i][s.len[i] - 1].term : 0; }  // :84
+template <class St>
+RMC_HD int wlast_term(const St& s, int i) { return s.len[i] ? s.log[i][s.len[i] - 1].term : 0; }  // :84
 
-RMC_HD void winit(const WModel& M, WState& s) {  // Init raft.tla:113-129
+template <class St>
+RMC_HD void winit(const WModel& M, St& s) {  // Init raft.tla:113-129
     wzero(&s, (int)sizeof s);
     for (int i = 0; i < M.S; ++i) {
         s.ct[i] = 1;
@@ -141,21 +160,24 @@ enum : int { W_OFF = 0, W_ON = 1, W_TERM = 2, W_LOG = 3, W_MSGS = 4, W_DUP = 5 }
 RMC_HD int woverflow_bits(int code) { return code >= W_TERM ? 1 << (code - W_TERM) : 0; }
 
 // Would Bag (+) SetToBag({m}) fit (without changing s)?
-RMC_HD int wbag_fits(const WState& s, const WMsg& m) {
+template <class St>
+RMC_HD int wbag_fits(const St& s, const typename St::Msg& m) {
     for (int k = 0; k < s.nmsg; ++k)
         if (wmsg_cmp(s.msg[k], m) == 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
-    return s.nmsg >= KW ? W_MSGS : W_ON;
+    return s.nmsg >= St::kKW ? W_MSGS : W_ON;
 }
 // Would Reply(r, s.msg[x]) (raft.tla:102-103: add the response, remove the
 // request) fit?  The capacity is that of the resulting bag: a request with count
 // 1 frees its slot (r never equals a request: the types differ).
-RMC_HD int wreply_fits(const WState& s, const WMsg& r, int x) {
+template <class St>
+RMC_HD int wreply_fits(const St& s, const typename St::Msg& r, int x) {
     for (int k = 0; k < s.nmsg; ++k)
         if (wmsg_cmp(s.msg[k], r) == 0) return s.cnt[k] >= CMAX ? W_DUP : W_ON;
-    return (s.nmsg >= KW && s.cnt[x] > 1) ? W_MSGS : W_ON;
+    return (s.nmsg >= St::kKW && s.cnt[x] > 1) ? W_MSGS : W_ON;
 }
 // Bag (+) SetToBag({m}) (raft.tla:88), kept sorted (call after wbag_fits).
-RMC_HD int wbag_add(WState& s, const WMsg& m) {
+template <class St>
+RMC_HD int wbag_add(St& s, const typename St::Msg& m) {
     int k = 0;
     for (; k < s.nmsg; ++k) {
         const int c = wmsg_cmp(s.msg[k], m);
@@ -166,7 +188,7 @@ RMC_HD int wbag_add(WState& s, const WMsg& m) {
         }
         if (c > 0) break;
     }
-    if (s.nmsg >= KW) return W_MSGS;
+    if (s.nmsg >= St::kKW) return W_MSGS;
     for (int q = s.nmsg; q > k; --q) {
         s.msg[q] = s.msg[q - 1];
         s.cnt[q] = s.cnt[q - 1];
@@ -178,7 +200,8 @@ RMC_HD int wbag_add(WState& s, const WMsg& m) {
 }
 // Bag (-) SetToBag({m}) (raft.tla:92) of the message in slot k: a count that
 // reaches 0 removes the key (Bags' (-)).
-RMC_HD void wbag_remove_at(WState& s, int k) {
+template <class St>
+RMC_HD void wbag_remove_at(St& s, int k) {
     if (--s.cnt[k]) return;
     for (int q = k; q + 1 < s.nmsg; ++q) {
         s.msg[q] = s.msg[q + 1];
@@ -193,10 +216,14 @@ RMC_HD void wbag_remove_at(WState& s, int k) {
 // whole wave on a record in LDS (WaveBag, rmc_wide.hip: every lane calls with
 // the same arguments, each compares / moves one message).
 struct SerialBag {
-    static RMC_HD int fits(const WState& s, const WMsg& m) { return wbag_fits(s, m); }
-    static RMC_HD int reply_fits(const WState& s, const WMsg& r, int x) { return wreply_fits(s, r, x); }
-    static RMC_HD int add(WState& s, const WMsg& m) { return wbag_add(s, m); }
-    static RMC_HD void remove_at(WState& s, int k) { wbag_remove_at(s, k); }
+    template <class St>
+    static RMC_HD int fits(const St& s, const typename St::Msg& m) { return wbag_fits(s, m); }
+    template <class St>
+    static RMC_HD int reply_fits(const St& s, const typename St::Msg& r, int x) { return wreply_fits(s, r, x); }
+    template <class St>
+    static RMC_HD int add(St& s, const typename St::Msg& m) { return wbag_add(s, m); }
+    template <class St>
+    static RMC_HD void remove_at(St& s, int k) { wbag_remove_at(s, k); }
 };
 
 // Lane `lane` on s (raft.tla:136-417, one action instance): W_OFF when the
@@ -210,8 +237,14 @@ struct SerialBag {
 // Scalar fields of *t are written from s (never read-modify-written), so a
 // wave whose lanes all apply the same lane to a shared record writes the same
 // values.
-template <class Bag = SerialBag>
-RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre = false) {
+template <class T>
+struct WSame {  // a non-deduced parameter type (t may be nullptr)
+    typedef T type;
+};
+template <class Bag = SerialBag, class St = WState>
+RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::type* t, bool pre = false) {
+    typedef typename St::Msg WMsg;
+    constexpr int LW = St::kLW;
     const int S = M.S;
     const int f = M.L.family(lane), x = lane - M.L.off[f];
     switch (f) {
@@ -461,7 +494,8 @@ RMC_HD int wlane(const WModel& M, const WState& s, int lane, WState* t, bool pre
 
 // CONSTRAINT of a successor the layout holds: 1 in the model, 0 filtered
 // (generated, neither stored nor checked).
-RMC_HD int win_model(const WModel& M, const WState& t) {
+template <class St>
+RMC_HD int win_model(const WModel& M, const St& t) {
     int ok = 1;
     for (int i = 0; i < M.S; ++i) {
         if (t.ct[i] > M.max_term) ok = 0;
@@ -475,7 +509,8 @@ RMC_HD int win_model(const WModel& M, const WState& t) {
 
 // ---- invariants (raft.tla:482-492; the config-5 and proof invariants as restated
 // in specs/MCraftBounded.tla) --------------------------------------------------------
-RMC_HD int wtype_ok(const WModel& M, const WState& s) {  // raft.tla:482-492
+template <class St>
+RMC_HD int wtype_ok(const WModel& M, const St& s) {  // raft.tla:482-492
     for (int i = 0; i < M.S; ++i) {
         if (s.st[i] > LEADER) return 0;
         if (s.vf[i] != NIL && s.vf[i] >= M.S) return 0;
@@ -486,20 +521,22 @@ RMC_HD int wtype_ok(const WModel& M, const WState& s) {  // raft.tla:482-492
             if (s.log[i][x].value >= M.V) return 0;
     }
     for (int q = 0; q < s.nmsg; ++q) {
-        const WMsg& m = s.msg[q];
+        const auto& m = s.msg[q];
         if (s.cnt[q] < 1 || m.src >= M.S || m.dst >= M.S) return 0;
         for (int x = 0; x < m.n; ++x)
             if (m.e[x].value >= M.V) return 0;
     }
     return 1;
 }
-RMC_HD int wcommitted_prefix_of(const WState& s, int j, int i) {  // IsPrefix(Committed(j), log[i])
+template <class St>
+RMC_HD int wcommitted_prefix_of(const St& s, int j, int i) {  // IsPrefix(Committed(j), log[i])
     const int c = s.ci[j] < s.len[j] ? s.ci[j] : s.len[j];
     if (s.len[i] < c) return 0;
     return wmemcmp(s.log[i], s.log[j], c * (int)sizeof(WEnt)) == 0;
 }
 // 0 = every named invariant holds, else the RMC_INV_* bit (index) of the first violated one + 1
-RMC_HD int wcheck_invariants(const WModel& M, const WState& s) {
+template <class St>
+RMC_HD int wcheck_invariants(const WModel& M, const St& s) {
     const int S = M.S, mask = M.inv_mask;
     if ((mask & 1) && !wtype_ok(M, s)) return 1;
     if (mask & 2)  // OneLeaderPerTerm (ElectionSafety restated, raft.tla:1124)
@@ -517,7 +554,7 @@ RMC_HD int wcheck_invariants(const WModel& M, const WState& s) {
             }
     if (mask & 8)  // MessagesInv raft.tla:941-946 (:910's m.dest read as m.mdest)
         for (int q = 0; q < s.nmsg; ++q) {
-            const WMsg& m = s.msg[q];
+            const auto& m = s.msg[q];
             const int src = m.src, dst = m.dst, cs = s.ct[src];
             if (m.term > cs) return 4;  // :934-935
             if (m.type == RVP && m.a && cs == s.ct[dst] && cs == m.term) {  // :903-910
@@ -593,25 +630,43 @@ RMC_HD u64 w_rand(u64& x) {  // splitmix64 stream (the simulators' draws)
 // than any action count (at most 83 actions), so every stride visits every
 // action.  en: the enabled lanes (bit l of en[l >> 6]); returns the lane, -1
 // if none is enabled.
+// Lanes [lo, hi) of the mask words: how many are set, and the k-th set one.
+template <int NC>
+RMC_HD u64 range_word(const u64 (&en)[NC], int c, int lo, int hi) {
+    const int b0 = 64 * c;
+    if (hi <= b0 || lo >= b0 + 64) return 0;
+    u64 m = en[c];
+    if (lo > b0) m &= ~0ull << (lo - b0);
+    if (hi < b0 + 64) m &= (1ull << (hi - b0)) - 1ull;
+    return m;
+}
 template <int NC>
 RMC_HD int tlc_draw(const u64 (&en)[NC], int nl, int o7, int o8, int o9, u64& rs) {
     auto on = [&](int lane) { return ((en[lane >> 6] >> (lane & 63)) & 1ull) != 0; };
     const int nact = o7 + 3;
     const u32 primes[8] = {89, 97, 101, 103, 107, 109, 113, 127};
     const u32 start = (u32)(w_rand(rs) % (u64)nact), stride = primes[w_rand(rs) & 7u];
-    for (int i = 0; i < nact; ++i) {
-        const int a = (int)((start + (u32)i * stride) % (u32)nact);
-        if (a < o7) {
-            if (on(a)) return a;
+    const u32 step = stride % (u32)nact;  // (start + i * stride) % nact, one addition per action
+    u32 a = start;
+    for (int i = 0; i < nact; ++i, a = a + step >= (u32)nact ? a + step - (u32)nact : a + step) {
+        if ((int)a < o7) {
+            if (on((int)a)) return (int)a;
             continue;
         }
-        const int f = a - o7, lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
+        const int f = (int)a - o7, lo = f == 0 ? o7 : f == 1 ? o8 : o9, hi = f == 0 ? o8 : f == 1 ? o9 : nl;
         u32 cnt = 0;
-        for (int lane = lo; lane < hi; ++lane) cnt += on(lane) ? 1u : 0u;
+        for (int c = 0; c < NC; ++c) cnt += (u32)__builtin_popcountll(range_word<NC>(en, c, lo, hi));
         if (!cnt) continue;
-        u32 k = (u32)(w_rand(rs) % (u64)cnt);
-        for (int lane = lo; lane < hi; ++lane)
-            if (on(lane) && k-- == 0) return lane;
+        u32 k = (u32)(w_rand(rs) % (u64)cnt);  // the k-th enabled lane of the family, in lane order
+        for (int c = 0; c < NC; ++c) {
+            u64 m = range_word<NC>(en, c, lo, hi);
+            const u32 p = (u32)__builtin_popcountll(m);
+            if (k < p) {
+                for (; k; --k) m &= m - 1;
+                return 64 * c + __builtin_ctzll(m);
+            }
+            k -= p;
+        }
     }
     return -1;
 }
@@ -639,11 +694,12 @@ RMC_HD int uniform_draw(const u64 (&en)[NC], const u64 (&excl)[NC], u64& rs) {
 // Fingerprint of a canonical record (every byte; salted like the packed one):
 // k the chained mix over the words, s the sum of smix over the chain's states
 // (raft_packed.h Fp: the second 32 bits the fingerprint set folds in).
-RMC_HD Fp wfp(const WState& s, u64 salt) {
+template <class St>
+RMC_HD Fp wfp(const St& s, u64 salt) {
     const u64* w = reinterpret_cast<const u64*>(&s);
     u64 h = 0x6A09E667F3BCC909ull ^ salt;
     u32 s2 = 0;
-    for (int k = 0; k < WWORDS; ++k) {
+    for (int k = 0; k < (int)(sizeof(St) / 8); ++k) {
         h = mix64(h ^ (w[k] + (u64)k * 0x9E3779B97F4A7C15ull));
         s2 += smix(h);
     }

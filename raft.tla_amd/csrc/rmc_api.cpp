@@ -452,7 +452,7 @@ const char* rmc_last_error(const rmc_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 size_t rmc_state_bytes(const rmc_config* cfg) {
     if (!cfg) return 0;
-    if (wide_wanted(*cfg)) return sizeof(rmc::wide::WState);
+    if (wide_wanted(*cfg)) return wide_record_bytes(*cfg);
     return (size_t)(2 * cfg->n_servers + kcap_for(cfg->max_msgs)) * 4u;
 }
 

@@ -182,6 +182,7 @@ void spill_free(rmc_ctx* c);
 int read_link(rmc_ctx* c, rmc::u64 idx, rmc::u64* parent, uint8_t* act);
 // the wide layout (rmc_wide.cpp)
 bool wide_wanted(const rmc_config& g);
+size_t wide_record_bytes(const rmc_config& g);  // the BFS store's record: compact or full
 int validate_wide(const rmc_config* c, std::string* why);
 int create_wide(rmc_ctx* c);
 void destroy_wide(rmc_ctx* c);

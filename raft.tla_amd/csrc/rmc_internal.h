@@ -162,7 +162,8 @@ hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int 
 // ---- the wide layout (raft_wide.h, rmc_wide.hip) ------------------------------------
 namespace wide {
 struct WideBufs {
-    WState* store;    // wide records; levels are contiguous ranges
+    void* store;      // wide records (WState, or WStateC when compact); levels are contiguous ranges
+    int compact;      // 1: the store holds compact records (raft_wide.h WStateC)
     u64* parent;      // parent index per state (~0 for initial states)
     uint8_t* act;     // lane that produced the state (255 for initial states)
     u64* table;       // fingerprint set (wfp keys), power-of-two slots
@@ -177,7 +178,7 @@ struct WSucc {
     u64 fp;
     WState state;
 };
-hipError_t launch_wseed(const WModel& M, const WideBufs& B, const WState* staged, u64 n, hipStream_t st);
+hipError_t launch_wseed(const WModel& M, const WideBufs& B, const void* staged, u64 n, hipStream_t st);  // B's layout
 hipError_t launch_wexpand(const WModel& M, const WideBufs& B, u64 lo, u64 hi, hipStream_t st);
 hipError_t launch_wlist(const WModel& M, const WState* in, u64 n, WSucc* out, u64 cap, unsigned long long* count,
                         u64 salt, hipStream_t st);

@@ -57,6 +57,21 @@ void fill_wide_model(rmc_ctx* c) {
 
 int wide_family(const rmc_ctx* c, int lane) { return lane == 255 ? -1 : c->WM.L.family(lane); }
 
+// The BFS store holds compact records (raft_wide.h WStateC: 16 log entries,
+// 16 messages) when no state of the run can need more: each field is either
+// bounded by a CONSTRAINT within the record (a successor beyond it is out of
+// the model anyway) or unbounded in a run of at most 17 levels (one step adds
+// at most one log entry and one distinct message).  RMC_WIDE_COMPACT=0/1
+// overrides (A/B, tests).
+static bool wide_compact(const rmc_config& g) {
+    if (const char* e = getenv("RMC_WIDE_COMPACT")) return atoi(e) != 0;
+    const int steps = g.max_depth > 0 ? g.max_depth - 1 : 1 << 30;
+    const bool logs = ((g.flags & RMC_FLAG_UNBOUNDED_LOG) == 0 && g.max_log_len <= LWC) || steps <= LWC;
+    const bool msgs = ((g.flags & RMC_FLAG_UNBOUNDED_MSGS) == 0 && g.max_msgs <= KWC) || steps <= KWC;
+    return logs && msgs;
+}
+size_t wide_record_bytes(const rmc_config& g) { return wide_compact(g) ? sizeof(WStateC) : sizeof(WState); }
+
 // ---- codec ----------------------------------------------------------------------
 int encode_wide(const rmc_ctx* c, const rmc_state_view& v, WState* out, std::string* why) {
     const int S = c->WM.S;
@@ -156,7 +171,8 @@ int encode_wide(const rmc_ctx* c, const rmc_state_view& v, WState* out, std::str
     return 0;
 }
 
-void decode_wide(const rmc_ctx* c, const WState& s, rmc_state_view* v) {
+template <class St>
+void decode_wide(const rmc_ctx* c, const St& s, rmc_state_view* v) {
     const int S = c->WM.S;
     memset(v, 0, sizeof *v);
     v->n_servers = S;
@@ -179,7 +195,7 @@ void decode_wide(const rmc_ctx* c, const WState& s, rmc_state_view* v) {
     }
     v->n_msgs = s.nmsg;
     for (int q = 0; q < s.nmsg; ++q) {
-        const WMsg& w = s.msg[q];
+        const auto& w = s.msg[q];
         rmc_msg_view& m = v->msgs[q];
         m.mtype = w.type;
         m.mterm = w.term;
@@ -208,7 +224,9 @@ void decode_wide(const rmc_ctx* c, const WState& s, rmc_state_view* v) {
 // ---- context ----------------------------------------------------------------------
 int create_wide(rmc_ctx* c) {
     fill_wide_model(c);
-    const u64 per_state = sizeof(WState) + 8 + 1;
+    const bool compact = wide_compact(c->cfg);
+    const u64 rec = compact ? sizeof(WStateC) : sizeof(WState);
+    const u64 per_state = rec + 8 + 1;
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
     const u64 budget = (u64)((double)fr * 0.80);
@@ -221,7 +239,8 @@ int create_wide(rmc_ctx* c) {
     B = WideBufs{};
     B.cap = cap;
     B.tmask = slots - 1;
-    if (hipMalloc(&B.store, cap * sizeof(WState)) != hipSuccess || hipMalloc(&B.parent, cap * 8) != hipSuccess ||
+    B.compact = compact ? 1 : 0;
+    if (hipMalloc(&B.store, cap * rec) != hipSuccess || hipMalloc(&B.parent, cap * 8) != hipSuccess ||
         hipMalloc(&B.act, cap) != hipSuccess || hipMalloc(&B.table, slots * 8) != hipSuccess ||
         hipMalloc(&B.ctr, sizeof(Counters)) != hipSuccess || hipMalloc(&c->w_staged, sizeof(WState)) != hipSuccess)
         return fail(c, RMC_E_NOMEM, "device allocation failed (wide layout, capacity " + std::to_string(cap) + " states)");
@@ -259,8 +278,12 @@ int run_bfs_wide(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->h_ctr->count = 0;
     if (int rc = reset_counters(c, false)) return rc;
     WState init;
+    WStateC initc;
     winit(c->WM, init);
-    HIPCHK(c, hipMemcpyAsync(c->w_staged, &init, sizeof init, hipMemcpyHostToDevice, c->st));
+    winit(c->WM, initc);
+    if (B.compact) HIPCHK(c, hipMemcpyAsync(c->w_staged, &initc, sizeof initc, hipMemcpyHostToDevice, c->st));
+    else HIPCHK(c, hipMemcpyAsync(c->w_staged, &init, sizeof init, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));  // (the staging copies live on this stack frame)
     HIPCHK(c, launch_wseed(c->WM, B, c->w_staged, 1, c->st));
     if (int rc = read_counters(c)) return rc;
     c->res.generated = 1;
@@ -357,9 +380,15 @@ int trace_wide(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* i
     std::reverse(acts.begin(), acts.end());
     *len = chain.size();
     for (size_t q = 0; q < chain.size() && q < cap; ++q) {
-        WState s;
-        HIPCHK(c, hipMemcpy(&s, c->WB.store + chain[q], sizeof s, hipMemcpyDeviceToHost));
-        if (states) decode_wide(c, s, &states[q]);
+        if (c->WB.compact) {
+            WStateC s;
+            HIPCHK(c, hipMemcpy(&s, static_cast<const WStateC*>(c->WB.store) + chain[q], sizeof s, hipMemcpyDeviceToHost));
+            if (states) decode_wide(c, s, &states[q]);
+        } else {
+            WState s;
+            HIPCHK(c, hipMemcpy(&s, static_cast<const WState*>(c->WB.store) + chain[q], sizeof s, hipMemcpyDeviceToHost));
+            if (states) decode_wide(c, s, &states[q]);
+        }
         if (families) families[q] = wide_family(c, acts[q]);
         if (instances) instances[q] = acts[q] == 255 ? -1 : acts[q];
     }

@@ -40,9 +40,10 @@ __device__ __forceinline__ u64 w_wave_sum(u64 v) {
 
 // Store a new state (slot allocated by the caller) with its trace link and the
 // fused invariant check.
-__device__ __forceinline__ void w_store(const WModel& M, const WideBufs& B, u64 ni, const WState& t, u64 parent,
+template <class St>
+__device__ __forceinline__ void w_store(const WModel& M, const WideBufs& B, u64 ni, const St& t, u64 parent,
                                         int lane) {
-    wcopy_state(B.store[ni], t);
+    wcopy_state(static_cast<St*>(B.store)[ni], t);
     B.parent[ni] = parent;
     B.act[ni] = (uint8_t)lane;
     const int v = wcheck_invariants(M, t);
@@ -50,7 +51,8 @@ __device__ __forceinline__ void w_store(const WModel& M, const WideBufs& B, u64 
 }
 
 // Init (raft.tla:125-129) or SmokeInit's states: n staged records.
-__global__ __launch_bounds__(256) void k_wseed(const WModel M, const WideBufs B, const WState* staged, u64 n) {
+template <class St>
+__global__ __launch_bounds__(256) void k_wseed(const WModel M, const WideBufs B, const St* staged, u64 n) {
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n; t += (u64)gridDim.x * 256ull) {
         if (!w_insert(B.table, B.tmask, wfp(staged[t], B.salt), &B.ctr->table_full)) continue;
         const u64 ni = atomicAdd((unsigned long long*)&B.ctr->count, 1ull);
@@ -66,13 +68,14 @@ __global__ __launch_bounds__(256) void k_wseed(const WModel M, const WideBufs B,
 // outside the CONSTRAINT count as generated and are dropped; a successor the
 // layout cannot hold in a field no CONSTRAINT bounds stops the search
 // (Counters.overflow bits 8-11, the field).
+template <class St>
 __global__ __launch_bounds__(256) void k_wexpand(const WModel M, const WideBufs B, u64 lo, u64 hi) {
     u64 gen = 0, probes = 0;
     u32 bad = 0;
     const int nl = M.L.off[10];
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
-        WState s, t;
-        wcopy_state(s, B.store[i]);
+        St s, t;
+        wcopy_state(s, static_cast<const St*>(B.store)[i]);
         u32 g = 0;
         for (int lane = 0; lane < nl; ++lane) {
             const int r = wlane(M, s, lane, &t);
@@ -424,14 +427,22 @@ static unsigned grid_for(u64 n, u64 threads, u64 maxg) {
     return (unsigned)(b < maxg ? (b ? b : 1) : maxg);
 }
 
-hipError_t launch_wseed(const WModel& M, const WideBufs& B, const WState* staged, u64 n, hipStream_t st) {
+hipError_t launch_wseed(const WModel& M, const WideBufs& B, const void* staged, u64 n, hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_wseed, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, M, B, staged, n);
+    if (B.compact)
+        hipLaunchKernelGGL(k_wseed<WStateC>, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, M, B,
+                           static_cast<const WStateC*>(staged), n);
+    else
+        hipLaunchKernelGGL(k_wseed<WState>, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, M, B,
+                           static_cast<const WState*>(staged), n);
     return hipGetLastError();
 }
 hipError_t launch_wexpand(const WModel& M, const WideBufs& B, u64 lo, u64 hi, hipStream_t st) {
     if (hi <= lo) return hipSuccess;
-    hipLaunchKernelGGL(k_wexpand, dim3(grid_for(hi - lo, 256, 4096)), dim3(256), 0, st, M, B, lo, hi);
+    if (B.compact)
+        hipLaunchKernelGGL(k_wexpand<WStateC>, dim3(grid_for(hi - lo, 256, 4096)), dim3(256), 0, st, M, B, lo, hi);
+    else
+        hipLaunchKernelGGL(k_wexpand<WState>, dim3(grid_for(hi - lo, 256, 4096)), dim3(256), 0, st, M, B, lo, hi);
     return hipGetLastError();
 }
 hipError_t launch_wlist(const WModel& M, const WState* in, u64 n, WSucc* out, u64 cap, unsigned long long* count,

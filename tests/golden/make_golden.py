@@ -75,6 +75,14 @@ CONFIGS = {
     # MCraftBounded.cfg at full size (78 M states, ~2 min on 8 threads, ~10 GB)
     "bounded_full": (3, 2, 2, 1, 2, 1, 0, 1, 0, 0),
 }
+# The reference's own MCraft.cfg (no CONSTRAINT: tests/golden/models/MCunbounded.cfg)
+# under a depth bound, on the oracle build holding logs of 8 entries and 12
+# messages (liboracle_wide.so): terms and counts unbounded (-1); Len(log) <= 8 and
+# 12 messages never bind within 11 steps (each step adds at most one entry and
+# one distinct message), so these are the unconstrained spec's levels.
+WIDE_CONFIGS = {
+    "mcraft_shipped_d12": (3, 2, -1, 8, 12, -1, 0, 1, 0, 12),
+}
 
 
 def main(only=None):
@@ -82,11 +90,12 @@ def main(only=None):
     names every entry is regenerated (bounded_full included)."""
     path = os.path.join(ROOT, "tests", "golden", "oracle_levels.json")
     out = json.load(open(path)) if only else {}
-    for name, (S, V, mt, ml, mm, md, bug, inv, sym, lv) in CONFIGS.items():
+    todo = [(n, c, False) for n, c in CONFIGS.items()] + [(n, c, True) for n, c in WIDE_CONFIGS.items()]
+    for name, (S, V, mt, ml, mm, md, bug, inv, sym, lv), wide in todo:
         if only and name not in only:
             continue
         r, ln, lg = oracle_c.bfs(S, V, mt, ml, mm, md, bug=bug, inv=inv, sym=sym, threads=8,
-                                 max_levels=lv, capacity=1 << 27)
+                                 max_levels=lv, capacity=1 << (26 if wide else 27), wide=wide)
         out[name] = dict(params=dict(n_servers=S, n_values=V, max_term=mt, max_log_len=ml,
                                      max_msgs=mm, max_dup=md, bug_quorum=bug, invariants=inv,
                                      symmetry=sym, max_depth=lv),

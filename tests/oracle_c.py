@@ -5,6 +5,7 @@ import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+LIB_WIDE = os.path.join(ROOT, "oracle", "_build", "liboracle_wide.so")  # logs of 8, 12 messages
 
 
 class OrcResult(C.Structure):
@@ -13,28 +14,29 @@ class OrcResult(C.Structure):
                 ("overflow", C.c_int32), ("violation_index", C.c_uint64), ("seconds", C.c_double)]
 
 
-_lib = None
+_libs = {}
 
 
-def load():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def load(wide=False):
+    path = LIB_WIDE if wide else LIB
+    if path not in _libs:
+        if not os.path.exists(path):
             subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                            capture_output=True)
-        lib = C.CDLL(LIB)
+        lib = C.CDLL(path)
         lib.orc_bfs.argtypes = [C.c_int] * 11 + [C.c_uint64, C.POINTER(OrcResult),
                                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                                  C.c_int]
         lib.orc_bfs.restype = C.c_int
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
 def bfs(S, V, max_term, max_log, max_msgs, max_dup, bug=0, inv=1, sym=0, threads=8,
-        max_levels=0, capacity=1 << 24):
-    """Run the C oracle; returns (OrcResult, level_new list, level_gen list)."""
-    lib = load()
+        max_levels=0, capacity=1 << 24, wide=False):
+    """Run the C oracle; returns (OrcResult, level_new list, level_gen list).
+    wide: the build holding logs of 8 entries and 12 messages."""
+    lib = load(wide)
     r = OrcResult()
     ln = (C.c_uint64 * 512)()
     lg = (C.c_uint64 * 512)()

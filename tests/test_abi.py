@@ -47,6 +47,30 @@ def test_version_and_state_bytes():
     assert lib.rmc_state_bytes(C.byref(cfg)) == (2 * 5 + 8) * 4
 
 
+def test_wide_bfs_record_is_sized_from_the_run(monkeypatch):
+    """the wide BFS stores compact 904-B records (16 log
+    entries, 16 messages) when no state of the run can need more — a CONSTRAINT
+    within them, or at most 16 steps of an unbounded field (one step adds at
+    most one log entry and one distinct message) — else the full 5,080 B."""
+    lib = rmc.native()
+    unb = rmc.FLAG_UNBOUNDED_TERM | rmc.FLAG_UNBOUNDED_LOG | rmc.FLAG_UNBOUNDED_MSGS | rmc.FLAG_UNBOUNDED_DUP
+
+    def nbytes(**kw):
+        flags = kw.pop("flags", 0)
+        cfg = rmc.make_config(**kw)
+        cfg.flags |= flags
+        return lib.rmc_state_bytes(C.byref(cfg))
+    shipped = dict(max_term=255, max_log_len=32, max_msgs=64, max_dup=255, flags=unb)  # MCraft.cfg as shipped
+    assert nbytes(max_depth=17, **shipped) == 904
+    assert nbytes(max_depth=18, **shipped) == 5080
+    assert nbytes(max_depth=0, **shipped) == 5080
+    assert nbytes(max_log_len=16, max_msgs=16) == 904     # bounded within the compact record
+    assert nbytes(max_log_len=16, max_msgs=17) == 5080
+    assert nbytes(max_log_len=17, max_msgs=9, max_depth=17) == 904  # bounded beyond it, but 16 steps
+    monkeypatch.setenv("RMC_WIDE_COMPACT", "0")
+    assert nbytes(max_depth=8, **shipped) == 5080
+
+
 def test_create_validates_config():
     lib = rmc.native()
     ctx = C.c_void_p()

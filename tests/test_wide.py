@@ -38,13 +38,20 @@ def cfg_from(p, capacity=1 << 20):
                            max_depth=p["max_depth"], state_capacity=capacity)
 
 
+@pytest.fixture(params=["full", "compact"])
+def wide_record(request, monkeypatch):
+    """The BFS store's record: full (5,080 B) or compact (904 B, WStateC)."""
+    monkeypatch.setenv("RMC_WIDE_COMPACT", "1" if request.param == "compact" else "0")
+    return 904 if request.param == "compact" else 5080
+
+
 @pytest.mark.parametrize("name", ["tiny2", "tiny2_v2", "small", "s4_prefix10", "msgs5_dup2_prefix9"])
-def test_wide_layout_matches_oracle_levels(name, force_wide):
-    """The wide layout on packed-size golden models: every per-level count,
-    distinct, generated and depth equal the oracle's."""
+def test_wide_layout_matches_oracle_levels(name, force_wide, wide_record):
+    """The wide layout (both records) on packed-size golden models: every
+    per-level count, distinct, generated and depth equal the oracle's."""
     g = GOLDEN[name]
     with rmc.Checker(cfg_from(g["params"], capacity=max(1 << 20, int(g["distinct"] * 1.25)))) as ck:
-        assert rmc.native().rmc_state_bytes(ck.cfg) == 5080
+        assert rmc.native().rmc_state_bytes(ck.cfg) == wide_record
         r = ck.run()
         levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
     assert levels == g["level_new"]
@@ -53,7 +60,7 @@ def test_wide_layout_matches_oracle_levels(name, force_wide):
 
 
 @pytest.mark.parametrize("name", ["bug_one_leader", "bug_log_matching", "messages_small"])
-def test_wide_layout_violation_and_trace(name, force_wide):
+def test_wide_layout_violation_and_trace(name, force_wide, wide_record):
     g = GOLDEN[name]
     p = g["params"]
     with rmc.Checker(cfg_from(p, capacity=int(g["distinct"] * 1.25) + (1 << 16))) as ck:  # 5-KB records
@@ -78,7 +85,8 @@ def test_reference_mcraft_cfg_under_a_depth_bound():
     for depth in (6, 7, 8):
         c = rmc.Config.from_buffer_copy(base)
         c.max_depth = depth
-        c.state_capacity = 1 << 18  # 5 KB records: 56,761 states at depth 8
+        c.state_capacity = 1 << 18  # 56,761 states at depth 8
+        assert rmc.native().rmc_state_bytes(c) == 904  # 7 steps: the compact record holds every state
         with rmc.Checker(c) as ck:
             r = ck.run()
             levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
@@ -88,6 +96,33 @@ def test_reference_mcraft_cfg_under_a_depth_bound():
         assert (r.distinct, r.generated, r.depth, r.left_on_queue) == (ref.distinct, ref.generated, ref.depth,
                                                                       ref.left_on_queue), depth
         assert levels == ln, depth
+
+
+@pytest.mark.parametrize("depth,record", [(12, "compact"), (10, "full")])
+def test_reference_mcraft_cfg_deeper_on_the_record_sized_from_the_run(depth, record, monkeypatch):
+    """MCraft.cfg as shipped (no CONSTRAINT) to depth 12 —
+    24.6 M states, beyond the 8 levels the full 5-KB record was tested to — on
+    the compact 904-B record the front-end picks for depth <= 17, and on the full
+    record at depth 10: every per-level count, distinct, generated and the queue
+    equal the C oracle build holding logs of 8 and 12 messages
+    (tests/golden/oracle_levels.json mcraft_shipped_d12).  One GPU completes
+    depth 13 on the compact record (110.9 M states; profiles/r05/wide5/)."""
+    g = GOLDEN["mcraft_shipped_d12"]
+    monkeypatch.setenv("RMC_WIDE_COMPACT", "1" if record == "compact" else "0")
+    cfgp = os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg")
+    c, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, depth_bounded=True)
+    c.max_depth = depth
+    c.state_capacity = int(sum(g["level_new"][:depth]) * 1.1) + 4096
+    assert rmc.native().rmc_state_bytes(c) == (904 if record == "compact" else 5080)
+    with rmc.Checker(c) as ck:
+        r = ck.run()
+        levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+    assert levels == g["level_new"][:depth]
+    assert r.distinct == sum(g["level_new"][:depth]) and r.depth == depth
+    assert r.left_on_queue == g["level_new"][depth - 1]
+    assert r.generated == sum(g["level_generated"][:depth])
+    if depth == 12:
+        assert (r.distinct, r.generated) == (g["distinct"], g["generated"])
 
 
 def _walk_states(model, n, depth, seed):
