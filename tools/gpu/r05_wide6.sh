@@ -12,5 +12,5 @@ timeout -k 10 200 python -u tools/mcraft_shipped.py 13 auto > $O/shipped_d13_aut
 tail -1 $O/shipped_d13_auto.jsonl
 timeout -k 10 200 python -u tools/mcraft_shipped.py 12 full > $O/shipped_d12_full.jsonl 2> $O/s12.err || { tail -5 $O/s12.err; exit 1; }
 tail -1 $O/shipped_d12_full.jsonl
-timeout -k 10 200 raft.tla_amd/bin/rmc-tlc -depth 13 tests/golden/models/MCunbounded.tla > $O/cli_mcraft_shipped_depth13.txt 2>&1; echo "cli rc $?"
+timeout -k 10 200 raft.tla_amd/bin/rmc-tlc -builtin-raft -depth 13 tests/golden/models/MCunbounded.tla > $O/cli_mcraft_shipped_depth13.txt 2>&1; echo "cli rc $?"
 tail -6 $O/cli_mcraft_shipped_depth13.txt
