@@ -461,6 +461,11 @@ def main(argv=None):
             "probe_rate_per_s": NP / ks if ks > 0 else 0.0,
             "probe_ceiling_per_s": r_max,
             "frac_of_probe_ceiling": (NP / ks / r_max) if (ks > 0 and r_max) else None,
+            # the kernel's whole HBM traffic (probes, CAS write-backs of new keys, frontier
+            # reads, state stores: PMC) per second against the random-granule ceiling —
+            # the measured random 8-B load rate x the 64-B granule each one moves
+            "traffic_frac_of_random_ceiling": (traffic * nlaunch / ks / (r_max * 64.0))
+                                              if (traffic and ks > 0 and r_max) else None,
         },
     }
     if sharded:
