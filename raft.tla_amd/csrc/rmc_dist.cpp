@@ -108,8 +108,14 @@ int xwait(rmc_ctx* c, hipEvent_t ev) {
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady)
             return fail(c, RMC_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e) + " at " + where(c));
-        if ((spin & 63) == 0 && now_s() - t0 > D.timeout_s) return deadline_fail(c, "a wait on the exchange");
-        if (spin > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if ((spin & 63) == 0) {
+            const double dt = now_s() - t0;
+            if (dt > D.timeout_s) return deadline_fail(c, "a wait on the exchange");
+            // a level's expansion takes up to tens of ms: poll without sleeping for
+            // the first 100 ms (a 20-us sleep wakes 50-80 us late, once per wait),
+            // then gently (a stalled peer)
+            if (dt > 0.1) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
     }
     D.wait_seconds += now_s() - t0;
     return 0;
