@@ -1,11 +1,14 @@
-// Host model of commuting-diamond probe elimination.
+// Measurement tool derived from tests/native/diamond_model.cpp: of the probes left
+// after commuting diamonds, how many two candidate same-parent rules would remove
+// (A: a Receive equal to Drop of its message; B: an UpdateTerm equal to an earlier
+// slot one).  // Host model of commuting-diamond probe elimination.
 //
 // A BFS on the packed encoding (raft_packed.h, the kernels' own lane code),
 // recording for every stored state t its first discoverer: parent s and lane
 // a, t = a(s).  When t is expanded, a successor b(t) need not be probed when
 //   (1) b precedes a in a fixed, state-independent order of action instances
-//       (DropMessage first, then by family; the lane index for server actions,
-//       the message for bag actions);
+//       (family, then the lane index for server actions, the message for bag
+//       actions);
 //   (2) a and b are independent: they read/write different server words
 //       (a lane touches at most one: Restart..AppendEntries their server i,
 //       Receive the message's mdest, Duplicate/Drop none) and touch disjoint
@@ -54,11 +57,12 @@ struct Model {
         while (f < 9 && lane >= P.off[f + 1]) ++f;
         return f;
     }
+    u64 last_slot = 0;
     bool insert(u64 key) {
         key = key ? key : 1;
         for (u64 s = key & mask;; s = (s + 1) & mask) {
-            if (table[s] == key) return false;
-            if (!table[s]) { table[s] = key; return true; }
+            if (table[s] == key) { last_slot = s; return false; }
+            if (!table[s]) { table[s] = key; last_slot = s; return true; }
         }
     }
     // the server word a lane reads/writes (-1: none) and the message it acts on
@@ -73,10 +77,10 @@ struct Model {
             default: return -1;
         }
     }
-    u64 order_key(int lane, u32 msg) const {  // DropMessage first, then families 0-8
+    int rank[10] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9};  // family order of the diamond rule (argv 9)
+    u64 order_key(int lane, u32 msg) const {
         const int f = family(lane);
-        const u64 rank = f == 9 ? 0 : (u64)f + 1;
-        return (rank << 40) | (f < 7 ? (u64)lane : (u64)(msg & MSG_MASK));
+        return ((u64)rank[f] << 40) | (f < 7 ? (u64)lane : (u64)(msg & MSG_MASK));
     }
     static int cnt_of(const u32 (&m)[K], u32 msg) {
         for (int q = 0; q < K; ++q)
@@ -120,7 +124,15 @@ struct Model {
         return true;
     }
 
-    struct Out { std::vector<u64> level_new; u64 generated = 0, probes = 0, skipped = 0, mismatch = 0; };
+    struct Out {
+        std::vector<u64> level_new;
+        u64 generated = 0, probes = 0, skipped = 0, mismatch = 0;
+        u64 hits = 0, ruleA = 0, ruleA_hit = 0, ruleB = 0, ruleB_hit = 0;
+        u64 hit_rel[4] = {0, 0, 0, 0};  // found state's level - parent level + 2 (0: <= -2)
+        u64 hit_fam[10] = {0}, probe_fam[10] = {0};
+    };
+    std::vector<u64> slot_idx;  // table slot -> state index
+    std::vector<int> lvl_of;    // state index -> level
 
     Out bfs(int max_levels, bool skip, u64 cap) {
         Out o;
@@ -128,12 +140,16 @@ struct Model {
         u64 slots = 1;
         while (slots < 2 * cap) slots <<= 1;
         table.assign(slots, 0);
+        slot_idx.assign(slots, 0);
+        lvl_of.clear();
         mask = slots - 1;
         u64 w0[S];
         u32 m0[K];
         for (int i = 0; i < S; ++i) w0[i] = 1ull | ((u64)NILV << VF_SH);
         for (int q = 0; q < K; ++q) m0[q] = 0;
         insert(state_fp<S, K>(w0, m0).k);
+        slot_idx[last_slot] = 0;
+        lvl_of.push_back(1);
         W.insert(W.end(), w0, w0 + S);
         M.insert(M.end(), m0, m0 + K);
         act.push_back(255);
@@ -187,16 +203,42 @@ struct Model {
                         int nmb = 0;
                         Fp h2{0, 0};
                         delta_fp<S, K>(w, m, h0, d, P, &h2, &nmb);
-                        if (diamond_skip<S, K>(m, lane, d, nmb, dm, P) != sk) ++o.mismatch;
-                        // the lane-descriptor form the sorted kernels use decides the same
-                        if (diamond_skip_desc<S, K>(m, lane, P.ldesc[lane], d, nmb, dm) != sk) ++o.mismatch;
+                        (void)nmb;
                     }
                     if (sk) {
                         ++o.skipped;
                         if (skip) continue;
                     }
                     ++o.probes;
-                    if (!insert(h.k)) continue;
+                    const int fam = family(lane);
+                    // rule A: a Receive whose successor is Drop(k)'s (no word change, no add, slot k removed)
+                    bool rA = false, rB = false;
+                    if (fam == 7) {
+                        const int k = lane - P.off[7];
+                        const bool noword = d.srv < 0 || d.w_new == selw<S>(w, d.srv);
+                        rA = d.rm == k && !d.has_add && noword;
+                        // rule B: an UpdateTerm (word change only) equal to an earlier slot's UpdateTerm
+                        if (d.rm < 0 && !d.has_add && d.srv >= 0)
+                            for (int k2 = 0; k2 < k; ++k2) {
+                                Delta d2;
+                                lane_delta<S, K>(w, m, P.off[7] + k2, P, d2);
+                                if (d2.en && d2.rm < 0 && !d2.has_add && d2.srv == d.srv && d2.w_new == d.w_new) rB = true;
+                            }
+                    }
+                    const bool fresh = insert(h.k);
+                    ++o.probe_fam[fam];
+                    if (!fresh) {
+                        ++o.hits;
+                        ++o.hit_fam[fam];
+                        const int rel = lvl_of[slot_idx[last_slot]] - lv;  // parent at level lv
+                        ++o.hit_rel[rel <= -2 ? 0 : rel + 2 > 3 ? 3 : rel + 2];
+                    } else {
+                        slot_idx[last_slot] = act.size();
+                        lvl_of.push_back(lv + 1);
+                    }
+                    if (rA) { ++o.ruleA; if (!fresh) ++o.ruleA_hit; }
+                    if (rB) { ++o.ruleB; if (!fresh) ++o.ruleB_hit; }
+                    if (!fresh) continue;
                     u64 wo[S];
                     u32 mo[K];
                     materialise<S, K>(w, m, d, wo, mo);
@@ -204,7 +246,6 @@ struct Model {
                     M.insert(M.end(), mo, mo + K);
                     act.push_back((uint8_t)lane);
                     Foot f{};
-                    const int fam = family(lane);
                     if (fam >= 7) {
                         f.has_act = 1;
                         f.m_act = selm<K>(m, lane - P.off[fam]) & MSG_MASK;
@@ -224,27 +265,29 @@ struct Model {
     }
 };
 
+static const char* g_rank = nullptr;
 template <int S, int K>
 int run(int V, int mt, int ml, int mm, int md, int levels, u64 cap) {
     Model<S, K> X;
+    if (g_rank)
+        for (int f = 0; f < 10 && g_rank[f]; ++f) X.rank[g_rank[f] - '0'] = f;  // "9012345678": Drop first
     X.P.V = V; X.P.max_term = mt; X.P.max_log = ml; X.P.max_msgs = mm; X.P.max_dup = md; X.P.diamond = 1;
     for (int f = 0; f <= 10; ++f) X.P.off[f] = Lanes<S, K>::off(f);
     fill_lane_desc(X.P, S);
-    auto a = X.bfs(levels, false, cap);
-    auto b = X.bfs(levels, true, cap);
-    u64 da = 0, db = 0;
+    auto a = X.bfs(levels, true, cap);
+    u64 da = 0;
     for (u64 x : a.level_new) da += x;
-    for (u64 x : b.level_new) db += x;
-    printf("{\"S\": %d, \"V\": %d, \"max_term\": %d, \"max_log\": %d, \"max_msgs\": %d, \"max_dup\": %d, "
-           "\"levels\": %zu, \"distinct\": %llu, \"generated\": %llu, \"probes\": %llu, \"skippable\": %llu, "
-           "\"skippable_frac\": %.4f, \"with_skip\": {\"distinct\": %llu, \"generated\": %llu, \"probes\": %llu, "
-           "\"levels\": %zu}, \"same_levels\": %s, \"kernel_rule_mismatches\": %llu}\n",
-           S, V, mt, ml, mm, md, a.level_new.size(), (unsigned long long)da, (unsigned long long)a.generated,
-           (unsigned long long)a.probes, (unsigned long long)a.skipped, (double)a.skipped / (double)a.probes,
-           (unsigned long long)db, (unsigned long long)b.generated, (unsigned long long)b.probes,
-           b.level_new.size(), a.level_new == b.level_new && a.generated == b.generated ? "true" : "false",
-           (unsigned long long)(a.mismatch + b.mismatch));
-    return a.level_new == b.level_new && a.generated == b.generated && !a.mismatch && !b.mismatch ? 0 : 1;
+    printf("hit level - parent level: <=-2 %llu, -1 %llu, 0 %llu, +1 %llu\n", (unsigned long long)a.hit_rel[0],
+           (unsigned long long)a.hit_rel[1], (unsigned long long)a.hit_rel[2], (unsigned long long)a.hit_rel[3]);
+    for (int f = 0; f < 10; ++f)
+        printf("family %d: probes %llu hits %llu\n", f, (unsigned long long)a.probe_fam[f], (unsigned long long)a.hit_fam[f]);
+    printf("skipped by diamonds %llu\n", (unsigned long long)a.skipped);
+    printf("{\"distinct\": %llu, \"generated\": %llu, \"probes\": %llu, \"hits\": %llu, \"ruleA\": %llu, "
+           "\"ruleA_hit\": %llu, \"ruleB\": %llu, \"ruleB_hit\": %llu}\n",
+           (unsigned long long)da, (unsigned long long)a.generated, (unsigned long long)a.probes,
+           (unsigned long long)a.hits, (unsigned long long)a.ruleA, (unsigned long long)a.ruleA_hit,
+           (unsigned long long)a.ruleB, (unsigned long long)a.ruleB_hit);
+    return 0;
 }
 
 }  // namespace
@@ -257,6 +300,7 @@ int main(int argc, char** argv) {
     const int S = atoi(argv[1]), V = atoi(argv[2]), mt = atoi(argv[3]), ml = atoi(argv[4]), mm = atoi(argv[5]),
               md = atoi(argv[6]), lv = atoi(argv[7]);
     const u64 cap = argc > 8 ? strtoull(argv[8], nullptr, 10) : (1ull << 26);
+    if (argc > 9) g_rank = argv[9];
     const bool k8 = mm > 4;
     if (S == 2) return k8 ? run<2, 8>(V, mt, ml, mm, md, lv, cap) : run<2, 4>(V, mt, ml, mm, md, lv, cap);
     if (S == 3) return k8 ? run<3, 8>(V, mt, ml, mm, md, lv, cap) : run<3, 4>(V, mt, ml, mm, md, lv, cap);
