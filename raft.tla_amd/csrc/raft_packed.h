@@ -925,8 +925,13 @@ RMC_HD u32 diamond_order(int f, int lane, u32 msg) {
 struct Diamond {
     u32 ord;     // a's instance order key; 0 = no skipping from this state
     u32 k0, k1;  // a's messages (sentinels when absent; never equal to a 30-bit message)
-    u32 sd;      // a's server word (bits 0-7, 0xFF none) | max |DOMAIN messages| of b(t) so that b(s) is in the model << 8
+    u32 sd;      // a's server word (bits 0-7, 0xFF none) | max |DOMAIN messages| of b(t) so that
+                 // b(s) is in the model (bits 8-23) | DM_UNDO_ADD / DM_UNDO_DUP
 };
+// a added one copy of k1 and changed nothing else (RequestVote, AppendEntries,
+// raft.tla:157-166, 171-192), or one copy of k0 (DuplicateMessage, :410-412):
+// DropMessage of that message on t gives back a's parent s, a stored state
+constexpr u32 DM_UNDO_ADD = 1u << 24, DM_UNDO_DUP = 1u << 25;
 template <int S, int K>
 RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diamond& dm) {
     dm.ord = 0;
@@ -944,18 +949,28 @@ RMC_HD void diamond_of(const u32 (&m)[K], int a, u64 foot, const Params& P, Diam
     if ((foot & FOOT_ADD) && count_of<K>(m, madd) == 1) delta += 1;       // a created the key
     if ((foot & FOOT_CONSUMED) && count_of<K>(m, mact) == 0) delta -= 1;  // a removed its last copy
     dm.sd = (u32)(srv & 0xFF) | ((u32)(P.max_msgs + delta) << 8);
+    if ((fa == 2 || fa == 6) && (foot & FOOT_ADD)) dm.sd |= DM_UNDO_ADD;
+    if (fa == 8 && (foot & FOOT_ACT)) dm.sd |= DM_UNDO_DUP;
 }
 RMC_HD bool diamond_rest(int sb, u32 mb, const Delta& db, int nmsg_b, const Diamond& dm) {
     if (sb >= 0 && (u32)sb == (dm.sd & 0xFFu)) return false;
     const u32 kb1 = db.has_add ? (db.add & MSG_MASK) : 0xFFFFFFFCu;
     if (mb == dm.k0 || mb == dm.k1 || kb1 == dm.k0 || kb1 == dm.k1) return false;
-    return nmsg_b <= (int)(dm.sd >> 8);
+    return nmsg_b <= (int)((dm.sd >> 8) & 0xFFFFu);
+}
+// A shortcut checked before the order (it needs no diamond): b = DropMessage of
+// the message a only added or duplicated (DM_UNDO_*) gives back s, a's parent.
+// (A Receive that only removes its message has Drop's successor too — a "twin"
+// rule skipping it measured slower for its extra registers: profiles/r05/samepar/.)
+RMC_HD bool diamond_undo(int fb, u32 mb, const Diamond& dm) {
+    return fb == 9 && ((mb == dm.k1 && (dm.sd & DM_UNDO_ADD)) || (mb == dm.k0 && (dm.sd & DM_UNDO_DUP)));
 }
 // b's side from lane b's descriptor: the same test as diamond_skip.
 template <int S, int K>
 RMC_HD bool diamond_skip_desc(const u32 (&m)[K], int b, u32 desc, const Delta& db, int nmsg_b, const Diamond& dm) {
     const int fb = (int)(desc & 15u), tb = (int)((desc >> 4) & 255u), sd = (int)((desc >> 12) & 7u);
     const u32 mb = fb >= 7 ? (selm<K>(m, tb) & MSG_MASK) : 0xFFFFFFFDu;
+    if (diamond_undo(fb, mb, dm)) return true;
     if (!(diamond_order(fb, b, mb) < dm.ord)) return false;  // dm.ord = 0: never (the common exit)
     const int sb = sd < 7 ? sd : fb == 7 ? (int)m_dst(mb) : -1;
     return diamond_rest(sb, mb, db, nmsg_b, dm);
@@ -965,6 +980,7 @@ template <int S, int K>
 RMC_HD bool diamond_skip(const u32 (&m)[K], int b, const Delta& db, int nmsg_b, const Diamond& dm, const Params& P) {
     const int fb = lane_family(P, b);
     const u32 mb = fb >= 7 ? (selm<K>(m, b - family_off(P, fb)) & MSG_MASK) : 0xFFFFFFFDu;
+    if (diamond_undo(fb, mb, dm)) return true;
     if (!(diamond_order(fb, b, mb) < dm.ord)) return false;  // dm.ord = 0: never
     return diamond_rest(lane_server<S>(P, b, fb, mb), mb, db, nmsg_b, dm);
 }

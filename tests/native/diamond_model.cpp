@@ -14,7 +14,9 @@
 //       b(t): by a's net change of the bag's domain).
 // Then b is enabled at s with the same effect, a is enabled at b(s), and
 // a(b(s)) = b(a(s)) = b(t): the state is generated from b(s), a state of the
-// same or an earlier level, in the same or an earlier pass.  Successors whose
+// same or an earlier level, in the same or an earlier pass.  One same-parent
+// rule skips without the order: DropMessage of the message a only added
+// (RequestVote / AppendEntries) or duplicated gives back s.  Successors whose
 // probe is skipped still count as generated (TLC counts them).  Mode "check"
 // runs the BFS twice, without and with skipping, and requires identical
 // per-level counts; mode "count" reports the skippable fraction of probes.
@@ -91,12 +93,18 @@ struct Model {
         if (d.has_add && !cnt_of(m, d.add)) n += 1;
         return n;
     }
-    bool skippable(u64 t, const u32 (&m)[K], int lane_b, const Delta& db) const {
+    bool skippable(u64 t, const u64 (&w)[S], const u32 (&m)[K], int lane_b, const Delta& db) const {
         const int a = act[t];
-        if (a == 255) return false;
-        const Foot& fa = foot[t];
         const int fb = family(lane_b);
         const u32 mb = fb >= 7 ? (selm<K>(m, lane_b - P.off[fb]) & MSG_MASK) : 0u;
+        (void)w;
+        if (a == 255) return false;
+        const Foot& fa = foot[t];
+        // (undo) Drop of the message a only added (RequestVote, AppendEntries) or
+        // duplicated gives back a's parent
+        const int fam_a = family(a);
+        if (fb == 9 && (fam_a == 2 || fam_a == 6) && fa.has_add && fa.m_add == mb) return true;
+        if (fb == 9 && fam_a == 8 && fa.has_act && fa.m_act == mb) return true;
         // (1) order
         if (!(order_key(lane_b, mb) < order_key(a, fa.m_act))) return false;
         // (2) independence: server words
@@ -180,7 +188,7 @@ struct Model {
                         if (hm.k != h.k || hm.s != h.s) ++o.mismatch;
                     }
                     if (h.k == h0.k) continue;  // stutter
-                    const bool sk = skippable(t, m, lane, d);
+                    const bool sk = skippable(t, w, m, lane, d);
                     {  // the kernels' implementation (raft_packed.h) must decide the same
                         Diamond dm;
                         diamond_of<S, K>(m, act[t], hfoot[t], P, dm);

@@ -2,7 +2,7 @@
 # then MCraftBench and the XL bench with the old build (RMC_LIB=librmc_prev.so) alternated.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05/dropfirst; mkdir -p $O
+O=${OUT:-gpurun_out/r05/dropfirst}; mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "level or prefix or golden or config3 or symmetry or violation" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for r in 1 2; do

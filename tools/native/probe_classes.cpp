@@ -127,7 +127,7 @@ struct Model {
     struct Out {
         std::vector<u64> level_new;
         u64 generated = 0, probes = 0, skipped = 0, mismatch = 0;
-        u64 hits = 0, ruleA = 0, ruleA_hit = 0, ruleB = 0, ruleB_hit = 0;
+        u64 hits = 0, ruleA = 0, ruleA_hit = 0, ruleB = 0, ruleB_hit = 0, ruleC = 0, ruleC_hit = 0, ruleD = 0, ruleD_hit = 0;
         u64 hit_rel[4] = {0, 0, 0, 0};  // found state's level - parent level + 2 (0: <= -2)
         u64 hit_fam[10] = {0}, probe_fam[10] = {0};
     };
@@ -225,7 +225,25 @@ struct Model {
                                 if (d2.en && d2.rm < 0 && !d2.has_add && d2.srv == d.srv && d2.w_new == d.w_new) rB = true;
                             }
                     }
+                    // rule C: Drop(m) undoing the discovering lane's pure add of m (RequestVote,
+                    // AppendEntries, DuplicateMessage): the successor is t's parent
+                    bool rC = false;
+                    if (fam == 9 && act[t] != 255) {
+                        const int fa = family(act[t]);
+                        const u32 mb = selm<K>(m, lane - P.off[9]) & MSG_MASK;
+                        rC = (fa == 2 || fa == 6 || fa == 8) && foot[t].has_add && foot[t].m_add == mb;
+                        if (fa == 8) rC = foot[t].has_act && foot[t].m_act == mb;
+                    }
+                    // rule D: Restart(i) absorbing the discovering lane's change of server i
+                    // (BecomeLeader(i), AdvanceCommitIndex(i): fields Restart resets)
+                    bool rD = false;
+                    if (fam == 0 && act[t] != 255) {
+                        const int fa = family(act[t]);
+                        rD = (fa == 3 || fa == 5) && (act[t] - P.off[fa]) == (lane - P.off[0]);
+                    }
                     const bool fresh = insert(h.k);
+                    if (rD) { ++o.ruleD; if (!fresh) ++o.ruleD_hit; }
+                    if (rC) { ++o.ruleC; if (!fresh) ++o.ruleC_hit; }
                     ++o.probe_fam[fam];
                     if (!fresh) {
                         ++o.hits;
@@ -281,7 +299,9 @@ int run(int V, int mt, int ml, int mm, int md, int levels, u64 cap) {
            (unsigned long long)a.hit_rel[1], (unsigned long long)a.hit_rel[2], (unsigned long long)a.hit_rel[3]);
     for (int f = 0; f < 10; ++f)
         printf("family %d: probes %llu hits %llu\n", f, (unsigned long long)a.probe_fam[f], (unsigned long long)a.hit_fam[f]);
-    printf("skipped by diamonds %llu\n", (unsigned long long)a.skipped);
+    printf("skipped by diamonds %llu; rule C %llu (hits %llu); rule D %llu (hits %llu)\n",
+           (unsigned long long)a.skipped, (unsigned long long)a.ruleC, (unsigned long long)a.ruleC_hit,
+           (unsigned long long)a.ruleD, (unsigned long long)a.ruleD_hit);
     printf("{\"distinct\": %llu, \"generated\": %llu, \"probes\": %llu, \"hits\": %llu, \"ruleA\": %llu, "
            "\"ruleA_hit\": %llu, \"ruleB\": %llu, \"ruleB_hit\": %llu}\n",
            (unsigned long long)da, (unsigned long long)a.generated, (unsigned long long)a.probes,
