@@ -2005,15 +2005,17 @@ static u64 resident_grid(const void* k) {
     return v;
 }
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 19 (default) =
-// k_expand_sort over windows of 16 tiles presorted by class (k_window_order;
-// no sort in the kernel, so a smaller block), 5 probes in flight per thread,
-// the parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD), each block
-// taking a fixed share of the windows; 20 = each wave taking its next
-// quarter-window from a launch-wide counter instead (a tie over three boxes:
+// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 20 (default since
+// round 5) = k_expand_sort over windows of 16 tiles presorted by class
+// (k_window_order; no sort in the kernel, so a smaller block), 5 probes in flight
+// per thread, the parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD),
+// each wave taking its next quarter-window from a launch-wide counter; 19 = the
+// same with each block taking a fixed share of the windows (a tie in round 4:
 // 229-232 vs 241-243, 240 vs 228-234 and 229-242 vs 227-234 ms for 19,
-// profiles/r04/ab/expand_dynamic_units_*; asking for the next unit one unit
-// ahead measured 245-255 ms, removed); 10 = 6 probes at 5 waves with the mixes held (247-250
+// profiles/r04/ab/expand_dynamic_units_*; with the Drop-first diamond order's
+// fewer probes 20 wins, XL 739.3-741.6 vs 760.1-762.1 ms, profiles/r05/variants/;
+// asking for the next unit one unit ahead measured 245-255 ms, removed);
+// 10 = 6 probes at 5 waves with the mixes held (247-250
 // ms); 15 = 5 probes at 5 waves; 18 = 6 probes at 6 waves (spills); 6 = the
 // round-3 kernel (windows sorted in LDS, 8 probes, 4 waves: 263-269 ms); 1 =
 // every lane of every state (k_expand, what shapes with more than 64 lanes
@@ -2024,7 +2026,7 @@ static u64 resident_grid(const void* k) {
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
-        return e ? atoi(e) : 19;
+        return e ? atoi(e) : 20;
     }();
     return v;
 }
