@@ -1306,12 +1306,12 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
 // POOL: the pool flush (flush_pool) with the single-GPU kernel's shape (presorted
 // windows of 16 tiles, early probe loads, the parent's mixes recomputed per lane).
-template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool POOL = false>
+template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool POOL = false, int DYN = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_dist(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 128 && POOL && !REP)
-        expand_body<S, K, false, BATCH, true, false, false, true, true, true, 16, K <= 4 ? 1 : 0, false, true, 0, true>(
-            P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, true, false, false, true, true, true, 16, K <= 4 ? 1 : 0, false, true, DYN,
+                    true>(P, PT, B, lo, hi);
     else if constexpr (POOL && !REP)  // more than 64 lanes: every lane, the pool flush
         expand_body<S, K, false, BATCH, true, false, false, false, false, true, 8, 0, false, false, 0, true>(P, PT, B,
                                                                                                            lo, hi);
@@ -2123,6 +2123,16 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
+        } else if (dist_kvariant() == 4 && B.pool) {  // 3 with dynamic per-wave units (a tie at one rank:
+                                                       // 224.7-226.0 vs 225.3-225.5 ms, profiles/r05/kv4/)
+            if constexpr (SORTED) {
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true, 1>));
+                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, true, 1>));
+            } else {
+                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, false, 4, true>));
+            }
         } else if (dist_kvariant() == 3 && B.pool) {  // the pool flush at the single-GPU kernel's shape
             if constexpr (SORTED) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
