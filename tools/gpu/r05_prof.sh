@@ -2,7 +2,7 @@
 # times (the cost model's T1), and the sharded kernel's rate at one rank (k_dist).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05/prof; mkdir -p $O
+O=${OUT:-gpurun_out/r05/prof}; mkdir -p $O
 OUT=$O/pmc_xl bash tools/gpu/pmc.sh || exit 1
 python3 tools/pmc_summary.py $O/pmc_xl $O/summary MCraftBenchXL || exit 1
 ls $O/summary
