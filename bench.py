@@ -65,6 +65,9 @@ def parse(argv=None):
                     help="model timed to its fixpoint on the host CPU oracle AND on the GPU "
                          "('' to skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--v2-config", default=os.path.join(ROOT, "specs", "MCraftBench.cfg"),
+                    help="one GPU: also time this model (the reference's Value = {v1, v2}, MCraft.tla:15-16) "
+                         "to its fixpoint after the timed steps, untimed in the line's value ('' to skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch logic only: ranks rendezvous over gloo and report, no GPU, no librmc")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
@@ -236,6 +239,27 @@ def pmc_traffic(config_path):
         if os.path.exists(pf):
             return json.load(open(pf))["hbm_bytes_per_launch"], os.path.relpath(pf, ROOT)
     return None, None
+
+
+def v2_fixpoint(path, dev, runs=3):
+    """The bench model of rounds 1-4, MCraftBench.cfg (S=3 with the reference's
+    Value = {v1, v2}, MCraft.tla:15-16), searched to its fixpoint on the same GPU
+    after the timed steps: one warm run, then the best and mean of `runs`.  Not
+    part of the line's value (the XL model, V = 1, is the headline workload)."""
+    import rmc
+    c = rmc.config_from_files(path, builtin_raft=True)
+    c.device = dev
+    c.state_capacity = int(1.5e9)  # resident, no spill (the size every round measured)
+    ts = []
+    with rmc.Checker(c) as ck:
+        ck.run(record_levels=False)
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            r = ck.run(record_levels=False)
+            ts.append(time.perf_counter() - t0)
+    return {"model": os.path.basename(path) + ": " + gpu_fix_name(c), "distinct": r.distinct,
+            "generated": r.generated, "depth": r.depth, "runs": runs, "ms_best": min(ts) * 1e3,
+            "ms_mean": sum(ts) / len(ts) * 1e3, "distinct_per_s_best": r.distinct / min(ts)}
 
 
 # ---- one rank ------------------------------------------------------------------
@@ -481,6 +505,8 @@ def main(argv=None):
                                    "world / rank 0's kernel time")
         out["roofline"]["achieved"] = (b_alg / world) / ks / 1e9 if ks > 0 else 0.0
         out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
+    if rank == 0 and world == 1 and a.v2_config and os.path.abspath(a.v2_config) != os.path.abspath(a.config):
+        out["value_set_v2"] = v2_fixpoint(a.v2_config, dev)
     if rank == 0 and not a.no_cpu and world == 1:
         fix_cfg, gpu_fix = None, None
         if a.cpu_fixpoint:

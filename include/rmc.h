@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 6 /* 6: rmc_result.spill_links_on_device (round 5) */
+#define RMC_ABI_VERSION 7 /* 6: rmc_result.spill_links_on_device (round 5); 7: .verified_spilled (round 6) */
 
 /* Capacity of the packed encoding (DESIGN.md "Packed state"): the layout the
  * BFS kernels run on when every bound fits it. */
@@ -170,6 +170,9 @@ typedef struct rmc_result {
     int32_t spill_links_on_device; /* 1: the trace links (parent, lane) of spilled states stayed */
                                    /* in HBM and the window was a ring; 0: links on the host   */
     int32_t pad2;
+    /* RMC_FLAG_VERIFY_STATES with RMC_FLAG_SPILL */
+    uint64_t verified_spilled; /* hits (of `verified`) whose stored state had left the device */
+                               /* window, compared with its host copy                       */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */

@@ -49,8 +49,6 @@ int validate(const rmc_config* c, std::string* why) {
     if (c->max_log_len < 0 || c->max_log_len > RMC_MAX_LOG) return bad("max_log_len must be 0..3");
     if (c->max_msgs < 0 || c->max_msgs > RMC_MAX_MSGS) return bad("max_msgs must be 0..8");
     if (c->max_dup < 1 || c->max_dup > RMC_MAX_DUP) return bad("max_dup must be 1..3");
-    if ((c->flags & RMC_FLAG_SPILL) && (c->flags & RMC_FLAG_VERIFY_STATES))
-        return bad("RMC_FLAG_SPILL does not combine with RMC_FLAG_VERIFY_STATES");
     return 0;
 }
 
@@ -397,6 +395,10 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
     }
     HIPCHK(c, hipMemcpyAsync(hp, X.parent, n * 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipMemcpyAsync(ha, X.act, n, hipMemcpyDeviceToHost, c->st));
+    if (X.h_state) {  // verification: the states too (the window's first n are [base, a))
+        HIPCHK(c, hipMemcpyAsync(X.h_state + X.base * (u64)c->NW, X.store, n * W, hipMemcpyDeviceToHost, c->st));
+        X.hcopied = a;
+    }
     // shift in pieces of at most n states: no piece overlaps its own destination,
     // and stream order keeps every source read before a later piece overwrites it
     const u64 m = count - a;
@@ -425,6 +427,76 @@ int spill_to(rmc_ctx* c, u64 a, u64 count) {
     c->res.spilled += n;
     c->res.spills += 1;
     c->res.spill_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+// ---- verification + spill --------------------------------------------------------
+// Full-state verification compares every fingerprint hit with the stored state
+// that owns the slot.  A spilled search overwrites (ring) or drops (shifted
+// window) the device copies of old states, so each state is copied to a host
+// mirror before its device copy goes, and a hit on such an owner is parked by
+// the expansion kernel (B.hbuf) and compared after the launch with the owner's
+// host copy (k_verify_host).  Most duplicates are of recent states, so few hits
+// take that path.
+int verify_spill_reserve(rmc_ctx* c) {
+    SpillState& X = c->spill;
+    X.hs_bytes = (size_t)X.total_cap * (size_t)c->NW * 4;
+    void* m = mmap(nullptr, X.hs_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) {
+        X.hs_bytes = 0;
+        return fail(c, RMC_E_NOMEM, "verification + spill: cannot reserve host address space for the states");
+    }
+    (void)madvise(m, X.hs_bytes, MADV_HUGEPAGE);
+    X.h_state = (u32*)m;
+    X.ostage_cap = 1ull << 22;
+    c->B.hcap = 1ull << 26;
+    if (hipHostMalloc(&X.h_ostage, X.ostage_cap * (u64)c->NW * 4, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&X.d_ostage, X.ostage_cap * (u64)c->NW * 4) != hipSuccess ||
+        hipMalloc(&c->B.hbuf, c->B.hcap * 16) != hipSuccess)
+        return fail(c, RMC_E_NOMEM, "verification + spill: staging allocation failed");
+    return 0;
+}
+
+// Ring window: copy the states [hcopied, upto) — all below the launch's frontier,
+// so final, and not yet overwritten — to the host mirror (up to two pieces).
+int verify_copy_out(rmc_ctx* c, u64 upto) {
+    SpillState& X = c->spill;
+    const u64 W = (u64)c->NW * 4;
+    while (X.hcopied < upto) {
+        const u64 i = X.hcopied, sl = i & c->B.wmask;
+        const u64 n = std::min(upto - i, X.win - sl);
+        HIPCHK(c, hipMemcpyAsync((char*)X.h_state + i * W, (char*)X.store + sl * W, n * W, hipMemcpyDeviceToHost,
+                                 c->st));
+        X.hcopied = i + n;
+    }
+    return 0;
+}
+
+// The n hits the last launch parked in B.hbuf {parent, owner index | lane << 56}:
+// stage the owners' host copies (batches of ostage_cap) and compare on the device.
+int verify_host_hits(rmc_ctx* c, u64 n) {
+    SpillState& X = c->spill;
+    if (n > c->B.hcap) return fail(c, RMC_E_CAPACITY, "verification buffer full");
+    std::vector<u64> rec(2 * n);
+    HIPCHK(c, hipMemcpyAsync(rec.data(), c->B.hbuf, n * 16, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    const u64 NW = (u64)c->NW;
+    for (u64 off = 0; off < n; off += X.ostage_cap) {
+        const u64 m = std::min(X.ostage_cap, n - off);
+        for (u64 q = 0; q < m; ++q) {
+            const u64 ix = rec[2 * (off + q) + 1] & ((1ull << 56) - 1);
+            if (ix >= X.hcopied)
+                return fail(c, RMC_E_HIP, "verification: a spilled owner (index " + std::to_string(ix) +
+                                              ") has no host copy");
+            memcpy(X.h_ostage + q * NW, X.h_state + ix * NW, NW * 4);
+        }
+        HIPCHK(c, hipMemcpyAsync(X.d_ostage, X.h_ostage, m * NW * 4, hipMemcpyHostToDevice, c->st));
+        HIPCHK(c, launch(c->sh, 15, c->P, c->PT, c->B, m, off, X.d_ostage, nullptr, 0, nullptr, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));  // the pinned stage is refilled next
+    }
+    HIPCHK(c, hipMemsetAsync(&c->B.ctr->hcount, 0, 8, c->st));
+    c->h_ctr->hcount = 0;
+    X.host_hits += n;
     return 0;
 }
 
@@ -510,7 +582,11 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     if (cap == 0) {
         // table <= 4 slots per state after pow2 rounding (+ as many sidx words when verifying);
         // spilling: the largest set of at most half the budget, two slots per state
-        if (spill) {
+        if (spill && c->sh.verify) {  // the set and its slot -> index map: 16 B per slot, <= 2/3 of the budget
+            u64 sl = 1ull << 20;
+            while (sl * 32 <= budget / 3 * 2) sl <<= 1;
+            cap = sl / 2;
+        } else if (spill) {
             u64 sl = 1ull << 20;
             while (sl * 16 <= budget / 2) sl <<= 1;  // 8 B * (2 sl) <= budget / 2
             cap = sl / 2;
@@ -530,10 +606,13 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     bool dev_links = false;
     u64 link_cap = win;
     if (spill) {
-        const u64 rest = budget - std::min<u64>(budget, slots * 8);
+        // (verification: the slot -> index map and the two hit buffers, 1 GB each)
+        const u64 fixed = slots * (c->sh.verify ? 16 : 8) + (c->sh.verify ? (2ull << 30) : 0);
+        const u64 rest = budget - std::min<u64>(budget, fixed);
         const char* hl = getenv("RMC_SPILL_HOST_LINKS");
         const u64 wbytes = per_state - 9;  // state, footprint, class
-        const u64 need_win = cfg->device_window ? cfg->device_window : cap / 4;
+        // verification keeps a smaller ring (its set is twice the size): an eighth of the states
+        const u64 need_win = cfg->device_window ? cfg->device_window : cap / (c->sh.verify ? 8 : 4);
         dev_links = !(hl && atoi(hl)) && rest > cap * 9 && (rest - cap * 9) / wbytes >= need_win;
         win = cfg->device_window;
         if (win == 0) win = dev_links ? (rest - cap * 9) / wbytes : rest / per_state;
@@ -597,6 +676,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
             c->err = "device allocation failed (verification buffers)";
             return bail(RMC_E_NOMEM);
         }
+        if (spill && verify_spill_reserve(c)) return bail(RMC_E_NOMEM);
     }
     c->B.rank = 0;
     c->B.world = 1;
@@ -623,6 +703,10 @@ void rmc_destroy(rmc_ctx* c) {
     free_dist(c);
     (void)hipFree(c->B.sidx);
     (void)hipFree(c->B.vbuf);
+    (void)hipFree(c->B.hbuf);
+    (void)hipFree(c->spill.d_ostage);
+    if (c->spill.h_ostage) (void)hipHostFree(c->spill.h_ostage);
+    if (c->spill.hs_bytes) munmap(c->spill.h_state, c->spill.hs_bytes);
     (void)hipFree(c->B.ties);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -671,6 +755,9 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
     HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (int rc = reset_counters(c, false)) return rc;
+    c->B.vlo = 0;
+    c->spill.hcopied = 0;
+    c->spill.host_hits = 0;
 
     // ---- Init (raft.tla:125-129): one initial state
     rmc_state_view iv;
@@ -730,13 +817,23 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 // count + n * lanes <= a + win — nothing is ever moved
                 const u64 lanes = (u64)c->P.off[10], count = c->h_ctr->count, win = c->spill.win;
                 const u64 room = count - a < win ? a + win - count : 0;
-                const u64 want = std::min(b - a, room / lanes);
+                u64 want = std::min(b - a, room / lanes);
+                if (c->sh.verify) want = std::min(want, c->B.hcap / lanes);  // hbuf holds every hit of a launch
                 if (want == 0)
                     return fail(c, RMC_E_CAPACITY,
                                 "spill: the device window (" + std::to_string(win) +
                                     " states) cannot hold the frontier and the level being built; raise "
                                     "rmc_config.device_window");
                 b = a + want;
+                if (c->sh.verify) {
+                    // the launch may overwrite the ring slots of states below
+                    // count + n * lanes - win (<= a): copy them to the host first, and
+                    // send hits on them to hbuf
+                    const u64 top = count + want * lanes;
+                    const u64 vlo = top > win ? top - win : 0;
+                    if (int rc = verify_copy_out(c, vlo)) return rc;
+                    c->B.vlo = vlo;
+                }
             } else if (c->spill.on) {
                 // every lane yields at most one new state: a launch of n states
                 // stays inside the window when n * lanes <= room.  Launches
@@ -751,6 +848,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                 if (due)
                     if (int rc = spill_to(c, a, count)) return rc;
                 want = std::min(want, (c->B.cap - count) / lanes);
+                if (c->sh.verify) {
+                    want = std::min(want, c->B.hcap / lanes);
+                    c->B.vlo = c->spill.base;  // [0, base) were copied to the host by spill_to
+                }
                 if (want == 0)
                     return fail(c, RMC_E_CAPACITY,
                                 "spill: the device window (" + std::to_string(c->spill.win) +
@@ -774,6 +875,8 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                                  c->st));
                 HIPCHK(c, hipMemsetAsync(&c->B.ctr->vcount, 0, 8, c->st));
                 c->h_ctr->vcount = 0;
+                if (c->h_ctr->hcount)  // hits on spilled owners: against their host copies
+                    if (int rc = verify_host_hits(c, c->h_ctr->hcount)) return rc;
             }
             if (c->spill.on) {
                 if (int rc = read_counters(c)) return rc;
@@ -841,6 +944,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     }
     c->res.distinct = c->level_start.back();
     c->res.depth = depth;
+    c->res.verified_spilled = c->spill.host_hits;
     const double D = (double)c->res.distinct, G = (double)c->res.generated;
     // TLC's "calculated (optimistic)" fingerprint-collision estimate
     c->res.collision_probability = fp_collision_estimate(D, G, c->table_slots);
@@ -934,6 +1038,9 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     if (c->level_start.size() < 2 || c->have_target)
         return fail(c, RMC_E_STATE, "checkpoint: needs a BFS stopped at a level boundary without a violation");
     if (c->res.left_on_queue == 0) return fail(c, RMC_E_STATE, "checkpoint: the search is complete");
+    if (c->spill.on && c->sh.verify)
+        return fail(c, RMC_E_STATE, "checkpoint: not supported with RMC_FLAG_VERIFY_STATES and RMC_FLAG_SPILL "
+                                    "(the host copies of the spilled states are not written)");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->st));
     // a sharded search: every rank writes its own part, <path>.rank<r> (collective
@@ -979,6 +1086,8 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
 int rmc_recover(rmc_ctx* c, const char* path) {
     if (!c || !path) return RMC_E_INVAL;
     if (c->wide) return fail(c, RMC_E_STATE, "checkpoint / recover: not supported on the wide layout");
+    if (c->spill.on && c->sh.verify)
+        return fail(c, RMC_E_STATE, "recover: not supported with RMC_FLAG_VERIFY_STATES and RMC_FLAG_SPILL");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     const std::string file = shard_path(c, path);
     FILE* f = fopen(file.c_str(), "rb");

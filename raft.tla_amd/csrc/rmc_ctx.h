@@ -25,7 +25,7 @@ struct DistState {
     // Outbox sets, double-buffered: the expansion of round k + 1 (ctx stream)
     // fills one set while round k's exchange (xs) drains the other.
     struct Set {
-        rmc::u64* key_out = nullptr;             // [world][kcap][2] keys per owner (k, s32)
+        rmc::u64* key_out = nullptr;             // [world][kcap] 12-B keys per owner {k lo, k hi, s32}
         rmc::u64* tick_out = nullptr;            // [world][kcap] tickets (parent | lane << 56)
         unsigned long long* ocount = nullptr;    // [world] keys written per owner, [world]: pool records
         rmc::u32* pool = nullptr;                // remote-successor pool (phase-2 records, flush_pool)
@@ -40,7 +40,7 @@ struct DistState {
     hipEvent_t ev_cnt = nullptr, ev_acc = nullptr, ev_c = nullptr, ev_x = nullptr;
     hipEvent_t ev_h = nullptr;      // host waits on xs (under the deadline)
     // single buffers (used on xs only, rounds in order)
-    rmc::u64* key_in = nullptr;     // keys received (k, s32 pairs), blocks by source
+    rmc::u64* key_in = nullptr;     // keys received (12-B {k, s32} records), blocks by source
     uint8_t* rep_out = nullptr;     // replies to the keys received (same layout)
     uint8_t* rep_in = nullptr;      // replies to the keys sent, [world][kcap]
     rmc::u32* st_in = nullptr;      // accepted states received, blocks by source
@@ -107,6 +107,16 @@ struct SpillState {
     size_t h_bytes = 0;
     rmc::u64 faulted = 0;          // links [0, faulted) have backed pages
     std::thread ahead;             // backs the next window's pages during expansion
+    // verification + spill (RMC_FLAG_VERIFY_STATES): a host copy of every state that
+    // leaves the device window ([0, hcopied) copied), against which the hits on
+    // spilled owners are checked (B.hbuf, k_verify_host); reserved like the links
+    rmc::u32* h_state = nullptr;
+    size_t hs_bytes = 0;
+    rmc::u64 hcopied = 0;
+    rmc::u32* h_ostage = nullptr;  // pinned / device staging of the owners of one batch of hits
+    rmc::u32* d_ostage = nullptr;
+    rmc::u64 ostage_cap = 0;       // states per batch
+    rmc::u64 host_hits = 0;        // hits checked against host copies in the last run
 };
 
 struct rmc_ctx {

@@ -39,9 +39,10 @@ using namespace rmc_host;
 
 namespace {
 
-// Bytes per phase-1 key record: the raw fingerprint (k, s32) as two u64
-// (raft_packed.h Fp; the owner derives its own table value and slot).
-constexpr u64 KEYB = 16;
+// Bytes per phase-1 key record: the raw fingerprint (k, s32) as three u32
+// {k lo, k hi, s32} (raft_packed.h Fp, put_key; the owner derives its own
+// table value and slot).
+constexpr u64 KEYB = 12;
 
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -675,7 +676,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             for (int p = 0; p < W; ++p) {
                 global_more |= (rx(cx, p)[1] & 1u) != 0;
                 global_sends |= (rx(cx, p)[1] & 4u) != 0;
-                // phase-1 key records: the raw fingerprint (k, s32) in two u64 (KEYB bytes)
+                // phase-1 key records: the raw fingerprint (k, s32), KEYB bytes each
                 scnt[(size_t)p] = cx[RWD * (u64)p] * KEYB;
                 soff[(size_t)p] = (u64)p * kcap * KEYB;
                 rcnt[(size_t)p] = rx(cx, p)[0] * KEYB;

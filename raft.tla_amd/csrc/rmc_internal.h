@@ -25,6 +25,7 @@ struct Counters {
     u64 novf;       // sharded: keys that did not fit their owner's outbox (parked in B.ovf)
     u64 wnext;      // dynamic work units: the next (window, wave slot) of the launch (zeroed by k_window_order)
     u64 walked;     // (state, lane) slots the lane walk visited (RMC_WALK_STATS: lane efficiency = generated / walked)
+    u64 hcount;     // verification + spill: hits in hbuf whose stored owner has left the device window
 };
 
 struct DevBufs {
@@ -49,7 +50,7 @@ struct DevBufs {
     u64* sent;                 // lossy cache of fingerprints already shipped to their owner
     u64 smask;                 // sent-cache slots - 1
     // two-phase exchange: phase 1 keys, phase 2 accepted states
-    u64* key_out;              // [world][kcap][2] keys for each owner: the raw fingerprint (k, s32)
+    u64* key_out;              // [world][kcap] 12-B keys for each owner: the raw fingerprint {k lo, k hi, s32}
     u64* tick_out;             // [world][kcap] local tickets: parent index | lane << 56, or POOL_TICK | pool index
     u64 kcap;                  // keys per destination and chunk
     unsigned long long* ocount;  // [world] keys written per destination
@@ -77,6 +78,12 @@ struct DevBufs {
     u64* sidx;
     u64* vbuf;
     u64 vcap;                  // records in vbuf
+    // verification + spill: owners with a store index below vlo are no longer on
+    // the device (spilled; their host copies are compared after the launch): such
+    // hits go to hbuf as {parent index, owner index | lane << 56}
+    u64 vlo;
+    u64* hbuf;
+    u64 hcap;                  // records in hbuf
     // SYMMETRY: successors whose server signatures tie, {parent index | lane << 56},
     // canonicalised by k_ties after each expansion launch
     u64* ties;
@@ -106,7 +113,9 @@ struct Shape {
 //       11 = k_compare_remote of `a` received state records `in` (sharded verification);
 //       12 = k_expand_dist<REP> over the replicated level's records B.rep[a, b);
 //       13 = k_pack_rep of this rank's stored states [a, b) into records at `out`;
-//       14 = k_route: key the pool's records and fill the outboxes (counts on the device).
+//       14 = k_route: key the pool's records and fill the outboxes (counts on the device);
+//       15 = k_verify_host of `a` hits B.hbuf[b, b + a) against their owners' host copies
+//            staged at `in` (verification + spill).
 hipError_t launch(const Shape& sh, int which, const Params& P, const PermTable& PT, const DevBufs& B, u64 a, u64 b,
                   const u32* in, u32* out, u64 cap, unsigned long long* count, hipStream_t st);
 
@@ -119,7 +128,8 @@ struct SimCounters {
 hipError_t launch_sim(const Shape& sh, const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, u64 seed,
                       int mode, SimCounters* out, i64 rec_beh, u32* rec, hipStream_t st);
 
-// Sharded mode, phase 1 owner side: insert n received keys (k, s32 pairs), reply[t] = new;
+// Sharded mode, phase 1 owner side: insert n received keys (12-B {k lo, k hi, s32}
+// records), reply[t] = new;
 // keys [src_off[p], src_off[p + 1]) came from rank p, acc[p] += keys of p that were new.
 constexpr int kMaxWorld = 64;
 struct SrcOff {

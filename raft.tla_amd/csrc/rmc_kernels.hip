@@ -343,12 +343,14 @@ __device__ __forceinline__ int verify_hit(const u64 (&w)[S], const u32 (&m)[K], 
     if (slot == ~0ull) return 3;
     const u64 ix = B.sidx[slot];
     if (ix == ~0ull) return 2;  // owner found in this launch: check after it
+    if (ix < B.vlo) return 4;   // owner spilled: checked against its host copy after the launch
     Delta d;
     lane_delta<S, K>(w, m, lane, P, d);
     PackedState<S, K> o;
     materialise<S, K>(w, m, d, o.w, o.m);
-    if constexpr (SYM) return same_orbit<S, K>(o, B.store + ix * (u64)NW, PT) ? 0 : 1;
-    return same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW) ? 0 : 1;
+    const u32* st = B.store + wslot(B, ix) * (u64)NW;
+    if constexpr (SYM) return same_orbit<S, K>(o, st, PT) ? 0 : 1;
+    return same_state<S, K>(o.w, o.m, st) ? 0 : 1;
 }
 
 __device__ __forceinline__ u64 wave_sum64(u64 v) {
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(256) void k_publish(const Params P, const PermTable
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + i * (u64)NW, w, m);
+        load_state<S, K>(B.store + wslot(B, i) * (u64)NW, w, m);
         const TKey key = verify_key<S, K, SYM>(w, m, P, PT, B.tmask);
         u64 s = key.s0;
         u64 n = 0;
@@ -392,7 +394,7 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable 
         const int lane = (int)(sl >> 56);
         u64 w[S];
         u32 m[K];
-        load_state<S, K>(B.store + parent * (u64)NW, w, m);
+        load_state<S, K>(B.store + wslot(B, parent) * (u64)NW, w, m);
         Delta d;
         lane_delta<S, K>(w, m, lane, P, d);
         PackedState<S, K> o;
@@ -403,9 +405,42 @@ __global__ __launch_bounds__(256) void k_verify(const Params P, const PermTable 
             continue;
         }
         ++vchk;
+        const u32* st = B.store + wslot(B, ix) * (u64)NW;  // found in this launch: in the window
         bool same;
-        if constexpr (SYM) same = same_orbit<S, K>(o, B.store + ix * (u64)NW, PT);
-        else same = same_state<S, K>(o.w, o.m, B.store + ix * (u64)NW);
+        if constexpr (SYM) same = same_orbit<S, K>(o, st, PT);
+        else same = same_state<S, K>(o.w, o.m, st);
+        vcol += same ? 0u : 1u;
+    }
+    vchk = wave_sum64(vchk);
+    vcol = wave_sum64(vcol);
+    if (__lane_id() == 0 && vchk) atomicAdd((unsigned long long*)&B.ctr->vchecked, (unsigned long long)vchk);
+    if (__lane_id() == 0 && vcol) atomicAdd((unsigned long long*)&B.ctr->collisions, (unsigned long long)vcol);
+}
+
+// Verification + spill: the hits hbuf[off, off + n) whose owners had left the
+// device window, against the owners' host copies staged at `owners` (one
+// record each, in hbuf order).  The parents are the launch's frontier states,
+// still in the window (the ring never overwrites a launch's own frontier).
+template <int S, int K, bool SYM>
+__global__ __launch_bounds__(256) void k_verify_host(const Params P, const PermTable PT, const DevBufs B,
+                                                     const u32* owners, u64 n, u64 off) {
+    constexpr int NW = 2 * S + K;
+    u64 vchk = 0, vcol = 0;
+    for (u64 q = (u64)blockIdx.x * 256ull + threadIdx.x; q < n; q += (u64)gridDim.x * 256ull) {
+        const u64 parent = B.hbuf[2 * (off + q)];
+        const int lane = (int)(B.hbuf[2 * (off + q) + 1] >> 56);
+        u64 w[S];
+        u32 m[K];
+        load_state<S, K>(B.store + wslot(B, parent) * (u64)NW, w, m);
+        Delta d;
+        lane_delta<S, K>(w, m, lane, P, d);
+        PackedState<S, K> o;
+        materialise<S, K>(w, m, d, o.w, o.m);
+        const u32* st = owners + q * (u64)NW;
+        bool same;
+        if constexpr (SYM) same = same_orbit<S, K>(o, st, PT);
+        else same = same_state<S, K>(o.w, o.m, st);
+        ++vchk;
         vcol += same ? 0u : 1u;
     }
     vchk = wave_sum64(vchk);
@@ -471,14 +506,16 @@ __device__ __forceinline__ Fp fp_of_materialised(const u64 (&w)[S], const u32 (&
 
 // Phase-1 keys travel as the raw fingerprint (k, low 32 bits of s): the owner
 // derives its own table value and slot (tkey; tables may differ in size across
-// ranks).  Outbox: two u64 per key; parking (B.ovf): {k, s32 | flags << 32,
+// ranks).  Outbox: 12 B per key, three u32 {k lo, k hi, s32} (round 6; 16 B
+// before: a quarter of phase 1's bytes was padding); parking (B.ovf): {k, s32 | flags << 32,
 // ticket}, where flag OVF_UNKEYED marks a ticket the expansion parked without
 // computing its key (k_route_fix computes it).
 constexpr u64 OVF_UNKEYED = 1ull << 32;
 __device__ __forceinline__ void put_key(const DevBufs& B, u32 dest, u64 slot, u64 k, u32 s32, u64 tick) {
-    u64* o = B.key_out + 2 * ((u64)dest * B.kcap + slot);
-    o[0] = k;
-    o[1] = s32;
+    u32* o = reinterpret_cast<u32*>(B.key_out) + 3 * ((u64)dest * B.kcap + slot);
+    o[0] = (u32)k;
+    o[1] = (u32)(k >> 32);
+    o[2] = s32;
     B.tick_out[(u64)dest * B.kcap + slot] = tick;
 }
 __device__ __forceinline__ void park_key(const DevBufs& B, u64 k, u64 s_and_flags, u64 tick) {
@@ -792,8 +829,12 @@ __device__ __forceinline__ void flush_pool(const Params& P, const DevBufs& B, u6
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
           bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
-          int DYN = 0, bool POOL = false>
+          int DYN = 0, bool POOL = false, bool EARLY = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
+    // EARLY: the CONSTRAINT, the structural stutter and the commuting-diamond
+    // test before the lane's hash (delta_bounds, delta_mix_pre): a skipped
+    // successor costs no mixes (the same probes as without it)
+    static_assert(!EARLY || (DIA && !REP && !DIST), "EARLY: the single-GPU diamond kernel");
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     static_assert(!POOL || (MARK && !REP), "the pool flush: the send-marker kernel");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -1036,6 +1077,24 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                                 h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
                             }
                         }
+                    } else if (EARLY && en) {
+                        int nmb = 0, nm0 = 0;
+                        bool stut = false;
+                        if constexpr (PRE) {
+                            nm0 = pmx.nmsg;
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < K; ++q) nm0 += m[q] ? 1 : 0;
+                        }
+                        in_model = delta_bounds<S, K>(w, m, nm0, d, P, &nmb, &stut);
+                        if (in_model && (stut || (SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d,
+                                                                                  nmb, dm)
+                                                       : diamond_skip<S, K>(m, lane, d, nmb, dm, P))))
+                            in_model = 0;
+                        if (in_model) {
+                            if constexpr (PRE) h = delta_mix_pre<S, K>(w, m, pmx, d);
+                            else h = delta_mix<S, K>(w, m, h0, d);
+                        }
                     } else if (en) {
                         int nmb = 0;
                         if constexpr (PRE)
@@ -1154,13 +1213,34 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
             }
             if constexpr (VERIFY) {
                 // compare each hit with the stored owner of its slot (parked in s_key)
-                u32 defbits = 0;
+                u32 defbits = 0, hostbits = 0;
                 for (int b = 0; b < BATCH; ++b) {  // rolled: one inlined copy of the check
                     if (!((hitbits >> b) & 1u)) continue;
                     const int r = verify_hit<S, K, SYM>(w, m, lane0 + b, s_key[b][threadIdx.x], P, PT, B);
                     vchk += (u64)(r <= 1);
                     vcol += (u64)(r == 1);
                     defbits |= (u32)(r == 2) << b;
+                    hostbits |= (u32)(r == 4) << b;
+                }
+                // owners that left the device window (spill): checked on their host
+                // copies after the launch (k_verify_host)
+                for (int b = 0; b < BATCH; ++b) {
+                    const bool hd = (hostbits >> b) & 1u;
+                    const u64 bal = __ballot(hd);
+                    if (!bal) continue;
+                    const int leader = __ffsll((long long)bal) - 1;
+                    u64 q0 = 0;
+                    if (me == leader) q0 = atomicAdd((unsigned long long*)&B.ctr->hcount, (unsigned long long)__popcll(bal));
+                    q0 = bcast64(q0, leader);
+                    if (hd) {
+                        const u64 q = q0 + (u64)__popcll(bal & lt_mask);
+                        if (q < B.hcap) {
+                            B.hbuf[2 * q] = lo + rel;
+                            B.hbuf[2 * q + 1] = B.sidx[s_key[b][threadIdx.x]] | ((u64)(lane0 + b) << 56);
+                        } else {
+                            atomicOr(&B.ctr->overflow, 4u);
+                        }
+                    }
                 }
                 // defer hits on owners not yet published (one atomic per wave and probe batch)
                 for (int b = 0; b < BATCH; ++b) {
@@ -1269,15 +1349,17 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
     expand_body<S, K, SYM, BATCH, DIST, VERIFY, PRE>(P, PT, B, lo, hi);
 }
 
-// The single-GPU expansion kernel: the lane-superset walk over class-sorted
-// windows of 16 tiles, commuting-diamond skipping, 4 waves/SIMD; PI: probe
-// loads issued during the lane code (K = 8 shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0>
+// The single-GPU expansion kernel: the lane-superset walk over windows of 16
+// tiles presorted by class (PS), commuting-diamond skipping, WPE waves/SIMD, DYN
+// dynamic per-wave work units; PI: probe loads issued during the lane code (K = 8
+// shapes would spill 10-13 VGPRs).
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0,
+          bool EARLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 128)
-        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, DYN>(P, PT, B, lo,
-                                                                                                     hi);
+        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, DYN, false, EARLY>(
+            P, PT, B, lo, hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1288,10 +1370,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // (Round 4: windows presorted by k_window_order, 6 probes, 5 waves/SIMD measured
 // 78.0-78.5 vs 78.6-78.9 ms on the MCraftBench bounds, profiles/r04/ab/sym_variant_r04n.txt:
 // neutral, removed.)
-template <int S, int K, int BATCH, bool WS>
+// PS (round 6, the default): the windows presorted by k_window_order, so the
+// block carries no LDS sort (35 instead of 48 KB: the 96-bit keys' s_ks array
+// had cut the in-kernel sort's block to 3 per CU, i.e. 3 waves/SIMD).
+template <int S, int K, int BATCH, bool WS, bool PS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
 k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
-    if constexpr (WS && Lanes<S, K>::N <= 128)
+    if constexpr (WS && PS && Lanes<S, K>::N <= 128)
+        expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16, 0, false, true>(P, PT, B, lo, hi);
+    else if constexpr (WS && Lanes<S, K>::N <= 128)
         expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16>(P, PT, B, lo, hi);
     else
         expand_body<S, K, true, BATCH, false, false, false>(P, PT, B, lo, hi);
@@ -1303,7 +1390,6 @@ k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi
 // the lane-superset walk over class-sorted windows of 8 tiles (4 waves/SIMD;
 // uncapped it takes 131 VGPRs: 3 waves); every lane for more than 64 lanes.
 // REP: a replicated level (the whole level's records in B.rep).
-// PS: windows of 16 tiles presorted by k_window_order (RMC_DIST_KVARIANT=1, A/B).
 // POOL: the pool flush (flush_pool) with the single-GPU kernel's shape (presorted
 // windows of 16 tiles, early probe loads, the parent's mixes recomputed per lane).
 template <int S, int K, int BATCH, bool REP, bool PS = false, int WPE = 4, bool POOL = false, int DYN = 0>
@@ -1315,8 +1401,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     else if constexpr (POOL && !REP)  // more than 64 lanes: every lane, the pool flush
         expand_body<S, K, false, BATCH, true, false, false, false, false, true, 8, 0, false, false, 0, true>(P, PT, B,
                                                                                                            lo, hi);
-    else if constexpr (Lanes<S, K>::N <= 128 && PS && !REP)
-        expand_body<S, K, false, BATCH, true, false, true, true, true, true, 16, 0, false, true>(P, PT, B, lo, hi);
     else if constexpr (Lanes<S, K>::N <= 128)
         expand_body<S, K, false, BATCH, true, false, true, true, true, true, 8, 0, REP>(P, PT, B, lo, hi);
     else if constexpr (!REP)
@@ -1329,7 +1413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // acc[p] counts the new keys of source p — the states p will send in phase 2,
 // so the receive sizes need no second count exchange.  Keys arrive grouped by
 // source, so a wave mostly adds to one counter (one atomic per source present).
-__global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64* keys, uint8_t* reply, u64 n,
+__global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u32* keys, uint8_t* reply, u64 n,
                                                       const SrcOff so, unsigned long long* acc) {
     u64 pr = 0;
     const int me = (int)__lane_id();
@@ -1337,7 +1421,9 @@ __global__ __launch_bounds__(256) void k_owner_insert(const DevBufs B, const u64
         const u64 t = t0 + threadIdx.x;
         u32 src = 0xFFFFFFFFu;
         if (t < n) {
-            const int isnew = fp_insert_fp(B.table, B.tmask, Fp{keys[2 * t], (u32)keys[2 * t + 1]}, &B.ctr->table_full);
+            const u32* kr = keys + 3 * t;  // {k lo, k hi, s32}
+            const int isnew = fp_insert_fp(B.table, B.tmask, Fp{(u64)kr[0] | ((u64)kr[1] << 32), kr[2]},
+                                           &B.ctr->table_full);
             reply[t] = (uint8_t)isnew;
             if (isnew) {
                 u32 p = 0;
@@ -1747,8 +1833,8 @@ hipError_t launch_owner_insert(const DevBufs& B, const u64* keys, uint8_t* reply
                                unsigned long long* acc, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const u64 blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_owner_insert, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, st, B, keys,
-                       reply, n, so, acc);
+    hipLaunchKernelGGL(k_owner_insert, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, st, B,
+                       reinterpret_cast<const u32*>(keys), reply, n, so, acc);
     return hipGetLastError();
 }
 
@@ -2005,24 +2091,16 @@ static u64 resident_grid(const void* k) {
     return v;
 }
 
-// Expansion kernel variant (RMC_EXPAND_VARIANT, same-box A/B): 20 (default since
-// round 5) = k_expand_sort over windows of 16 tiles presorted by class
-// (k_window_order; no sort in the kernel, so a smaller block), 5 probes in flight
-// per thread, the parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD),
-// each wave taking its next quarter-window from a launch-wide counter; 19 = the
-// same with each block taking a fixed share of the windows (a tie in round 4:
-// 229-232 vs 241-243, 240 vs 228-234 and 229-242 vs 227-234 ms for 19,
-// profiles/r04/ab/expand_dynamic_units_*; with the Drop-first diamond order's
-// fewer probes 20 wins, XL 739.3-741.6 vs 760.1-762.1 ms, profiles/r05/variants/;
-// asking for the next unit one unit ahead measured 245-255 ms, removed);
-// 10 = 6 probes at 5 waves with the mixes held (247-250
-// ms); 15 = 5 probes at 5 waves; 18 = 6 probes at 6 waves (spills); 6 = the
-// round-3 kernel (windows sorted in LDS, 8 probes, 4 waves: 263-269 ms); 1 =
-// every lane of every state (k_expand, what shapes with more than 64 lanes
-// run).  Measured and removed in round 4: 8 probes at 5-6 waves, 4 probes at
-// 5-6 waves, 7 probes at 5 waves (spills or fewer probes in flight), the next
-// tile's state prefetched into registers or by LDS-DMA, 64-B store records.
-// Rounds 2-3's rejected variants are in git history.
+// Expansion kernel variant (RMC_EXPAND_VARIANT): 20 (the default, any value but 1)
+// = k_expand_sort over windows of 16 tiles presorted by class (k_window_order; no
+// sort in the kernel, so a smaller block), 5 probes in flight per thread, the
+// parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD), each wave taking its
+// next quarter-window from a launch-wide counter (XL 739.3-741.6 vs 760.1-762.1 ms
+// for fixed per-block shares, profiles/r05/variants/); 1 = every lane of every
+// state (k_expand, the kernel of shapes with more than 128 lanes).  The variants
+// measured and rejected in rounds 2-5 (6 probes at 5 waves with the mixes held,
+// windows sorted in LDS, fixed shares, 4-8 probes at 4-6 waves, prefetching, 64-B
+// store records) are in git history; their numbers are in DESIGN.md §Kernels.
 static int expand_variant() {
     static int v = [] {
         const char* e = getenv("RMC_EXPAND_VARIANT");
@@ -2031,24 +2109,26 @@ static int expand_variant() {
     return v;
 }
 
-// Sharded expansion kernel (RMC_DIST_KVARIANT, A/B): 0 (default) windows of 8
-// tiles sorted in LDS; 1 windows of 16 tiles presorted by k_window_order; 2 the
-// same with 6 probes in flight per thread at 5 waves/SIMD (default: 293-299 vs
-// 299-304 ms for 0 at one rank, profiles/r04/ab/dist_kvariant_*; 5 probes at 6
-// waves without parent mixes, the single-GPU default's shape, spills 48 B here:
-// 305-307 ms, removed; 2 with dynamic per-wave units: 300-307 vs 298-305 ms on
-// two boxes, profiles/r04/ab/dist_kvariant_2_3_*, removed; with the owner found
-// at flush time, the single-GPU kernel's shape (5 probes, 6 waves, mixes
-// recomputed; 80 B of scratch here) 296-297 ms, with early probe loads 289-291,
-// against 282-283 ms for 2, profiles/r04/ab/dist_kvariant_2_4_6_r04z.txt, removed;
-// the flush deferred to a kernel after the launch (the expansion only lists new
-// successors: 80 VGPRs, no scratch, 6 waves) 283-286 vs 282-286 ms, the parents
-// re-read cold by the separate pass, profiles/r04/ab/dist_deferred_flush_r04h.txt,
-// removed).
+// Sharded expansion kernel (RMC_DIST_KVARIANT): 3 (the default, any value but 0)
+// = the pool flush at the single-GPU kernel's shape (presorted windows, 5 probes,
+// 6 waves/SIMD; remote successors pooled whole and routed by k_route after the
+// launch); 0 = the round-3 send-marker kernel with the flush doing the routing
+// (windows sorted in LDS).  The other variants measured in rounds 3-5
+// (profiles/r04/ab/dist_kvariant_*, profiles/r05/kv4/) are in git history.
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
         return e ? atoi(e) : 3;
+    }();
+    return v;
+}
+
+// SYMMETRY expansion kernel (RMC_SYM_VARIANT): 1 (default) windows presorted by
+// k_window_order; 0 windows sorted in LDS by the kernel itself (round 5).
+static int sym_variant() {
+    static int v = [] {
+        const char* e = getenv("RMC_SYM_VARIANT");
+        return e ? atoi(e) : 1;
     }();
     return v;
 }
@@ -2082,35 +2162,25 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else
+            else if (sym_variant() != 0 && SORTED && B.word) {  // windows presorted by k_window_order
+                if (hipError_t e = launch_window_order(B, a, b, g, 16, st)) return e;
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+                                   PT, B, a, b);
+            } else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
         } else if (verify) {
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
-        } else if (expand_variant() == 6 && SORTED) {  // windows sorted in LDS, 8 probes, 4 waves/SIMD
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, kBatch, K <= 4 ? 1 : 0>));
-        } else if (expand_variant() == 20 && SORTED && B.word) {  // 19 with dynamic per-wave work units
+        } else if (expand_variant() == 21 && SORTED && B.word) {  // 20 with the hash after the skip tests (EARLY)
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1, true>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1, true>));
+        } else if (expand_variant() != 1 && SORTED && B.word) {  // 20: presorted windows, dynamic per-wave units
             const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
             if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
             RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
-        } else if ((expand_variant() == 10 || expand_variant() == 15 || expand_variant() == 18 || expand_variant() == 19) &&
-                   SORTED && B.word) {
-            // windows presorted by k_window_order (no sort in LDS, so a smaller block):
-            // 10 (default) 6 probes in flight per thread at 5 waves/SIMD, 15 5 probes
-            // at 5 waves, 18 (19) 6 (5) probes at 6 waves with the parent's mixes recomputed
-#define RMC_PRESORT(BT, WPE, PRE)                                                                            \
-    {                                                                                                        \
-        const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE, PRE>)); \
-        const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);                          \
-        if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;                             \
-        RMC_EXPAND_LAUNCH((k_expand_sort<S, K, BT, K <= 4 ? 1 : 0, true, WPE, PRE>));                        \
-    }
-            if (expand_variant() == 10) RMC_PRESORT(6, 5, true)
-            else if (expand_variant() == 15) RMC_PRESORT(5, 5, true)
-            else if (expand_variant() == 18) RMC_PRESORT(6, 6, false)
-            else RMC_PRESORT(5, 6, false)
-#undef RMC_PRESORT
         } else {  // 1, and shapes with more than 64 lanes
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
         }
@@ -2118,22 +2188,7 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
     } else if (which == 3) {
         if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
-        else if (dist_kvariant() == 1 && SORTED && B.word) {                      // presorted windows (A/B)
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, kBatch, false, true>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, true>));
-        } else if (dist_kvariant() == 4 && B.pool) {  // 3 with dynamic per-wave units (a tie at one rank:
-                                                       // 224.7-226.0 vs 225.3-225.5 ms, profiles/r05/kv4/)
-            if constexpr (SORTED) {
-                const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true, 1>));
-                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-                if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, true, 1>));
-            } else {
-                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, false, 4, true>));
-            }
-        } else if (dist_kvariant() == 3 && B.pool) {  // the pool flush at the single-GPU kernel's shape
+        else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
             if constexpr (SORTED) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
@@ -2142,11 +2197,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             } else {
                 RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, false, 4, true>));
             }
-        } else if (dist_kvariant() == 2 && SORTED && B.word) {  // presorted, 6 probes in flight, 5 waves/SIMD
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 6, false, true, 5>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 6, false, true, 5>));
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
     } else if (which == 12) {  // a replicated level: records [a, b) of B.rep (plain kernel, <= 64 lanes)
         if constexpr (!SYM && SORTED) RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, true>));
@@ -2175,6 +2225,8 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         hipLaunchKernelGGL((k_rehash<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a, b);
     } else if (which == 6) {
         hipLaunchKernelGGL((k_verify<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, a);
+    } else if (which == 15) {
+        hipLaunchKernelGGL((k_verify_host<S, K, SYM>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B, in, a, b);
     } else if (which == 1) {
         hipLaunchKernelGGL((k_seed<S, K, SYM>), dim3((unsigned)blocks), dim3(256), 0, st, P, PT, B, in, a);
     } else {

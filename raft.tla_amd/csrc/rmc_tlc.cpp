@@ -286,9 +286,11 @@ int main(int argc, char** argv) {
     if (nodeadlock) c.flags &= ~RMC_FLAG_CHECK_DEADLOCK;
     if (verify) c.flags |= RMC_FLAG_VERIFY_STATES;
     // like TLC's states/ directory, expanded levels leave the device when it fills
-    // (single GPU, packed layout; full-state verification keeps every state
-    // resident, and the wide layout of -depth runs of unbounded models has no spill)
-    if (!nospill && !verify && gpus == 1 && rmc_state_bytes(&c) <= 64 * 4) c.flags |= RMC_FLAG_SPILL;
+    // (single GPU, packed layout; under -verify the spilled states keep a host copy
+    // for the comparisons, and checkpoints of such runs stay resident; the wide
+    // layout of -depth runs of unbounded models has no spill)
+    if (!nospill && !(verify && (!ckpt.empty() || !recover.empty())) && gpus == 1 && rmc_state_bytes(&c) <= 64 * 4)
+        c.flags |= RMC_FLAG_SPILL;
     c.device_window = window;
     c.seed = fpseed;
     printf("Model: %d servers, %d values, CONSTRAINT MaxTerm=%d MaxLogLen=%d MaxMsgs=%d MaxDup=%d%s%s\n",
@@ -411,6 +413,9 @@ int main(int argc, char** argv) {
     if (verify)
         printf("Full-state verification: %llu fingerprint hits compared state by state, %llu collisions.\n",
                (unsigned long long)r.verified, (unsigned long long)r.collisions);
+        if (r.verified_spilled)
+            printf("  (%llu of the hits were on states that had left the device window: compared with "
+                   "their host copies)\n", (unsigned long long)r.verified_spilled);
     printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
            (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
     printf("The depth of the complete state graph search is %d.\n", r.depth);

@@ -59,7 +59,8 @@ class Result(C.Structure):
                 ("exchange_seconds", C.c_double), ("stored_here", C.c_uint64),
                 ("spilled", C.c_uint64), ("spills", C.c_uint64), ("spill_seconds", C.c_double),
                 ("parked", C.c_uint64), ("exchange_wait_seconds", C.c_double),
-                ("spill_links_on_device", C.c_int32), ("pad2", C.c_int32)]
+                ("spill_links_on_device", C.c_int32), ("pad2", C.c_int32),
+                ("verified_spilled", C.c_uint64)]
 
 
 class LevelStats(C.Structure):

@@ -509,6 +509,49 @@ def test_spill_trace_equals_the_resident_trace(name, mode, monkeypatch):
     check_trace(model, trace, res.violated_inv, res.violation_depth)
 
 
+@pytest.mark.parametrize("name,slack", [("bounded_full", 1 << 22), ("small", 1 << 16), ("small_sym", 1 << 14)])
+def test_verification_with_spill_is_exact(name, slack, links):
+    """RMC_FLAG_VERIFY_STATES with RMC_FLAG_SPILL: every fingerprint hit is
+    compared with the stored state that owns it, also when that state has left
+    the device window (its host copy, k_verify_host); the oracle's counts, no
+    collision, and every hit compared."""
+    g, cfg = spill_cfg(name, slack)
+    cfg.flags |= rmc.FLAG_VERIFY_STATES
+    res, levels, _ = run(cfg)
+    assert res.spills > 0 and res.spill_links_on_device == (links == "device")
+    assert levels == g["level_new"]
+    assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+    assert res.collisions == 0
+    assert res.verified == res.probes - (res.distinct - 1)
+    assert 0 < res.verified_spilled <= res.verified
+
+
+@pytest.mark.parametrize("bits,name", [(20, "small"), (20, "small_sym")])
+def test_verification_with_spill_reports_collisions(bits, name, links):
+    """A weakened fingerprint under spill: the collisions are reported, including
+    those whose stored state had left the device window."""
+    g, cfg = spill_cfg(name, 1 << 14)
+    cfg.flags |= rmc.FLAG_VERIFY_STATES
+    with rmc.Checker(cfg) as ck:
+        ck.set_fp_bits(bits)
+        res = ck.run()
+    assert res.spills > 0
+    assert res.distinct < g["distinct"]
+    assert res.collisions > 0
+    assert res.verified == res.probes - (res.distinct - 1)
+    assert res.verified_spilled > 0
+
+
+def test_verification_with_spill_refuses_checkpoints(tmp_path):
+    g, cfg = spill_cfg("tiny2_v2", 4096, max_depth=30)
+    cfg.flags |= rmc.FLAG_VERIFY_STATES
+    with rmc.Checker(cfg) as ck:
+        r1 = ck.run()
+        assert r1.depth == 30 and r1.spills > 0 and r1.collisions == 0
+        with pytest.raises(rmc.RmcError, match="VERIFY_STATES and RMC_FLAG_SPILL"):
+            ck.checkpoint(str(tmp_path / "ck"))
+
+
 @pytest.mark.parametrize("first,second", [("spill", "spill"), ("resident", "spill"), ("spill", "resident")])
 def test_spill_checkpoint_and_recover(first, second, tmp_path, links):
     """A spilled search checkpoints its trace links, frontier and fingerprint

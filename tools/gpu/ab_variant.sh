@@ -20,7 +20,7 @@ NV=${#VA[@]}
 for r in $(seq 1 ${ROUNDS:-2}); do
   for i in $(seq 0 $((NV - 1))); do
     v=${VA[$(( (i + r - 1) % NV ))]}
-    env $KNOB=$v timeout -k 10 200 python -u bench.py --no-cpu --no-probe-ceiling --steps 5 --warmup 1 $BENCH_EXTRA > $O/b_${v}_$r.json 2> $O/b_${v}_$r.err || { tail -20 $O/b_${v}_$r.err; exit 1; }
+    env $KNOB=$v timeout -k 10 200 python -u bench.py --no-cpu --no-probe-ceiling --v2-config= --steps ${STEPS:-5} --warmup 1 $BENCH_EXTRA > $O/b_${v}_$r.json 2> $O/b_${v}_$r.err || { tail -20 $O/b_${v}_$r.err; exit 1; }
     python -c "import json; d=json.load(open('$O/b_${v}_$r.json')); print('$KNOB=$v run $r', round(d['ms_per_step'],2), round(d['roofline']['kernel_ms_per_step'],2), d['config']['distinct'], (d['config']['fp_salt_crosscheck'] or {}).get('agrees'))" >> $O/ab.txt || exit 1
   done
 done

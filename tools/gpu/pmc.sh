@@ -1,6 +1,6 @@
 # rocprofv3 evidence for the bench command (the build in the tree):
 # a kernel trace with stats, then one PMC pass per counter group (separate
-# runs: FETCH_SIZE and WRITE_SIZE alone, instruction mix, waits, LDS).
+# runs: FETCH_SIZE and WRITE_SIZE alone, instruction mix, waits, LDS, atomics).
 #   OUT=gpurun_out/<tag> [ENVS="RMC_EXPAND_VARIANT=7"] [CMD="raft.tla_amd/bin/rmc-tlc ..."] bash tools/gpu/pmc.sh
 # (CMD replaces the bench command; it must be the program itself, no wrapper)
 set -o pipefail
@@ -22,3 +22,5 @@ pass write WRITE_SIZE
 pass insts SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_WAVE_CYCLES
 pass waits SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES
 pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
+# atomics: requests at L2 (all), those that go on to memory, and their in-flight sum (latency)
+pass atomics TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCC_EA0_ATOMIC_LEVEL_sum
