@@ -628,97 +628,6 @@ RMC_HD int delta_fp_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S,
     return 1;
 }
 
-// delta_fp_pre split in two (round 6, the EARLY expansion kernels): the
-// CONSTRAINT and whether the successor is structurally its parent (no bag
-// change and the same server word: a stutter) without any mix, so the stutter
-// and commuting-diamond tests run before the hash and a lane that is skipped
-// costs no mixes; then the fingerprint of a survivor (delta_mix_pre).
-template <int S, int K>
-RMC_HD int delta_bounds(const u64 (&w)[S], const u32 (&m)[K], int nmsg0, const Delta& d, const Params& P,
-                        int* nmsg_out, bool* stutter) {
-    int nmsg = nmsg0;
-    bool same = true;
-    if (d.srv >= 0) {
-        if ((d.w_new >> 63) != 0) return 0;  // term 16 or Len 4: beyond every bound
-        if ((int)w_ct(d.w_new) > P.max_term || (int)w_len(d.w_new) > P.max_log) return 0;
-        same = d.w_new == selw<S>(w, d.srv);
-    }
-    if (d.rm >= 0) {
-        same = false;
-        if (m_cnt(selm<K>(m, d.rm)) <= 1) nmsg -= 1;
-    }
-    if (d.has_add) {
-        same = false;
-        u32 cnt = 0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) cnt |= (m[q] && (m[q] & MSG_MASK) == d.add) ? m_cnt(m[q]) : 0u;
-        if ((int)cnt + 1 > P.max_dup) return 0;
-        nmsg += cnt ? 0 : 1;
-    }
-    if (nmsg > P.max_msgs) return 0;
-    *nmsg_out = nmsg;
-    *stutter = same;
-    return 1;
-}
-// The same from the parent's fingerprint alone (the parent's mixes recomputed).
-template <int S, int K>
-RMC_HD Fp delta_mix(const u64 (&w)[S], const u32 (&m)[K], const Fp& h0, const Delta& d) {
-    Fp hh = h0;
-    if (d.srv >= 0) {
-        const u64 wo = selw<S>(w, d.srv);
-        if (d.w_new != wo) {
-            fp_add(hh, hS(d.w_new, (u32)d.srv));
-            fp_sub(hh, hS(wo, (u32)d.srv));
-        }
-    }
-    if (d.rm >= 0) {
-        const u32 sl = selm<K>(m, d.rm);
-        fp_sub(hh, hM(sl));
-        if (m_cnt(sl) > 1) fp_add(hh, hM(sl - CNT_ONE));
-    }
-    if (d.has_add) {
-        int found = -1;
-#pragma unroll
-        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
-        if (found >= 0) {
-            const u32 sl = selm<K>(m, found);
-            fp_add(hh, hM(sl + CNT_ONE));
-            fp_sub(hh, hM(sl));
-        } else {
-            fp_add(hh, hM(d.add | CNT_ONE));
-        }
-    }
-    return hh;
-}
-template <int S, int K>
-RMC_HD Fp delta_mix_pre(const u64 (&w)[S], const u32 (&m)[K], const ParentMix<S, K>& pm, const Delta& d) {
-    Fp hh = pm.h0;
-    if (d.srv >= 0) {
-        const u64 wo = selw<S>(w, d.srv);
-        if (d.w_new != wo) {
-            fp_add(hh, hS(d.w_new, (u32)d.srv));
-            fp_sub(hh, sel64<S>(pm.hw, d.srv));
-        }
-    }
-    if (d.rm >= 0) {
-        const u32 sl = selm<K>(m, d.rm);
-        fp_sub(hh, sel64<K>(pm.hm, d.rm));
-        if (m_cnt(sl) > 1) fp_add(hh, hM(sl - CNT_ONE));
-    }
-    if (d.has_add) {
-        int found = -1;
-#pragma unroll
-        for (int q = 0; q < K; ++q) found = (m[q] && (m[q] & MSG_MASK) == d.add) ? q : found;
-        if (found >= 0) {
-            fp_add(hh, hM(selm<K>(m, found) + CNT_ONE));
-            fp_sub(hh, sel64<K>(pm.hm, found));
-        } else {
-            fp_add(hh, hM(d.add | CNT_ONE));
-        }
-    }
-    return hh;
-}
-
 // ---- wave homogeneity (the expansion kernels' window sort) ------------------------------
 // A wave walks every action lane that ANY of its 64 states enables, so states
 // of one kind (same roles, same number of messages) should sit together.

@@ -33,6 +33,19 @@ constexpr int KW = 64;   // distinct messages in the bag (rmc.h RMC_WIDE_MAX_MSG
 // 17 or less (each step adds at most one log entry and one distinct message)
 // and for CONSTRAINTs of at most 16 entries and messages.
 constexpr int LWC = 16, KWC = 16;
+// The depth-sized record (round 6): 4 log entries and 12 messages, 336 bytes —
+// enough for any state of a BFS bounded at depth 14 or less of a model whose
+// logs and bag no CONSTRAINT bounds (MCraft.cfg as shipped).  Every log entry
+// comes from a ClientRequest, which needs a leader: from Init (every server a
+// term-1 follower) that takes at least Timeout(i), RequestVote(i, i) and
+// RequestVote(i, j), the Receive of both requests, one UpdateTerm (or Timeout)
+// of j to reach i's term, the Receive of both responses and BecomeLeader — 9
+// steps for a quorum of 2 of 3 (5 with the weakened quorum of config 5: one
+// granted vote) — and each later step adds at most one entry, so after n steps
+// a log holds at most n - 9 (n - 5) entries.  The bag holds at most n - 1
+// messages (the first step, Restart or Timeout, adds none).  A successor beyond
+// the record is still caught (W_LOG / W_MSGS: a capacity error, never a silent cut).
+constexpr int LWD = 4, KWD = 12;
 constexpr int TMAX = 255, CMAX = 255;  // largest term / count a field holds
 constexpr uint8_t NIL = 255;           // votedFor = Nil
 
@@ -66,9 +79,11 @@ struct WStateT {
 typedef WMsgT<LW> WMsg;
 typedef WStateT<LW, KW> WState;     // the full record (5,080 B): simulation, rmc_expand, deep BFS
 typedef WStateT<LWC, KWC> WStateC;  // the compact record (904 B): BFS of depth <= 17
+typedef WStateT<LWD, KWD> WStateD;  // the depth-sized record (336 B): BFS of depth <= 14
 static_assert(sizeof(WMsg) == 8 + 2 * LW && sizeof(WMsg) % 8 == 0, "WMsg layout");
-static_assert(sizeof(WState) == 5080 && sizeof(WStateC) == 904, "wide record sizes");
-static_assert(sizeof(WState) % 8 == 0 && sizeof(WStateC) % 8 == 0, "records are read as u64 words");
+static_assert(sizeof(WState) == 5080 && sizeof(WStateC) == 904 && sizeof(WStateD) == 336, "wide record sizes");
+static_assert(sizeof(WState) % 8 == 0 && sizeof(WStateC) % 8 == 0 && sizeof(WStateD) % 8 == 0,
+              "records are read as u64 words");
 constexpr int WMWORDS = (int)(sizeof(WMsg) / 8);
 constexpr int WWORDS = (int)(sizeof(WState) / 8);
 
@@ -241,12 +256,26 @@ template <class T>
 struct WSame {  // a non-deduced parameter type (t may be nullptr)
     typedef T type;
 };
+// What a lane changed (the BFS's incremental fingerprint, wfp_delta): the
+// server whose fields it may have written, the message of s it removed one copy
+// of or duplicated (slot in s), and the slot in t of the message it added.
+struct WDelta {
+    int srv, rm, dup, add_at;
+};
+template <class St>
+RMC_HD int wfind(const St& t, const typename St::Msg& m) {
+    for (int k = 0; k < t.nmsg; ++k)
+        if (wmsg_cmp(t.msg[k], m) == 0) return k;
+    return -1;
+}
 template <class Bag = SerialBag, class St = WState>
-RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::type* t, bool pre = false) {
+RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::type* t, bool pre = false,
+                 WDelta* dl = nullptr) {
     typedef typename St::Msg WMsg;
     constexpr int LW = St::kLW;
     const int S = M.S;
     const int f = M.L.family(lane), x = lane - M.L.off[f];
+    if (dl) *dl = WDelta{f <= 5 ? (f == 2 ? -1 : f == 4 ? x / VMAX : x) : -1, -1, -1, -1};
     switch (f) {
     case 0: {  // Restart(i) :136-143 — always enabled
         const int i = x;
@@ -290,7 +319,9 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
         const int fit = Bag::fits(s, m);
         if (fit != W_ON) return fit;
         if (!pre) wcopy_state(*t, s);
-        return Bag::add(*t, m);
+        const int r = Bag::add(*t, m);
+        if (dl) dl->add_at = wfind(*t, m);
+        return r;
     }
     case 3: {  // BecomeLeader(i) :195-203
         const int i = x;
@@ -354,12 +385,15 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
         const int fit = Bag::fits(s, m);
         if (fit != W_ON) return fit;
         if (!pre) wcopy_state(*t, s);
-        return Bag::add(*t, m);
+        const int r = Bag::add(*t, m);
+        if (dl) dl->add_at = wfind(*t, m);
+        return r;
     }
     case 7: {  // Receive(m) :388-403 for bag slot x
         if (x >= s.nmsg) return W_OFF;
         const WMsg& m = s.msg[x];
         const int i = m.dst, j = m.src, ct = s.ct[i];
+        if (dl) dl->srv = i;  // (a branch that leaves m in the bag: only the server changes)
         if (m.term > ct) {  // UpdateTerm :373-379 — m stays
             if (!t) return W_ON;
             if (!pre) wcopy_state(*t, s);
@@ -389,6 +423,10 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
             if (grant) t->vf[i] = (uint8_t)j;
             Bag::remove_at(*t, x);
             Bag::add(*t, r);
+            if (dl) {
+                dl->rm = x;
+                dl->add_at = wfind(*t, r);
+            }
             return W_ON;
         }
         if (m.type == RVP) {
@@ -399,6 +437,7 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
                 if (m.a) t->vG[i] = (uint8_t)(s.vG[i] | (1u << j));
             }  // else DropStaleResponse :382-385
             Bag::remove_at(*t, x);
+            if (dl) dl->rm = x;
             return W_ON;
         }
         if (m.type == AEQ) {  // HandleAppendEntriesRequest :347-356
@@ -417,6 +456,10 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
                 if (!pre) wcopy_state(*t, s);
                 Bag::remove_at(*t, x);
                 Bag::add(*t, r);
+                if (dl) {
+                    dl->rm = x;
+                    dl->add_at = wfind(*t, r);
+                }
                 return W_ON;
             }
             if (s.st[i] == CANDIDATE) {  // ReturnToFollowerState :295-299 — m stays
@@ -439,6 +482,10 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
                 if (!pre) wcopy_state(*t, s);
                 Bag::remove_at(*t, x);
                 Bag::add(*t, r);
+                if (dl) {
+                    dl->rm = x;
+                    dl->add_at = wfind(*t, r);
+                }
                 return W_ON;
             }
             if (len >= index) {  // ConflictAppendEntriesRequest :319-325 — drops the LAST entry, m stays
@@ -472,6 +519,7 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
             }
         }  // else DropStaleResponse
         Bag::remove_at(*t, x);
+        if (dl) dl->rm = x;
         return W_ON;
     }
     case 8: {  // DuplicateMessage(m) :410-412
@@ -480,6 +528,7 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
         if (!t) return W_ON;
         if (!pre) wcopy_state(*t, s);
         t->cnt[x] = (uint8_t)(s.cnt[x] + 1);
+        if (dl) dl->dup = x;
         return W_ON;
     }
     default: {  // DropMessage(m) :415-417
@@ -487,6 +536,7 @@ RMC_HD int wlane(const WModel& M, const St& s, int lane, typename WSame<St>::typ
         if (!t) return W_ON;
         if (!pre) wcopy_state(*t, s);
         Bag::remove_at(*t, x);
+        if (dl) dl->rm = x;
         return W_ON;
     }
     }
@@ -691,19 +741,82 @@ RMC_HD int uniform_draw(const u64 (&en)[NC], const u64 (&excl)[NC], u64& rs) {
     return -1;
 }
 
-// Fingerprint of a canonical record (every byte; salted like the packed one):
-// k the chained mix over the words, s the sum of smix over the chain's states
-// (raft_packed.h Fp: the second 32 bits the fingerprint set folds in).
+// Fingerprint of a canonical record (salted like the packed one), round 6: like
+// the packed layout's, an order-free sum over components — each server's fields
+// (its log up to its length) and each message with its count, every component
+// a short chained mix of its own bytes — so a successor's fingerprint is its
+// parent's minus the components a lane changed plus their new values
+// (wfp_delta: about 10 mixes instead of the whole record's 62-635 words).
+// k = sum of the components mod 2^64, s = sum of their smix (raft_packed.h Fp).
+// Unused log entries and message fields are 0 in the canonical form, so the
+// record's capacity does not enter.
 template <class St>
-RMC_HD Fp wfp(const St& s, u64 salt) {
-    const u64* w = reinterpret_cast<const u64*>(&s);
-    u64 h = 0x6A09E667F3BCC909ull ^ salt;
-    u32 s2 = 0;
-    for (int k = 0; k < (int)(sizeof(St) / 8); ++k) {
-        h = mix64(h ^ (w[k] + (u64)k * 0x9E3779B97F4A7C15ull));
-        s2 += smix(h);
+RMC_HD u64 wcomp_srv(const St& s, int i, u64 salt) {
+    u64 w0 = (u64)s.ct[i] | ((u64)s.st[i] << 8) | ((u64)s.vf[i] << 16) | ((u64)s.ci[i] << 24) |
+             ((u64)s.len[i] << 32) | ((u64)s.vR[i] << 40) | ((u64)s.vG[i] << 48) | ((u64)i << 56);
+    u64 w1 = 0, w2 = 0;
+    for (int j = 0; j < WS; ++j) {
+        w1 |= (u64)s.ni[i][j] << (8 * j);
+        w2 |= (u64)s.mi[i][j] << (8 * j);
     }
-    return Fp{h, s2};
+    u64 h = mix64(w0 ^ salt ^ 0x243F6A8885A308D3ull);
+    h = mix64(h ^ w1 ^ (w2 << 40));
+    h = mix64(h ^ (w2 >> 24));
+    const int n = s.len[i];
+    for (int e = 0; e < n; e += 4) {  // 4 entries (8 bytes) per word
+        u64 lw = 0;
+        for (int q = 0; q < 4 && e + q < n; ++q)
+            lw |= ((u64)s.log[i][e + q].term | ((u64)s.log[i][e + q].value << 8)) << (16 * q);
+        h = mix64(h ^ lw ^ ((u64)e << 58));
+    }
+    return h;
+}
+template <class Mg>
+RMC_HD u64 wcomp_msg(const Mg& m, int cnt, u64 salt) {
+    const u64 hdr = (u64)m.type | ((u64)m.term << 8) | ((u64)m.src << 16) | ((u64)m.dst << 24) |
+                    ((u64)(uint8_t)m.a << 32) | ((u64)m.b << 40) | ((u64)m.c << 48) | ((u64)m.n << 56);
+    u64 h = mix64(hdr ^ salt ^ 0x13198A2E03707344ull);
+    h = mix64(h ^ (u64)(unsigned)cnt ^ 0xA4093822299F31D0ull);
+    const int n = m.n;
+    for (int e = 0; e < n; e += 4) {
+        u64 lw = 0;
+        for (int q = 0; q < 4 && e + q < n; ++q)
+            lw |= ((u64)m.e[e + q].term | ((u64)m.e[e + q].value << 8)) << (16 * q);
+        h = mix64(h ^ lw ^ ((u64)e << 58));
+    }
+    return h;
+}
+template <class St>
+RMC_HD Fp wfp(const St& s, u64 salt, int S = WS) {
+    Fp h{0, 0};
+    for (int i = 0; i < S; ++i) fp_add(h, wcomp_srv(s, i, salt));
+    for (int q = 0; q < s.nmsg; ++q) fp_add(h, wcomp_msg(s.msg[q], s.cnt[q], salt));
+    return h;
+}
+// The successor t = lane(s) from s's fingerprint h0 and what the lane changed.
+template <class St>
+RMC_HD Fp wfp_delta(const St& s, const St& t, const Fp& h0, const WDelta& d, u64 salt) {
+    Fp h = h0;
+    if (d.srv >= 0) {
+        fp_sub(h, wcomp_srv(s, d.srv, salt));
+        fp_add(h, wcomp_srv(t, d.srv, salt));
+    }
+    if (d.rm >= 0) {
+        const int c = s.cnt[d.rm];
+        fp_sub(h, wcomp_msg(s.msg[d.rm], c, salt));
+        if (c > 1) fp_add(h, wcomp_msg(s.msg[d.rm], c - 1, salt));
+    }
+    if (d.dup >= 0) {
+        const int c = s.cnt[d.dup];
+        fp_sub(h, wcomp_msg(s.msg[d.dup], c, salt));
+        fp_add(h, wcomp_msg(s.msg[d.dup], c + 1, salt));
+    }
+    if (d.add_at >= 0) {
+        const int c = t.cnt[d.add_at];
+        fp_add(h, wcomp_msg(t.msg[d.add_at], c, salt));
+        if (c > 1) fp_sub(h, wcomp_msg(t.msg[d.add_at], c - 1, salt));
+    }
+    return h;
 }
 
 }  // namespace wide

@@ -1023,10 +1023,12 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     }
     D.ag_cap = 4096;
     D.debug = getenv("RMC_DIST_DEBUG") != nullptr;
-    // rounds per large level: 2 at world > 1 so one round's exchange overlaps the next
-    // round's expansion; 1 at world 1, where no round exchanges anything (283.4-283.7
-    // vs 289.8-294.0 ms on the one-rank bench, profiles/r04/ab/dist_split_r04u.txt)
-    D.split = world > 1 ? 2 : 1;
+    // rounds per large level: 4 at world > 1 (round 6; 2 before), so each round's
+    // exchange overlaps the next round's expansion and only the last quarter of a
+    // level's exchange is exposed; 1 at world 1, where no round exchanges anything
+    // (283.4-283.7 vs 289.8-294.0 ms for 2 on the one-rank bench,
+    // profiles/r04/ab/dist_split_r04u.txt)
+    D.split = world > 1 ? 4 : 1;
     if (const char* s = getenv("RMC_DIST_SPLIT")) D.split = std::max(1, std::min(64, atoi(s)));
     if (const char* s = getenv("RMC_DIST_OVERLAP")) D.overlap = atoi(s) != 0;
     if (c->sh.verify) D.overlap = 0;  // rounds in order: each publishes its states before the next compares

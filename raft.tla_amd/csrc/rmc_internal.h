@@ -172,8 +172,8 @@ hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int 
 // ---- the wide layout (raft_wide.h, rmc_wide.hip) ------------------------------------
 namespace wide {
 struct WideBufs {
-    void* store;      // wide records (WState, or WStateC when compact); levels are contiguous ranges
-    int compact;      // 1: the store holds compact records (raft_wide.h WStateC)
+    void* store;      // wide records (WState, WStateC or WStateD); levels are contiguous ranges
+    int compact;      // the store's record: 0 WState, 1 the compact WStateC, 2 the depth-sized WStateD
     u64* parent;      // parent index per state (~0 for initial states)
     uint8_t* act;     // lane that produced the state (255 for initial states)
     u64* table;       // fingerprint set (wfp keys), power-of-two slots

@@ -829,12 +829,8 @@ __device__ __forceinline__ void flush_pool(const Params& P, const DevBufs& B, u6
 //   all of them and probes, stores and counts only the successors it owns.
 template <int S, int K, bool SYM, int BATCH, bool DIST, bool VERIFY = false, bool PRE = false, bool SORT = false,
           bool DIA = false, bool MARK = false, int WTILES = 8, int PIPE = 0, bool REP = false, bool PRESORT = false,
-          int DYN = 0, bool POOL = false, bool EARLY = false>
+          int DYN = 0, bool POOL = false>
 __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT, const DevBufs& B, u64 lo, u64 hi) {
-    // EARLY: the CONSTRAINT, the structural stutter and the commuting-diamond
-    // test before the lane's hash (delta_bounds, delta_mix_pre): a skipped
-    // successor costs no mixes (the same probes as without it)
-    static_assert(!EARLY || (DIA && !REP && !DIST), "EARLY: the single-GPU diamond kernel");
     static_assert(!MARK || (DIST && !VERIFY && !SYM), "send markers: the plain sharded kernel only");
     static_assert(!POOL || (MARK && !REP), "the pool flush: the send-marker kernel");
     constexpr bool SENTC = DIST && !MARK;  // the lossy sent-cache + (key, dest) list entries
@@ -1076,24 +1072,6 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                             } else {
                                 h = canon_delta<S, K>(w, m, sbase, d, PT.code, PT.np);
                             }
-                        }
-                    } else if (EARLY && en) {
-                        int nmb = 0, nm0 = 0;
-                        bool stut = false;
-                        if constexpr (PRE) {
-                            nm0 = pmx.nmsg;
-                        } else {
-#pragma unroll
-                            for (int q = 0; q < K; ++q) nm0 += m[q] ? 1 : 0;
-                        }
-                        in_model = delta_bounds<S, K>(w, m, nm0, d, P, &nmb, &stut);
-                        if (in_model && (stut || (SORT ? diamond_skip_desc<S, K>(m, lane, P.ldesc[SORT ? lane : 0], d,
-                                                                                  nmb, dm)
-                                                       : diamond_skip<S, K>(m, lane, d, nmb, dm, P))))
-                            in_model = 0;
-                        if (in_model) {
-                            if constexpr (PRE) h = delta_mix_pre<S, K>(w, m, pmx, d);
-                            else h = delta_mix<S, K>(w, m, h0, d);
                         }
                     } else if (en) {
                         int nmb = 0;
@@ -1353,13 +1331,12 @@ __global__ __launch_bounds__(256) void k_expand(const Params P, const PermTable 
 // tiles presorted by class (PS), commuting-diamond skipping, WPE waves/SIMD, DYN
 // dynamic per-wave work units; PI: probe loads issued during the lane code (K = 8
 // shapes would spill 10-13 VGPRs).
-template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0,
-          bool EARLY = false>
+template <int S, int K, int BATCH, int PI, bool PS = false, int WPE = 4, bool PRE = true, int DYN = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_expand_sort(
     const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (Lanes<S, K>::N <= 128)
-        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, DYN, false, EARLY>(
-            P, PT, B, lo, hi);
+        expand_body<S, K, false, BATCH, false, false, PRE, true, true, false, 16, PI, false, PS, DYN>(P, PT, B, lo,
+                                                                                                     hi);
 }
 
 // SYMMETRY expansion: each lane fingerprints its successor under the
@@ -1373,11 +1350,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // PS (round 6, the default): the windows presorted by k_window_order, so the
 // block carries no LDS sort (35 instead of 48 KB: the 96-bit keys' s_ks array
 // had cut the in-kernel sort's block to 3 per CU, i.e. 3 waves/SIMD).
-template <int S, int K, int BATCH, bool WS, bool PS = false>
+template <int S, int K, int BATCH, bool WS, bool PS = false, int DYN = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
 k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && PS && Lanes<S, K>::N <= 128)
-        expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16, 0, false, true>(P, PT, B, lo, hi);
+        expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16, 0, false, true, DYN>(P, PT, B, lo,
+                                                                                                       hi);
     else if constexpr (WS && Lanes<S, K>::N <= 128)
         expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16>(P, PT, B, lo, hi);
     else
@@ -2162,20 +2140,23 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else if (sym_variant() != 0 && SORTED && B.word) {  // windows presorted by k_window_order
-                if (hipError_t e = launch_window_order(B, a, b, g, 16, st)) return e;
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED, true>), dim3((unsigned)g), dim3(256), 0, st, P,
+            else if (sym_variant() >= 2 && SORTED && B.word) {  // 1 with dynamic per-wave units, resident grid
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_sym<S, K, kBatch, SORTED, true, 1>));
+                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp) * (u64)(sym_variant() - 1);
+                const u64 gs = blocks < want ? blocks : want;
+                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED, true, 1>), dim3((unsigned)gs), dim3(256), 0, st,
+                                   P, PT, B, a, b);
+            } else if (sym_variant() != 0 && SORTED && B.word) {  // windows presorted by k_window_order
+                const u64 gs = expand_grid_env() ? (blocks < expand_grid_env() ? blocks : expand_grid_env()) : g;
+                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
+                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED, true>), dim3((unsigned)gs), dim3(256), 0, st, P,
                                    PT, B, a, b);
             } else
                 hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED>), dim3((unsigned)g), dim3(256), 0, st, P, PT, B,
                                    a, b);
         } else if (verify) {
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
-        } else if (expand_variant() == 21 && SORTED && B.word) {  // 20 with the hash after the skip tests (EARLY)
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1, true>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1, true>));
         } else if (expand_variant() != 1 && SORTED && B.word) {  // 20: presorted windows, dynamic per-wave units
             const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
             const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);

@@ -57,20 +57,29 @@ void fill_wide_model(rmc_ctx* c) {
 
 int wide_family(const rmc_ctx* c, int lane) { return lane == 255 ? -1 : c->WM.L.family(lane); }
 
-// The BFS store holds compact records (raft_wide.h WStateC: 16 log entries,
-// 16 messages) when no state of the run can need more: each field is either
-// bounded by a CONSTRAINT within the record (a successor beyond it is out of
-// the model anyway) or unbounded in a run of at most 17 levels (one step adds
-// at most one log entry and one distinct message).  RMC_WIDE_COMPACT=0/1
-// overrides (A/B, tests).
-static bool wide_compact(const rmc_config& g) {
-    if (const char* e = getenv("RMC_WIDE_COMPACT")) return atoi(e) != 0;
+// The BFS store's record (WideBufs.compact): the smallest that no state of the
+// run can outgrow — each field either bounded by a CONSTRAINT within the record
+// (a successor beyond it is out of the model anyway) or unbounded in a run of
+// few enough levels.  2: the depth-sized WStateD (4 entries, 12 messages; after
+// n steps a log holds at most n - 9 entries, n - 5 under the weakened quorum,
+// and the bag at most n - 1 messages: raft_wide.h), 1: the compact WStateC (16,
+// 16; one step adds at most one entry and one message), 0: the full WState.
+// RMC_WIDE_COMPACT=0/1/2 overrides (A/B, tests).
+static int wide_compact(const rmc_config& g) {
+    if (const char* e = getenv("RMC_WIDE_COMPACT")) return std::max(0, std::min(2, atoi(e)));
     const int steps = g.max_depth > 0 ? g.max_depth - 1 : 1 << 30;
-    const bool logs = ((g.flags & RMC_FLAG_UNBOUNDED_LOG) == 0 && g.max_log_len <= LWC) || steps <= LWC;
-    const bool msgs = ((g.flags & RMC_FLAG_UNBOUNDED_MSGS) == 0 && g.max_msgs <= KWC) || steps <= KWC;
-    return logs && msgs;
+    const bool blog = (g.flags & RMC_FLAG_UNBOUNDED_LOG) == 0, bmsg = (g.flags & RMC_FLAG_UNBOUNDED_MSGS) == 0;
+    const int lead = (g.flags & RMC_FLAG_BUG_QUORUM) ? 5 : 9;  // steps before a first log entry can exist
+    if (((blog && g.max_log_len <= LWD) || steps - lead <= LWD) && ((bmsg && g.max_msgs <= KWD) || steps - 1 <= KWD))
+        return 2;
+    const bool logs = (blog && g.max_log_len <= LWC) || steps <= LWC;
+    const bool msgs = (bmsg && g.max_msgs <= KWC) || steps <= KWC;
+    return logs && msgs ? 1 : 0;
 }
-size_t wide_record_bytes(const rmc_config& g) { return wide_compact(g) ? sizeof(WStateC) : sizeof(WState); }
+static size_t record_bytes(int kind) {
+    return kind == 2 ? sizeof(WStateD) : kind == 1 ? sizeof(WStateC) : sizeof(WState);
+}
+size_t wide_record_bytes(const rmc_config& g) { return record_bytes(wide_compact(g)); }
 
 // ---- codec ----------------------------------------------------------------------
 int encode_wide(const rmc_ctx* c, const rmc_state_view& v, WState* out, std::string* why) {
@@ -224,8 +233,8 @@ void decode_wide(const rmc_ctx* c, const St& s, rmc_state_view* v) {
 // ---- context ----------------------------------------------------------------------
 int create_wide(rmc_ctx* c) {
     fill_wide_model(c);
-    const bool compact = wide_compact(c->cfg);
-    const u64 rec = compact ? sizeof(WStateC) : sizeof(WState);
+    const int compact = wide_compact(c->cfg);
+    const u64 rec = record_bytes(compact);
     const u64 per_state = rec + 8 + 1;
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
@@ -239,7 +248,7 @@ int create_wide(rmc_ctx* c) {
     B = WideBufs{};
     B.cap = cap;
     B.tmask = slots - 1;
-    B.compact = compact ? 1 : 0;
+    B.compact = compact;
     if (hipMalloc(&B.store, cap * rec) != hipSuccess || hipMalloc(&B.parent, cap * 8) != hipSuccess ||
         hipMalloc(&B.act, cap) != hipSuccess || hipMalloc(&B.table, slots * 8) != hipSuccess ||
         hipMalloc(&B.ctr, sizeof(Counters)) != hipSuccess || hipMalloc(&c->w_staged, sizeof(WState)) != hipSuccess)
@@ -279,9 +288,12 @@ int run_bfs_wide(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (int rc = reset_counters(c, false)) return rc;
     WState init;
     WStateC initc;
+    WStateD initd;
     winit(c->WM, init);
     winit(c->WM, initc);
-    if (B.compact) HIPCHK(c, hipMemcpyAsync(c->w_staged, &initc, sizeof initc, hipMemcpyHostToDevice, c->st));
+    winit(c->WM, initd);
+    if (B.compact == 2) HIPCHK(c, hipMemcpyAsync(c->w_staged, &initd, sizeof initd, hipMemcpyHostToDevice, c->st));
+    else if (B.compact) HIPCHK(c, hipMemcpyAsync(c->w_staged, &initc, sizeof initc, hipMemcpyHostToDevice, c->st));
     else HIPCHK(c, hipMemcpyAsync(c->w_staged, &init, sizeof init, hipMemcpyHostToDevice, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));  // (the staging copies live on this stack frame)
     HIPCHK(c, launch_wseed(c->WM, B, c->w_staged, 1, c->st));
@@ -380,7 +392,11 @@ int trace_wide(rmc_ctx* c, rmc_state_view* states, int32_t* families, int32_t* i
     std::reverse(acts.begin(), acts.end());
     *len = chain.size();
     for (size_t q = 0; q < chain.size() && q < cap; ++q) {
-        if (c->WB.compact) {
+        if (c->WB.compact == 2) {
+            WStateD s;
+            HIPCHK(c, hipMemcpy(&s, static_cast<const WStateD*>(c->WB.store) + chain[q], sizeof s, hipMemcpyDeviceToHost));
+            if (states) decode_wide(c, s, &states[q]);
+        } else if (c->WB.compact) {
             WStateC s;
             HIPCHK(c, hipMemcpy(&s, static_cast<const WStateC*>(c->WB.store) + chain[q], sizeof s, hipMemcpyDeviceToHost));
             if (states) decode_wide(c, s, &states[q]);

@@ -54,7 +54,7 @@ __device__ __forceinline__ void w_store(const WModel& M, const WideBufs& B, u64 
 template <class St>
 __global__ __launch_bounds__(256) void k_wseed(const WModel M, const WideBufs B, const St* staged, u64 n) {
     for (u64 t = (u64)blockIdx.x * 256ull + threadIdx.x; t < n; t += (u64)gridDim.x * 256ull) {
-        if (!w_insert(B.table, B.tmask, wfp(staged[t], B.salt), &B.ctr->table_full)) continue;
+        if (!w_insert(B.table, B.tmask, wfp(staged[t], B.salt, M.S), &B.ctr->table_full)) continue;
         const u64 ni = atomicAdd((unsigned long long*)&B.ctr->count, 1ull);
         if (ni >= B.cap) {
             atomicOr(&B.ctr->overflow, 1u);
@@ -67,18 +67,26 @@ __global__ __launch_bounds__(256) void k_wseed(const WModel M, const WideBufs B,
 // One BFS level: every lane of every frontier state [lo, hi).  Successors
 // outside the CONSTRAINT count as generated and are dropped; a successor the
 // layout cannot hold in a field no CONSTRAINT bounds stops the search
-// (Counters.overflow bits 8-11, the field).
+// (Counters.overflow bits 8-11, the field).  Round 6: the parent's fingerprint
+// once per state and each successor's from it (wfp_delta: the components the
+// lane changed), the bag families walked only over the state's messages, and
+// stuttering successors (the parent's fingerprint) not probed.
 template <class St>
 __global__ __launch_bounds__(256) void k_wexpand(const WModel M, const WideBufs B, u64 lo, u64 hi) {
     u64 gen = 0, probes = 0;
     u32 bad = 0;
-    const int nl = M.L.off[10];
+    const int o7 = M.L.off[7];
     for (u64 i = lo + (u64)blockIdx.x * 256ull + threadIdx.x; i < hi; i += (u64)gridDim.x * 256ull) {
         St s, t;
         wcopy_state(s, static_cast<const St*>(B.store)[i]);
+        const Fp h0 = wfp(s, B.salt, M.S);
         u32 g = 0;
-        for (int lane = 0; lane < nl; ++lane) {
-            const int r = wlane(M, s, lane, &t);
+        // lanes of families 0-6, then the three bag families over slots [0, nmsg)
+        const int nb = s.nmsg, nl = o7 + 3 * nb;
+        for (int q = 0; q < nl; ++q) {
+            const int lane = q < o7 ? q : M.L.off[7 + (q - o7) / nb] + (q - o7) % nb;
+            WDelta dl;
+            const int r = wlane(M, s, lane, &t, false, &dl);
             if (r == W_OFF) continue;
             ++g;
             if (r != W_ON) {  // beyond the layout: an error for a field no CONSTRAINT bounds,
@@ -86,8 +94,10 @@ __global__ __launch_bounds__(256) void k_wexpand(const WModel M, const WideBufs 
                 continue;
             }
             if (!win_model(M, t)) continue;
+            const Fp h = wfp_delta(s, t, h0, dl, B.salt);
+            if (h.k == h0.k && h.s == h0.s) continue;  // a stutter (or a full-fingerprint twin of the parent)
             ++probes;
-            if (!w_insert(B.table, B.tmask, wfp(t, B.salt), &B.ctr->table_full)) continue;
+            if (!w_insert(B.table, B.tmask, h, &B.ctr->table_full)) continue;
             const u64 ni = atomicAdd((unsigned long long*)&B.ctr->count, 1ull);
             if (ni >= B.cap) {
                 atomicOr(&B.ctr->overflow, 1u);
@@ -122,7 +132,7 @@ __global__ __launch_bounds__(64) void k_wlist(const WModel M, const WState* in, 
         w.code = r;
         const int inm = r == W_ON && win_model(M, t);
         w.in_model = inm;
-        w.fp = inm ? wfp(t, salt).k : 0ull;
+        w.fp = inm ? wfp(t, salt, M.S).k : 0ull;
         if (inm) wcopy_state(w.state, t);
         else wzero(&w.state, (int)sizeof(WState));
     }
@@ -429,7 +439,10 @@ static unsigned grid_for(u64 n, u64 threads, u64 maxg) {
 
 hipError_t launch_wseed(const WModel& M, const WideBufs& B, const void* staged, u64 n, hipStream_t st) {
     if (!n) return hipSuccess;
-    if (B.compact)
+    if (B.compact == 2)
+        hipLaunchKernelGGL(k_wseed<WStateD>, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, M, B,
+                           static_cast<const WStateD*>(staged), n);
+    else if (B.compact)
         hipLaunchKernelGGL(k_wseed<WStateC>, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, M, B,
                            static_cast<const WStateC*>(staged), n);
     else
@@ -439,7 +452,9 @@ hipError_t launch_wseed(const WModel& M, const WideBufs& B, const void* staged, 
 }
 hipError_t launch_wexpand(const WModel& M, const WideBufs& B, u64 lo, u64 hi, hipStream_t st) {
     if (hi <= lo) return hipSuccess;
-    if (B.compact)
+    if (B.compact == 2)
+        hipLaunchKernelGGL(k_wexpand<WStateD>, dim3(grid_for(hi - lo, 256, 4096)), dim3(256), 0, st, M, B, lo, hi);
+    else if (B.compact)
         hipLaunchKernelGGL(k_wexpand<WStateC>, dim3(grid_for(hi - lo, 256, 4096)), dim3(256), 0, st, M, B, lo, hi);
     else
         hipLaunchKernelGGL(k_wexpand<WState>, dim3(grid_for(hi - lo, 256, 4096)), dim3(256), 0, st, M, B, lo, hi);

@@ -38,11 +38,15 @@ def cfg_from(p, capacity=1 << 20):
                            max_depth=p["max_depth"], state_capacity=capacity)
 
 
-@pytest.fixture(params=["full", "compact"])
+RECORDS = {"full": ("0", 5080), "compact": ("1", 904), "depth": ("2", 336)}
+
+
+@pytest.fixture(params=["full", "compact", "depth"])
 def wide_record(request, monkeypatch):
-    """The BFS store's record: full (5,080 B) or compact (904 B, WStateC)."""
-    monkeypatch.setenv("RMC_WIDE_COMPACT", "1" if request.param == "compact" else "0")
-    return 904 if request.param == "compact" else 5080
+    """The BFS store's record: full (5,080 B), compact (904 B, WStateC) or
+    depth-sized (336 B, WStateD)."""
+    monkeypatch.setenv("RMC_WIDE_COMPACT", RECORDS[request.param][0])
+    return RECORDS[request.param][1]
 
 
 @pytest.mark.parametrize("name", ["tiny2", "tiny2_v2", "small", "s4_prefix10", "msgs5_dup2_prefix9"])
@@ -86,7 +90,7 @@ def test_reference_mcraft_cfg_under_a_depth_bound():
         c = rmc.Config.from_buffer_copy(base)
         c.max_depth = depth
         c.state_capacity = 1 << 18  # 56,761 states at depth 8
-        assert rmc.native().rmc_state_bytes(c) == 904  # 7 steps: the compact record holds every state
+        assert rmc.native().rmc_state_bytes(c) == 336  # 7 steps: the depth-sized record holds every state
         with rmc.Checker(c) as ck:
             r = ck.run()
             levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
@@ -98,7 +102,7 @@ def test_reference_mcraft_cfg_under_a_depth_bound():
         assert levels == ln, depth
 
 
-@pytest.mark.parametrize("depth,record", [(12, "compact"), (10, "full")])
+@pytest.mark.parametrize("depth,record", [(12, "depth"), (12, "compact"), (10, "full")])
 def test_reference_mcraft_cfg_deeper_on_the_record_sized_from_the_run(depth, record, monkeypatch):
     """MCraft.cfg as shipped (no CONSTRAINT) to depth 12 —
     24.6 M states, beyond the 8 levels the full 5-KB record was tested to — on
@@ -108,12 +112,12 @@ def test_reference_mcraft_cfg_deeper_on_the_record_sized_from_the_run(depth, rec
     (tests/golden/oracle_levels.json mcraft_shipped_d12).  One GPU completes
     depth 13 on the compact record (110.9 M states; profiles/r05/wide5/)."""
     g = GOLDEN["mcraft_shipped_d12"]
-    monkeypatch.setenv("RMC_WIDE_COMPACT", "1" if record == "compact" else "0")
+    monkeypatch.setenv("RMC_WIDE_COMPACT", RECORDS[record][0])
     cfgp = os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg")
     c, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, depth_bounded=True)
     c.max_depth = depth
     c.state_capacity = int(sum(g["level_new"][:depth]) * 1.1) + 4096
-    assert rmc.native().rmc_state_bytes(c) == (904 if record == "compact" else 5080)
+    assert rmc.native().rmc_state_bytes(c) == RECORDS[record][1]
     with rmc.Checker(c) as ck:
         r = ck.run()
         levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
@@ -123,6 +127,29 @@ def test_reference_mcraft_cfg_deeper_on_the_record_sized_from_the_run(depth, rec
     assert r.generated == sum(g["level_generated"][:depth])
     if depth == 12:
         assert (r.distinct, r.generated) == (g["distinct"], g["generated"])
+
+
+def test_reference_mcraft_cfg_depth_13_and_14_on_one_gpu():
+    """MCraft.cfg as shipped on the depth-sized record
+    (the front-end's default for depth <= 14): depth 13 gives the counts the
+    compact record measured in round 5 (profiles/r05/cli/
+    cli_config1_mcraft_as_shipped_depth13.txt), every level to 12 equal to the
+    oracle, and depth 14 completes on one GPU."""
+    g = GOLDEN["mcraft_shipped_d12"]
+    cfgp = os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg")
+    c, _, _ = rmc.model_from_files(cfgp, builtin_raft=True, depth_bounded=True)
+    for depth in (13, 14):
+        c.max_depth = depth
+        c.state_capacity = 0
+        assert rmc.native().rmc_state_bytes(c) == 336
+        with rmc.Checker(c) as ck:
+            r = ck.run()
+            levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+        assert levels[:12] == g["level_new"] and r.depth == depth
+        if depth == 13:
+            assert (r.distinct, r.generated) == (110878535, 542251150)
+        else:
+            assert r.distinct > 110878535 and r.left_on_queue == levels[-1]
 
 
 def _walk_states(model, n, depth, seed):

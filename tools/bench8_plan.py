@@ -78,6 +78,9 @@ def extrapolate(prefix_new, shape_new, stretch):
     return [int(v) for v in x]
 
 
+SPLIT = 4  # rmc_dist.cpp D.split at world > 1 (RMC_DIST_SPLIT)
+
+
 def slots_for(cap):
     s = 1
     while s < 2 * cap:
@@ -187,9 +190,10 @@ def main():
             St[L].update({r: F * share[r] for r in range(n)})
             rho = kappa / n
             per_round = min(1 << 25, kcap / max(rho, 0.02))
-            # librmc: at world > 1 a level of >= 2^21 states per rank takes at least
-            # 2 rounds (D.split), so one round's exchange overlaps the next's expansion
-            split = 2 if (n > 1 and F / n >= (1 << 21)) else 1
+            # librmc: at world > 1 a level of >= 2^21 states in its frontier takes at
+            # least D.split rounds (4 since round 6), so each round's exchange
+            # overlaps the next round's expansion
+            split = SPLIT if (n > 1 and F / n >= (1 << 21)) else 1
             Ro[L] = set(range(max(split, math.ceil(F / n / per_round))))
         if measured:  # the prefix levels too: this model's own one-GPU run (same build as the tail)
             for L in t1:
@@ -209,6 +213,8 @@ def main():
             mo = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist,
                            table_frac=table_frac, overlap=True)
             row.setdefault("T_N_ms_overlapped", []).append(round(mo["T_N_ms"], 1))
+            for part in ("insert_ms", "xgmi_ms", "stall_ms", "latency_ms"):
+                row.setdefault("overlapped_" + part, []).append(round(mo.get(part, 0.0), 1))
             row.setdefault("speedup_overlapped", []).append(round(mo["speedup"], 2))
             row.setdefault("T_N_ms", []).append(round(m["T_N_ms"], 1))
             row.setdefault("speedup", []).append(round(m["speedup"], 2))

@@ -66,10 +66,16 @@ def load(lv_path, log_path, pr_path):
 
 def model(t1, frontier, total1, rounds, keys_in, states, pr, n, rep_max, lat, k_dist=1.0, a_lane=0.55,
           link_bw=50e9, c_probe=1 / 30e9, table_frac=None, RB=56, RBR=64, overlap=False):
-    """overlap: a level of R >= 2 rounds runs round k's exchange (owner inserts and
-    xGMI bytes, on the exchange stream) under round k + 1's expansion (librmc's two
-    outbox sets), so only the last round's exchange, 1/R of the level's, is exposed;
-    without it (the default) every exchange is charged in full, serially."""
+    """overlap: a level of R >= 2 rounds runs round k's exchange — owner inserts,
+    xGMI bytes and its host round trips (count read-back, reply read-back,
+    collectives, launches), on the exchange stream while the host waits — under
+    round k + 1's expansion, which librmc queues before it waits (two outbox
+    sets): the level takes f + e_r + (R - 1) max(e_r, x_r + L_r) + x_r + L_r +
+    a_level with e_r, x_r its per-round expansion and exchange and L_r one
+    round's latencies, i.e. only the last round's exchange and latency are
+    exposed when a round's exchange fits under the next expansion (the "stall"
+    part is what does not fit); without overlap (the default) every exchange and
+    every round's latency is charged in full, serially."""
     a_sync, a_coll, a_launch, a_level = lat
     accept = pr["states_sent"] / max(1, pr["keys_sent"])  # phase-2 states per phase-1 key
     f_level = min(t1.values())
@@ -101,13 +107,19 @@ def model(t1, frontier, total1, rounds, keys_in, states, pr, n, rep_max, lat, k_
             x = byts / (link_bw * links) if n > 1 else 0.0
             per_rank.append((e, ins, x))
         e, ins, x = max(per_rank, key=lambda v: sum(v))
+        l_round = 2 * a_sync + 4 * a_coll + 5 * a_launch
         if overlap and R >= 2:
-            ins, x = ins / R, x / R
-        lat_l = R * (2 * a_sync + 4 * a_coll + 5 * a_launch) + a_level
+            er, xr = max(0.0, e - f_level) / R, (ins + x) / R
+            parts["expand"] += e
+            parts["insert"] += ins / R
+            parts["xgmi"] += x / R
+            parts["stall"] += (R - 1) * max(0.0, xr + l_round - er)
+            parts["latency"] += l_round + a_level
+            continue
         parts["expand"] += e
         parts["insert"] += ins
         parts["xgmi"] += x
-        parts["latency"] += lat_l
+        parts["latency"] += R * l_round + a_level
     tot = sum(parts.values())
     return {"N": n, "rep_max": rep_max, "replicated_levels": n_rep, "k_dist": k_dist, "a_lane": a_lane,
             "a_sync_us": a_sync * 1e6, "a_coll_us": a_coll * 1e6, "a_launch_us": a_launch * 1e6,
@@ -116,7 +128,7 @@ def model(t1, frontier, total1, rounds, keys_in, states, pr, n, rep_max, lat, k_
 
 
 LATENCIES = ((10e-6, 15e-6, 5e-6, 40e-6), (20e-6, 30e-6, 8e-6, 80e-6), (40e-6, 60e-6, 10e-6, 150e-6))
-KEYB = 16  # bytes per phase-1 key record: the raw 96-bit fingerprint (k, s32) in two u64 (rmc_dist.cpp)
+KEYB = 12  # bytes per phase-1 key record: the raw 96-bit fingerprint {k lo, k hi, s32} (rmc_dist.cpp, round 6)
 
 
 def main():

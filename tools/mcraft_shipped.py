@@ -2,9 +2,10 @@
 CONSTRAINT, terms / logs / bags / counts unbounded) under a BFS depth bound on
 the wide layout: per level the new states, generated,
 cumulative seconds and rate; the deepest bound one GPU completes; the record
-size the front-end picked (904-B compact up to depth 17).  Measurement tool.
+size the front-end picked (336-B depth-sized up to depth 14, 904-B compact up to
+depth 17).  Measurement tool.
 
-    python tools/mcraft_shipped.py MAX_DEPTH [record: auto|full|compact] > levels.jsonl
+    python tools/mcraft_shipped.py MAX_DEPTH [record: auto|full|compact|depth] > levels.jsonl
 """
 import json
 import os
@@ -15,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "raft.tla_amd"))
 depth = int(sys.argv[1])
 rec = sys.argv[2] if len(sys.argv) > 2 else "auto"
 if rec != "auto":
-    os.environ["RMC_WIDE_COMPACT"] = "1" if rec == "compact" else "0"
+    os.environ["RMC_WIDE_COMPACT"] = {"full": "0", "compact": "1", "depth": "2"}[rec]
 import rmc  # noqa: E402
 
 base, _, _ = rmc.model_from_files(os.path.join(ROOT, "tests", "golden", "models", "MCunbounded.cfg"),
