@@ -5,6 +5,6 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 P=${OUT:-gpurun_out/kt}
 mkdir -p $P
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-probe-ceiling ${BENCH_ARGS} > $P/kt_bench.json 2> $P/kt.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-probe-ceiling --v2-config= ${BENCH_ARGS} > $P/kt_bench.json 2> $P/kt.err || exit 1
 find $P/kt -name "*kernel_trace.csv" -delete
 find $P/kt -name "*stats.csv" | head -5

@@ -7,7 +7,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 P=${OUT:-gpurun_out/pmc}
 mkdir -p $P
-B="--steps 1 --warmup 0 --no-cpu --no-probe-ceiling ${BENCH_ARGS}"
+B="--steps 1 --warmup 0 --no-cpu --no-probe-ceiling --v2-config= ${BENCH_ARGS}"
 C=${CMD:-python3 bench.py $B}
 for v in $ENVS; do export $v; done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- $C > $P/kt.json 2> $P/kt.err || exit 1

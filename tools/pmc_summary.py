@@ -79,6 +79,30 @@ def main():
     counters["kernel_trace"] = kavg
     counters["all_kernels"] = tot
     json.dump(counters, open(os.path.join(dst, f"pmc_counters_{stem}.json"), "w"), indent=1)
+    if g("TCC_EA0_ATOMIC_sum") is not None:  # the atomics pass: per BFS, against the inserts it makes
+        nbfs = int(os.environ.get("PMC_BFS", "2"))  # bench.py --steps 1: the step + the salt re-run
+        distinct = None
+        bj = os.path.join(src, "kt.json")
+        if os.path.exists(bj):
+            try:
+                distinct = json.load(open(bj))["config"]["distinct"]
+            except (ValueError, KeyError):
+                pass
+        ea, l2 = g("TCC_EA0_ATOMIC_sum"), g("TCC_ATOMIC_sum")
+        lvl = g("TCC_EA0_ATOMIC_LEVEL_sum")
+        ksec = kt["total_ms"] / 1e3 / nbfs if kt else None  # the kernel trace ran the same command
+        atom = {"kernel": k, "launches": n, "bfs_per_profile": nbfs,
+                "tcc_atomic_per_bfs": l2 / nbfs if l2 is not None else None,
+                "tcc_ea0_atomic_per_bfs": ea / nbfs,
+                "ea_atomic_avg_latency_cycles": (lvl / ea) if (lvl and ea) else None,
+                "distinct_states": distinct,
+                "atomics_per_insert": (ea / nbfs / distinct) if distinct else None,
+                "kernel_seconds_per_bfs": ksec,
+                "ea_atomics_per_s": (ea / nbfs / ksec) if ksec else None,
+                "note": "TCC_ATOMIC: atomic requests at the L2 (all types); TCC_EA0_ATOMIC: those that go on "
+                        "to memory; every new state is one CAS of its key into the fingerprint set (plus lost CAS "
+                        "races, linear-probe CASes and the per-wave counters)"}
+        json.dump(atom, open(os.path.join(dst, f"pmc_atomics_{stem}.json"), "w"), indent=1)
     print(json.dumps({"hbm_bytes_per_launch": hbm / n, "launches": n, "kernel_avg_us": kt["avg_us"] if kt else None,
                       "salu_per_valu": counters.get("salu_per_valu"),
                       "wait_any_per_wave_cycle": counters.get("wait_any_per_wave_cycle")}))
