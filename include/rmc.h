@@ -77,8 +77,11 @@ extern "C" {
                                            /* fit (else they move to host memory).      */
                                            /* state_capacity then sizes the fingerprint */
                                            /* set and links (all states), device_window */
-                                           /* the resident states.  Single GPU; not     */
-                                           /* with RMC_FLAG_VERIFY_STATES               */
+                                           /* the resident states.  Single GPU.  With   */
+                                           /* RMC_FLAG_VERIFY_STATES every state leaving */
+                                           /* the window keeps a host copy, and hits on  */
+                                           /* it are compared with that copy (round 6;   */
+                                           /* no checkpoint / recover then)             */
 /* A model without a CONSTRAINT on some field (MCraft.cfg as shipped) runs only
  * under a depth bound (max_depth > 0, TLC -depth).  The front-end then gives
  * each unbounded field the wide capacity (RMC_WIDE_MAX_TERM, RMC_WIDE_MAX_LOG,

@@ -2169,7 +2169,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
     } else if (which == 3) {
         if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
-        else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
+        else if (dist_kvariant() == 4 && B.pool && SORTED) {  // 3 with dynamic per-wave units (A/B)
+            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true, 1>));
+            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, true, 1>));
+        } else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
             if constexpr (SORTED) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
