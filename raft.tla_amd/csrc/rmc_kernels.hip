@@ -2072,7 +2072,7 @@ static u64 resident_grid(const void* k) {
 // Expansion kernel variant (RMC_EXPAND_VARIANT): 20 (the default, any value but 1)
 // = k_expand_sort over windows of 16 tiles presorted by class (k_window_order; no
 // sort in the kernel, so a smaller block), 5 probes in flight per thread, the
-// parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD), each wave taking its
+// parent's mixes recomputed per lane (80 VGPRs: 6 waves/SIMD; 5 waves for S >= 4), each wave taking its
 // next quarter-window from a launch-wide counter (XL 739.3-741.6 vs 760.1-762.1 ms
 // for fixed per-block shares, profiles/r05/variants/); 1 = every lane of every
 // state (k_expand, the kernel of shapes with more than 128 lanes).  The variants
@@ -2091,8 +2091,9 @@ static int expand_variant() {
 // = the pool flush at the single-GPU kernel's shape (presorted windows, 5 probes,
 // 6 waves/SIMD; remote successors pooled whole and routed by k_route after the
 // launch); 0 = the round-3 send-marker kernel with the flush doing the routing
-// (windows sorted in LDS).  The other variants measured in rounds 3-5
-// (profiles/r04/ab/dist_kvariant_*, profiles/r05/kv4/) are in git history.
+// (windows sorted in LDS).  The other variants measured in rounds 3-6
+// (profiles/r04/ab/dist_kvariant_*, profiles/r05/kv4/; dynamic per-wave units a
+// tie again in round 6, profiles/r06/ab/dist_kvariant_3_4.txt) are in git history.
 static int dist_kvariant() {
     static int v = [] {
         const char* e = getenv("RMC_DIST_KVARIANT");
@@ -2157,11 +2158,23 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                                    a, b);
         } else if (verify) {
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, true>));
-        } else if (expand_variant() != 1 && SORTED && B.word) {  // 20: presorted windows, dynamic per-wave units
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
+        } else if (expand_variant() != 1 && S >= 4 && SORTED && B.word) {
+            // S >= 4 (68 / 92 lanes, the 128-bit lane mask): the same kernel at 5 waves/SIMD
+            // (96 VGPRs, 16 B of scratch) beats 6 waves with 48 B of spills: MCraft5 -depth 20
+            // 206 vs 245-246 ms (4 probes at 6 waves 247-248 ms), profiles/r06/ab/s5_waves.txt
+            if constexpr (S >= 4) {
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
+                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
+            }
+        } else if (expand_variant() != 1 && S < 4 && SORTED && B.word) {  // 20: presorted windows, dynamic units
+            if constexpr (S < 4) {
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
+                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
+            }
         } else {  // 1, and shapes with more than 64 lanes
             RMC_EXPAND_LAUNCH((k_expand<S, K, false, kBatch, false, false, true>));
         }
@@ -2169,12 +2182,7 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
     } else if (which == 3) {
         if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
-        else if (dist_kvariant() == 4 && B.pool && SORTED) {  // 3 with dynamic per-wave units (A/B)
-            const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true, 1>));
-            const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-            if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-            RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, true, 1>));
-        } else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
+        else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
             if constexpr (SORTED) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);

@@ -51,8 +51,9 @@ def main():
     kt = next((v for kk, v in kavg.items() if kname in kk and "<3, 4, 8, true" not in kk), None)
     traffic = {
         "command": "tools/gpu/pmc.sh: rocprofv3 --kernel-trace --stats, then one --pmc pass per counter group "
-                   "(FETCH_SIZE | WRITE_SIZE | SQ instruction mix | SQ waits | LDS) -- python3 bench.py --steps 1 "
-                   "--warmup 0 --no-cpu --no-probe-ceiling; per-kernel totals by tools/pmc_totals.py",
+                   "(FETCH_SIZE | WRITE_SIZE | SQ instruction mix | SQ waits | LDS | TCC atomics) -- python3 bench.py "
+                   "--steps 1 --warmup 0 --no-cpu --no-probe-ceiling --v2-config=; per-kernel totals by "
+                   "tools/pmc_totals.py",
         "workload": os.environ.get("PMC_WORKLOAD",
                                    f"specs/{stem}.cfg, BFS to fixpoint (bench step + the untimed fingerprint-salt re-run)"),
         "kernel": k,
