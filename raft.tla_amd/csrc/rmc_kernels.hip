@@ -1350,8 +1350,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // PS (round 6, the default): the windows presorted by k_window_order, so the
 // block carries no LDS sort (35 instead of 48 KB: the 96-bit keys' s_ks array
 // had cut the in-kernel sort's block to 3 per CU, i.e. 3 waves/SIMD).
-template <int S, int K, int BATCH, bool WS, bool PS = false, int DYN = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 3 && K == 4 ? (WS ? 4 : 5) : 1))) void
+template <int S, int K, int BATCH, bool WS, bool PS = false, int DYN = 0,
+          int WPE = (S == 3 && K == 4 ? (WS ? 4 : 5) : 1)>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 k_expand_sym(const Params P, const PermTable PT, const DevBufs B, u64 lo, u64 hi) {
     if constexpr (WS && PS && Lanes<S, K>::N <= 128)
         expand_body<S, K, true, BATCH, false, false, false, true, false, false, 16, 0, false, true, DYN>(P, PT, B, lo,
@@ -2141,7 +2142,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else if (sym_variant() >= 2 && SORTED && B.word) {  // 1 with dynamic per-wave units, resident grid
+            else if (sym_variant() == 4 && SORTED && B.word) {  // 1 with 6 probes in flight at 5 waves/SIMD (A/B)
+                const u64 gs = expand_grid_env() ? (blocks < expand_grid_env() ? blocks : expand_grid_env()) : g;
+                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
+                hipLaunchKernelGGL((k_expand_sym<S, K, 6, SORTED, true, 0, 5>), dim3((unsigned)gs), dim3(256), 0, st,
+                                   P, PT, B, a, b);
+            } else if (sym_variant() >= 2 && SORTED && B.word) {  // 1 with dynamic per-wave units, resident grid
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_sym<S, K, kBatch, SORTED, true, 1>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp) * (u64)(sym_variant() - 1);
                 const u64 gs = blocks < want ? blocks : want;
@@ -2168,6 +2174,21 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                 if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
                 RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
             }
+        } else if ((expand_variant() == 22 || expand_variant() == 24) && S < 4 && SORTED && B.word) {
+            // S < 4 (A/B): 20 at 5 waves/SIMD with 5 (22) or 6 (24) probes in flight
+            if constexpr (S < 4) {
+                if (expand_variant() == 22) {
+                    const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
+                    const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                    if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                    RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
+                } else {
+                    const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, 5, false, 1>));
+                    const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                    if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                    RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, 5, false, 1>));
+                }
+            }
         } else if (expand_variant() != 1 && S < 4 && SORTED && B.word) {  // 20: presorted windows, dynamic units
             if constexpr (S < 4) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
@@ -2182,7 +2203,14 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
     } else if (which == 3) {
         if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
-        else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
+        else if (dist_kvariant() == 5 && S >= 4 && B.pool) {  // 3 at 5 waves/SIMD for S >= 4 (A/B)
+            if constexpr (SORTED && S >= 4) {
+                const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 5, true>));
+                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
+                if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
+                RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 5, true>));
+            }
+        } else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
             if constexpr (SORTED) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
