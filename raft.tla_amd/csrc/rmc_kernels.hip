@@ -1349,7 +1349,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // neutral, removed.)
 // PS (round 6, the default): the windows presorted by k_window_order, so the
 // block carries no LDS sort (35 instead of 48 KB: the 96-bit keys' s_ks array
-// had cut the in-kernel sort's block to 3 per CU, i.e. 3 waves/SIMD).
+// had cut the in-kernel sort's block to 3 per CU, i.e. 3 waves/SIMD); with 6
+// probes in flight (BATCH) the block takes 28.7 KB and the kernel runs at 5 waves.
 template <int S, int K, int BATCH, bool WS, bool PS = false, int DYN = 0,
           int WPE = (S == 3 && K == 4 ? (WS ? 4 : 5) : 1)>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
@@ -2103,12 +2104,16 @@ static int dist_kvariant() {
     return v;
 }
 
-// SYMMETRY expansion kernel (RMC_SYM_VARIANT): 1 (default) windows presorted by
-// k_window_order; 0 windows sorted in LDS by the kernel itself (round 5).
+// SYMMETRY expansion kernel (RMC_SYM_VARIANT): 2 (default) windows presorted by
+// k_window_order, 6 probes in flight, 5 waves/SIMD (96 VGPRs, 28.7 KB of LDS:
+// 79-80 ms on MCraftBenchSym, profiles/r06/ab/sym_batch6_5waves.txt); 1 the same
+// with 8 probes at 4 waves (81-82 ms; dynamic per-wave units and other grids
+// measured the same, profiles/r06/ab/sym_presorted.txt); 0 windows sorted in LDS
+// by the kernel itself (round 5: 48 KB of LDS, 3 waves/SIMD, 87-88 ms).
 static int sym_variant() {
     static int v = [] {
         const char* e = getenv("RMC_SYM_VARIANT");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 2;
     }();
     return v;
 }
@@ -2142,18 +2147,15 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
             if (verify)
                 hipLaunchKernelGGL((k_expand<S, K, true, kBatch, false, true>), dim3((unsigned)g), dim3(256), 0, st, P,
                                    PT, B, a, b);
-            else if (sym_variant() == 4 && SORTED && B.word) {  // 1 with 6 probes in flight at 5 waves/SIMD (A/B)
-                const u64 gs = expand_grid_env() ? (blocks < expand_grid_env() ? blocks : expand_grid_env()) : g;
-                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
-                hipLaunchKernelGGL((k_expand_sym<S, K, 6, SORTED, true, 0, 5>), dim3((unsigned)gs), dim3(256), 0, st,
-                                   P, PT, B, a, b);
-            } else if (sym_variant() >= 2 && SORTED && B.word) {  // 1 with dynamic per-wave units, resident grid
-                const void* kp = reinterpret_cast<const void*>(&(k_expand_sym<S, K, kBatch, SORTED, true, 1>));
-                const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp) * (u64)(sym_variant() - 1);
-                const u64 gs = blocks < want ? blocks : want;
-                if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
-                hipLaunchKernelGGL((k_expand_sym<S, K, kBatch, SORTED, true, 1>), dim3((unsigned)gs), dim3(256), 0, st,
-                                   P, PT, B, a, b);
+            else if (sym_variant() >= 2 && S <= 3 && K == 4 && SORTED && B.word) {
+                // presorted, 6 probes in flight, 5 waves/SIMD (the shapes that fit 96 VGPRs
+                // without spills; the others take variant 1)
+                if constexpr (S <= 3 && K == 4) {
+                    const u64 gs = expand_grid_env() ? (blocks < expand_grid_env() ? blocks : expand_grid_env()) : g;
+                    if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
+                    hipLaunchKernelGGL((k_expand_sym<S, K, 6, SORTED, true, 0, 5>), dim3((unsigned)gs), dim3(256), 0,
+                                       st, P, PT, B, a, b);
+                }
             } else if (sym_variant() != 0 && SORTED && B.word) {  // windows presorted by k_window_order
                 const u64 gs = expand_grid_env() ? (blocks < expand_grid_env() ? blocks : expand_grid_env()) : g;
                 if (hipError_t e = launch_window_order(B, a, b, gs, 16, st)) return e;
@@ -2174,21 +2176,6 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                 if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
                 RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
             }
-        } else if ((expand_variant() == 22 || expand_variant() == 24) && S < 4 && SORTED && B.word) {
-            // S < 4 (A/B): 20 at 5 waves/SIMD with 5 (22) or 6 (24) probes in flight
-            if constexpr (S < 4) {
-                if (expand_variant() == 22) {
-                    const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
-                    const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-                    if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-                    RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 5, false, 1>));
-                } else {
-                    const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, 5, false, 1>));
-                    const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
-                    if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
-                    RMC_EXPAND_LAUNCH((k_expand_sort<S, K, 6, K <= 4 ? 1 : 0, true, 5, false, 1>));
-                }
-            }
         } else if (expand_variant() != 1 && S < 4 && SORTED && B.word) {  // 20: presorted windows, dynamic units
             if constexpr (S < 4) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_sort<S, K, 5, K <= 4 ? 1 : 0, true, 6, false, 1>));
@@ -2203,7 +2190,9 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
         RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true, true>));
     } else if (which == 3) {
         if constexpr (SYM) RMC_EXPAND_LAUNCH((k_expand<S, K, SYM, kBatch, true>));  // the lossy sent-cache
-        else if (dist_kvariant() == 5 && S >= 4 && B.pool) {  // 3 at 5 waves/SIMD for S >= 4 (A/B)
+        else if (dist_kvariant() != 0 && S >= 4 && B.pool) {
+            // S >= 4: 5 waves/SIMD (96 VGPRs) instead of 6 with 96 B of spills: MCraft5 to
+            // depth 20 on one sharded rank 0.322 vs 0.568 s (profiles/r06/ab/s5_dist_waves.txt)
             if constexpr (SORTED && S >= 4) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 5, true>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
@@ -2211,12 +2200,12 @@ static hipError_t launch_t(int which, bool verify, const Params& P, const PermTa
                 RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 5, true>));
             }
         } else if (dist_kvariant() != 0 && B.pool) {  // 3: the pool flush at the single-GPU kernel's shape
-            if constexpr (SORTED) {
+            if constexpr (SORTED && S < 4) {
                 const void* kp = reinterpret_cast<const void*>(&(k_expand_dist<S, K, 5, false, true, 6, true>));
                 const u64 want = expand_grid_env() ? expand_grid_env() : resident_grid(kp);
                 if (hipError_t e = launch_window_order(B, a, b, want, 16, st)) return e;
                 RMC_EXPAND_LAUNCH((k_expand_dist<S, K, 5, false, true, 6, true>));
-            } else {
+            } else if constexpr (!SORTED) {
                 RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false, false, 4, true>));
             }
         } else RMC_EXPAND_LAUNCH((k_expand_dist<S, K, kBatch, false>));            // send markers
