@@ -129,6 +129,11 @@ def main():
         k = args.index("--table-frac")
         table_frac = float(args[k + 1])
         del args[k:k + 2]
+    rep_max = 1 << 20  # librmc's RMC_DIST_REP default
+    if "--rep-max" in args:
+        k = args.index("--rep-max")
+        rep_max = int(args[k + 1])
+        del args[k:k + 2]
     measured = None
     if "--measured" in args:
         k = args.index("--measured")
@@ -206,11 +211,11 @@ def main():
                "T1_model_s": tot1, "peak_level_new": max(full)}
         row["memory"] = memory_plan(n, distinct)
         for lat in dcm.LATENCIES:
-            m = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist,
+            m = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=rep_max, lat=lat, k_dist=k_dist,
                           table_frac=table_frac)
             for part in ("expand_ms", "insert_ms", "xgmi_ms", "latency_ms"):
                 row.setdefault(part, []).append(round(m.get(part, 0.0), 1))
-            mo = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=1 << 20, lat=lat, k_dist=k_dist,
+            mo = dcm.model(T1, Fr, tot1, Ro, Ki, St, pr, n=n, rep_max=rep_max, lat=lat, k_dist=k_dist,
                            table_frac=table_frac, overlap=True)
             row.setdefault("T_N_ms_overlapped", []).append(round(mo["T_N_ms"], 1))
             for part in ("insert_ms", "xgmi_ms", "stall_ms", "latency_ms"):
