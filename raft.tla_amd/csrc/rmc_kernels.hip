@@ -1445,25 +1445,40 @@ __device__ __forceinline__ u64 match_class8(u32 c, bool act) {
 // positions (match_class8), not one per position: a window's states fall in a
 // few classes, and same-address LDS atomics serialise (0.91 bank conflicts per
 // LDS access with per-position atomics, round 4's PMC profile).
+// Round 6: every class byte of the thread's window positions is loaded up front
+// (16 independent loads, one memory latency per window instead of one per
+// 256-position round), each position's peers (match_class8) are found once and
+// kept for the scatter pass, and the grid is one round of resident blocks of
+// this kernel rather than of the expansion kernel.
 __global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 wmask, u64 lo, u64 nf, u64 wt,
                                                       uint16_t* word, unsigned long long* wnext) {
     __shared__ u32 bins[256];
-    __shared__ uint8_t cs[256 * 16];
     const u32 tid = threadIdx.x;
     const u64 lt = (1ull << __lane_id()) - 1ull;
     if (blockIdx.x == 0 && tid == 0) *wnext = 0;  // the next expansion launch's dynamic work counter
     for (u64 win = (u64)blockIdx.x * 256ull * wt; win < nf; win += (u64)gridDim.x * 256ull * wt) {
         const u32 wn = (u32)((nf - win) < 256ull * wt ? (nf - win) : 256ull * wt);
+        u32 cv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u32 p = (u32)k * 256u + tid;
+            cv[k] = p < wn ? (u32)cls[(lo + win + p) & wmask] : 0u;
+        }
         __syncthreads();
         bins[tid] = 0;
         __syncthreads();
-        for (u32 p0 = 0; p0 < wn; p0 += 256) {  // block-uniform rounds
-            const u32 p = p0 + tid;
-            const bool act = p < wn;
-            const u32 c = act ? (u32)cls[(lo + win + p) & wmask] : 0u;
-            if (act) cs[p] = (uint8_t)c;
+        // pass 1: one counter atomic per class present in a wave's 64 positions; each
+        // position keeps class | rank among its peers << 8 | their leader << 14 | their number << 20
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {  // block-uniform rounds
+            if ((u32)k * 256u >= wn) break;
+            const bool act = (u32)k * 256u + tid < wn;
+            const u32 c = cv[k];
             const u64 peers = match_class8(c, act);
-            if (act && (peers & lt) == 0) atomicAdd(&bins[c], (u32)__popcll(peers));
+            const u32 rank = (u32)__popcll(peers & lt), cnt = (u32)__popcll(peers);
+            if (act && rank == 0) atomicAdd(&bins[c], cnt);
+            const u32 leader = peers ? (u32)(__ffsll((long long)peers) - 1) : 0u;
+            cv[k] = c | (rank << 8) | (leader << 14) | (cnt << 20);
         }
         __syncthreads();
         if (tid < 64) {  // exclusive scan of the 256 counters: 4 per lane, then across the wave
@@ -1481,20 +1496,22 @@ __global__ __launch_bounds__(256) void k_window_order(const uint8_t* cls, u64 wm
             for (int q = 0; q < 4; ++q) { bins[tid * 4 + q] = ex; ex += v[q]; }
         }
         __syncthreads();
-        for (u32 p0 = 0; p0 < wn; p0 += 256) {  // one cursor atomic per class present in the wave
-            const u32 p = p0 + tid;
+        // pass 2: the leader of each class group reserves its group's positions
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if ((u32)k * 256u >= wn) break;
+            const u32 p = (u32)k * 256u + tid;
             const bool act = p < wn;
-            const u32 c = act ? (u32)cs[p] : 0u;
-            const u64 peers = match_class8(c, act);
-            const int leader = peers ? __ffsll((long long)peers) - 1 : 0;
+            const u32 v = cv[k], c = v & 0xFFu, rank = (v >> 8) & 63u, leader = (v >> 14) & 63u, cnt = v >> 20;
             u32 base = 0;
-            if (act && (peers & lt) == 0) base = atomicAdd(&bins[c], (u32)__popcll(peers));
-            base = (u32)__shfl((int)base, leader);
-            if (act) word[win + base + (u32)__popcll(peers & lt)] = (uint16_t)p;
+            if (act && rank == 0) base = atomicAdd(&bins[c], cnt);
+            base = (u32)__shfl((int)base, (int)leader);
+            if (act) word[win + base + rank] = (uint16_t)p;
         }
     }
 }
 
+static u64 resident_grid(const void* k);  // (host launchers, below)
 hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 wt_max, hipStream_t st) {
     const u64 nf = hi - lo;
     if (nf == 0) return hipSuccess;
@@ -1503,7 +1520,13 @@ hipError_t launch_window_order(const DevBufs& B, u64 lo, u64 hi, u64 grid, u64 w
     const u64 per_block = (nf + grid * 256ull - 1) / (grid * 256ull);
     const u64 wt = per_block < wt_max ? (per_block ? per_block : 1ull) : wt_max;
     const u64 nwin = (nf + 256ull * wt - 1) / (256ull * wt);
-    hipLaunchKernelGGL(k_window_order, dim3((unsigned)(nwin < grid ? nwin : grid)), dim3(256), 0, st, B.cls, B.wmask, lo, nf,
+    // its own grid: one round of its resident blocks (RMC_WORDER_GRID=0: the expansion's, round 5)
+    static const u64 og = [] {
+        const char* e = getenv("RMC_WORDER_GRID");
+        return e ? (u64)atoll(e) : (u64)1;
+    }();
+    const u64 g2 = og == 0 ? grid : og == 1 ? resident_grid(reinterpret_cast<const void*>(&k_window_order)) : og;
+    hipLaunchKernelGGL(k_window_order, dim3((unsigned)(nwin < g2 ? nwin : g2)), dim3(256), 0, st, B.cls, B.wmask, lo, nf,
                        wt, B.word, (unsigned long long*)&B.ctr->wnext);
     return hipGetLastError();
 }
