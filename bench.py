@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument("--capacity", type=int, default=0,
                     help="state capacity per GPU (0: 1.5e9 / world * 1.3 for MCraftBench.cfg, the table size every "
                          "round measured; any other model: librmc's own sizing, 80%% of free HBM)")
+    ap.add_argument("--set-bytes", type=int, default=-1,
+                    help="fingerprint-set bytes per GPU (rmc_config.set_bytes, TLC -fpmem; 0: librmc's sizing, "
+                         "load <= 1/2; -1: the bench default, load <= 1/4 of the capacity: sparse_set_bytes)")
     ap.add_argument("--spill", default="auto", choices=("auto", "on", "off"),
                     help="RMC_FLAG_SPILL (expanded levels leave the device window; their trace links stay in "
                          "HBM): auto = on for a single GPU unless the model is MCraftBench.cfg")
@@ -242,6 +245,19 @@ def pmc_traffic(config_path):
     return None, None
 
 
+def sparse_set_bytes(capacity):
+    """The bench's fingerprint-set size (rmc_config.set_bytes, TLC -fpmem): 8-B
+    slots for four times the states the GPU may store, rounded up to a power of
+    two — load <= 1/4 instead of librmc's default 1/2.  A probe for a new state
+    ends at the first empty slot, one dependent load per occupied slot before
+    it: doubling the set took XL 731 -> 704 ms and MCraftBench 210 -> 198 ms on
+    one box, its larger clear included (profiles/r06/ab/set_size.txt)."""
+    slots = 1
+    while slots < 4 * capacity:
+        slots <<= 1
+    return slots * 8
+
+
 def v2_fixpoint_child(path, dev):
     """v2_fixpoint in a child process (a fresh device address space: after the
     XL run's 230 GB were allocated and freed in this one, the same search
@@ -265,6 +281,7 @@ def v2_fixpoint(path, dev, runs=3):
     c = rmc.config_from_files(path, builtin_raft=True)
     c.device = dev
     c.state_capacity = int(1.5e9)  # resident, no spill (the size every round measured)
+    c.set_bytes = sparse_set_bytes(c.state_capacity)
     ts = []
     with rmc.Checker(c) as ck:
         ck.run(record_levels=False)
@@ -369,8 +386,14 @@ def main(argv=None):
     elif xl and sharded:  # 4.13 G states: a rank's share, +20 % for the owner imbalance (the 8-rank
         # rehearsal's fullest rank held 13.4 % of the states, 1.07x its share: profiles/r06/dist8/)
         cfg.state_capacity = int(4.14e9 / world * 1.2)
+    elif xl:  # 4,132,397,328 states: the store and the ring window fit beside a 2^34-slot set
+        cfg.state_capacity = int(4.14e9)
     else:  # librmc's own sizing (80 % of free HBM)
         cfg.state_capacity = 0
+    if a.set_bytes >= 0:
+        cfg.set_bytes = a.set_bytes
+    elif cfg.state_capacity:
+        cfg.set_bytes = sparse_set_bytes(cfg.state_capacity)
     spill = (a.spill == "on" or (a.spill == "auto" and not small)) and not sharded
     if spill:
         cfg.flags |= rmc.FLAG_SPILL
@@ -473,6 +496,11 @@ def main(argv=None):
                         f"{cfg.max_log_len} MaxMsgs={cfg.max_msgs} MaxDup={cfg.max_dup}, BFS to fixpoint",
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
+            "fingerprint_set": {"slots": last[0].set_slots, "bytes": last[0].set_slots * 8,
+                                "load": (last[0].distinct / last[0].set_slots) if last[0].set_slots else None,
+                                "set_bytes": cfg.set_bytes, "capacity": cfg.state_capacity,
+                                "rule": "sparse_set_bytes: load <= 1/4 of the capacity (TLC -fpmem)"
+                                        if a.set_bytes < 0 and cfg.set_bytes else "set_bytes given / librmc's"},
             "spill": ({"flag": "RMC_FLAG_SPILL", "trace_links": "device" if last[0].spill_links_on_device else "host",
                        "window": ("ring (slot reuse, nothing copied)" if last[0].spill_links_on_device
                                   else "shifted (links to host memory)"),

@@ -24,7 +24,8 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 7 /* 6: rmc_result.spill_links_on_device (round 5); 7: .verified_spilled (round 6) */
+#define RMC_ABI_VERSION 8 /* 6: rmc_result.spill_links_on_device (round 5); 7: .verified_spilled, 8: rmc_config.set_bytes and
+                             rmc_result.set_slots (round 6) */
 
 /* Capacity of the packed encoding (DESIGN.md "Packed state"): the layout the
  * BFS kernels run on when every bound fits it. */
@@ -130,6 +131,13 @@ typedef struct rmc_config {
                               /* fingerprint collisions); simulation: RNG seed     */
     uint64_t device_window;   /* RMC_FLAG_SPILL: states resident on the device    */
                               /* (frontier + the level being built); 0 = auto     */
+    uint64_t set_bytes;       /* the fingerprint set's size (TLC -fpmem), rounded */
+                              /* down to a power of two of 8-B slots; it holds at */
+                              /* most half as many states (a capacity error past  */
+                              /* that).  With state_capacity given it is an upper */
+                              /* bound, halved until the store fits beside it.    */
+                              /* 0 = auto: 2 slots per state of state_capacity    */
+                              /* (auto: for the largest store the device holds)   */
 } rmc_config;
 
 /* End-of-run summary.  Replaces TLC's stdout summary lines:
@@ -176,6 +184,7 @@ typedef struct rmc_result {
     /* RMC_FLAG_VERIFY_STATES with RMC_FLAG_SPILL */
     uint64_t verified_spilled; /* hits (of `verified`) whose stored state had left the device */
                                /* window, compared with its host copy                       */
+    uint64_t set_slots;        /* 8-B slots of the fingerprint set this run used (set_bytes) */
 } rmc_result;
 
 /* Per-level progress (TLC prints "Progress(D) ... states generated ..."). */

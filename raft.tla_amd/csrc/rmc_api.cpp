@@ -579,7 +579,28 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     (void)hipMemGetInfo(&fr, &tot);
     const u64 budget = (u64)((double)fr * 0.80);
     u64 cap = cfg->state_capacity;
-    if (cap == 0) {
+    // rmc_config.set_bytes (TLC -fpmem): the set's slots, the largest power of two that fits
+    u64 set_slots = set_slots_of(cfg->set_bytes);
+    if (set_slots && cap) {
+        // set_bytes is an upper bound: halved (down to load 1/2) until the store fits
+        // beside it — the states, or spilling the device trace links and the window
+        // the spill sizing below asks for (need_win)
+        const u64 sb = c->sh.verify ? 16 : 8;
+        const u64 need_win = cfg->device_window ? cfg->device_window : cap / (c->sh.verify ? 8 : 4);
+        const u64 store = spill ? cap * 9 + need_win * (per_state - 9) : cap * per_state;
+        while (set_slots > 1024 && set_slots / 2 >= 2 * cap && set_slots * sb + store > budget) set_slots >>= 1;
+    }
+    if (set_slots && cap > set_slots / 2) {
+        c->err = "state_capacity " + std::to_string(cap) + " exceeds what a set of set_bytes " +
+                 std::to_string(cfg->set_bytes) + " holds (" + std::to_string(set_slots / 2) + " states)";
+        return bail(RMC_E_INVAL);
+    }
+    if (cap == 0 && set_slots) {
+        // the given set holds set_slots / 2 states; the store fills what the set leaves
+        const u64 fixed = set_slots * (c->sh.verify ? 16 : 8);
+        cap = set_slots / 2;
+        if (!spill) cap = std::min<u64>(cap, (budget - std::min<u64>(budget, fixed)) / per_state);
+    } else if (cap == 0) {
         // table <= 4 slots per state after pow2 rounding (+ as many sidx words when verifying);
         // spilling: the largest set of at most half the budget, two slots per state
         if (spill && c->sh.verify) {  // the set and its slot -> index map: 16 B per slot, <= 2/3 of the budget
@@ -598,6 +619,7 @@ int rmc_create(const rmc_config* cfg, rmc_ctx** out) {
     cap = std::max<u64>(cap, 1024);
     u64 slots = 1;
     while (slots < 2 * cap) slots <<= 1;
+    if (set_slots) slots = std::max(slots, set_slots);
     c->table_slots = slots;
     u64 win = cap;  // states resident on the device
     // spilling: the trace links of every state stay on the device (9 B each) when
@@ -735,6 +757,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
         depth = c->resume_depth;
     } else {
     c->res = rmc_result{};
+    c->res.set_slots = c->table_slots;
     c->res.spill_links_on_device = c->spill.on && c->spill.dev_links;
     c->walked = 0;
     c->level_start.clear();
@@ -751,8 +774,8 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             });
         }
     }
-    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
-    if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
+    HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+    if (c->sh.verify) HIPCHK(c, launch_fill(c->B.sidx, c->table_slots * 8, 0xFF, c->st));
     HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (int rc = reset_counters(c, false)) return rc;
     c->B.vlo = 0;
@@ -984,8 +1007,9 @@ int rmc_get_result(const rmc_ctx* c, rmc_result* out) {
 namespace {
 // The header embeds the ABI structs rmc_config and rmc_result, so its size is
 // written too and must match: a struct that grows changes kCkptVersion.
-constexpr uint32_t kCkptVersion = 4;  // 3: rmc_result with parked / exchange_wait_seconds; 4: the set holds
-                                      // k ^ s values (raft_packed.h Fp), rmc_result with spill_links_on_device
+constexpr uint32_t kCkptVersion = 5;  // 3: rmc_result with parked / exchange_wait_seconds; 4: the set holds
+                                      // k ^ s values (raft_packed.h Fp), rmc_result with spill_links_on_device;
+                                      // 5: rmc_config.set_bytes, rmc_result.verified_spilled
 struct CkptHeader {
     char magic[8];
     uint32_t version, nw;
@@ -1148,8 +1172,8 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     auto get = [&](void* p, u64 n) {
         if (!rc && n && fread(p, 1, n, f) != n) rc = fail(c, RMC_E_IO, "checkpoint file truncated");
     };
-    HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
-    if (c->sh.verify) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
+    HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+    if (c->sh.verify) HIPCHK(c, launch_fill(c->B.sidx, c->table_slots * 8, 0xFF, c->st));
     // footprints are not checkpointed: the recovered frontier is expanded without
     // diamond skipping (FOOT_VALID clear), the levels after it with
     HIPCHK(c, hipMemsetAsync(c->spill.on ? c->spill.foot : c->B.foot, 0,

@@ -119,6 +119,15 @@ struct SpillState {
     rmc::u64 host_hits = 0;        // hits checked against host copies in the last run
 };
 
+// rmc_config.set_bytes -> fingerprint-set slots: the largest power of two of
+// 8-B slots within the bytes (at least 1024), 0 when the set is sized automatically
+inline rmc::u64 set_slots_of(rmc::u64 bytes) {
+    if (bytes == 0) return 0;
+    rmc::u64 sl = 1024;
+    while ((sl << 1) * 8 <= bytes) sl <<= 1;
+    return sl;
+}
+
 struct rmc_ctx {
     rmc_config cfg{};
     rmc::Shape sh{};

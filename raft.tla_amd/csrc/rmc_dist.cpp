@@ -417,15 +417,16 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->resume = 0;
     const rmc_result saved = c->res;
     c->res = rmc_result{};
+    c->res.set_slots = c->table_slots;
     if (!resume) c->level_start.clear();
     c->have_target = 0;
     D.keys_sent = D.states_sent = D.chunks = D.parked = 0;
     D.xfer_seconds = D.wait_seconds = 0;
     D.rep_levels = 0;
-    if (!resume) HIPCHK(c, hipMemsetAsync(c->B.table, 0, c->table_slots * 8, c->st));
-    if (c->B.sent) HIPCHK(c, hipMemsetAsync(c->B.sent, 0, D.sent_slots * 8, c->st));
+    if (!resume) HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+    if (c->B.sent) HIPCHK(c, launch_fill(c->B.sent, D.sent_slots * 8, 0, c->st));
     const bool verify = c->sh.verify;
-    if (verify && !resume) HIPCHK(c, hipMemsetAsync(c->B.sidx, 0xFF, c->table_slots * 8, c->st));
+    if (verify && !resume) HIPCHK(c, launch_fill(c->B.sidx, c->table_slots * 8, 0xFF, c->st));
     HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
     if (resume) c->h_ctr->count = c->level_start.back();
     if (int rc = reset_counters(c, resume)) return rc;

@@ -166,6 +166,8 @@ constexpr u64 POOL_TICK = 1ull << 48;
 // hash); returns after the copy (the staging value lives on the caller's stack).
 hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st);
 
+// Sets bytes [p, p + bytes) to `byte` (the fingerprint set's clear; RMC_FILL=0: hipMemsetAsync).
+hipError_t launch_fill(void* p, u64 bytes, uint8_t byte, hipStream_t st);
 // Random-probe microbenchmark over table[mask + 1] (mode 0 loads, 1 CAS).
 hipError_t launch_probe_bench(u64* table, u64 mask, u64 threads, u32 iters, int mode, u64* sink, hipStream_t st);
 

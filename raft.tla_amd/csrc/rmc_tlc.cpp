@@ -154,7 +154,7 @@ int usage() {
     fprintf(stderr,
             "usage: rmc-tlc [-config X.cfg] [-depth N] [-deadlock] [-device D] [-capacity N] [-workers N]\n"
             "               [-verify] [-fpseed S] [-checkpoint F] [-recover F] [-simulate [num=N]] [-seed S]\n"
-            "               [-raft raft.tla] [-builtin-raft] [-gpus N] [-nospill] [-window N] X.tla\n"
+            "               [-raft raft.tla] [-builtin-raft] [-gpus N] [-nospill] [-window N] [-fpmem B] X.tla\n"
             "  -gpus N        shard the search over N GPUs (one ctx and RCCL rank per GPU)\n"
             "  -raft F        the raft.tla to verify against the compiled-in spec (default: next to X.tla)\n"
             "  -builtin-raft  no raft.tla on disk: check the compiled-in lemmy/raft.tla (said in the output)\n"
@@ -164,6 +164,9 @@ int usage() {
             "             by default expanded levels spill to pinned host memory (single GPU)\n"
             "  -window N  states kept on the device when spilling (default: what the set leaves)\n"
             "  -fpseed S  fingerprint salt (TLC -fp: another member of the fingerprint family)\n"
+            "  -fpmem B   bytes of HBM for the fingerprint set (TLC -fpmem; suffix K/M/G; it holds\n"
+            "             B / 16 states, \"fingerprint set full\" past that); default: sized for the\n"
+            "             largest store the device holds\n"
             "  -checkpoint F  write the search to F when it stops at -depth (TLC -checkpoint)\n"
             "  -recover F     continue the search saved in F (TLC -recover)\n"
             "  -simulate  random simulation (TLC -simulate; num=N behaviours, default 2^20;\n"
@@ -236,7 +239,7 @@ int main(int argc, char** argv) {
     int simulate = 0, gpus = 1;
     std::string ckpt, recover, raft;
     uint32_t fopts = 0;
-    unsigned long long capacity = 0, window = 0;
+    unsigned long long capacity = 0, window = 0, fpmem = 0;
     int nospill = 0;
     for (int a = 1; a < argc; ++a) {
         std::string s = argv[a];
@@ -250,6 +253,16 @@ int main(int argc, char** argv) {
         else if (s == "-gpus") { const char* v = next(); if (!v) return usage(); gpus = atoi(v); }
         else if (s == "-verify") verify = 1;
         else if (s == "-nospill") nospill = 1;
+        else if (s == "-fpmem") {
+            const char* v = next();
+            if (!v) return usage();
+            char* e = nullptr;
+            fpmem = strtoull(v, &e, 10);
+            if (e && (*e == 'K' || *e == 'k')) fpmem <<= 10;
+            else if (e && (*e == 'M' || *e == 'm')) fpmem <<= 20;
+            else if (e && (*e == 'G' || *e == 'g')) fpmem <<= 30;
+            else if (e && *e) return usage();
+        }
         else if (s == "-window") { const char* v = next(); if (!v) return usage(); window = strtoull(v, nullptr, 10); }
         else if (s == "-raft") { const char* v = next(); if (!v) return usage(); raft = v; }
         else if (s == "-builtin-raft") fopts |= RMC_FRONT_BUILTIN_RAFT;
@@ -292,6 +305,7 @@ int main(int argc, char** argv) {
     if (!nospill && !(verify && (!ckpt.empty() || !recover.empty())) && gpus == 1 && rmc_state_bytes(&c) <= 64 * 4)
         c.flags |= RMC_FLAG_SPILL;
     c.device_window = window;
+    c.set_bytes = fpmem;
     c.seed = fpseed;
     printf("Model: %d servers, %d values, CONSTRAINT MaxTerm=%d MaxLogLen=%d MaxMsgs=%d MaxDup=%d%s%s\n",
            c.n_servers, c.n_values, c.max_term, c.max_log_len, c.max_msgs, c.max_dup,

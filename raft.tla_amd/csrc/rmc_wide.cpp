@@ -239,10 +239,19 @@ int create_wide(rmc_ctx* c) {
     size_t fr = 0, tot = 0;
     (void)hipMemGetInfo(&fr, &tot);
     const u64 budget = (u64)((double)fr * 0.80);
-    u64 cap = c->cfg.state_capacity ? c->cfg.state_capacity : budget / (per_state + 32);
+    const u64 set_slots = set_slots_of(c->cfg.set_bytes);  // rmc_config.set_bytes (TLC -fpmem)
+    u64 cap = c->cfg.state_capacity;
+    if (set_slots && cap > set_slots / 2) {
+        c->err = "state_capacity exceeds what a set of set_bytes " + std::to_string(c->cfg.set_bytes) + " holds";
+        return RMC_E_INVAL;
+    }
+    if (cap == 0)
+        cap = set_slots ? std::min<u64>(set_slots / 2, (budget - std::min<u64>(budget, set_slots * 8)) / per_state)
+                        : budget / (per_state + 32);
     cap = std::max<u64>(std::min<u64>(cap, 1ull << 33), 1024);
     u64 slots = 1;
     while (slots < 2 * cap) slots <<= 1;
+    if (set_slots) slots = std::max(slots, set_slots);
     c->table_slots = slots;
     WideBufs& B = c->WB;
     B = WideBufs{};
@@ -282,8 +291,9 @@ int run_bfs_wide(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     B.salt = wide_salt(c->cfg.seed);
     c->have_target = 0;
     c->res = rmc_result{};
+    c->res.set_slots = c->table_slots;
     c->level_start.clear();
-    HIPCHK(c, hipMemsetAsync(B.table, 0, c->table_slots * 8, c->st));
+    HIPCHK(c, launch_fill(B.table, c->table_slots * 8, 0, c->st));
     c->h_ctr->count = 0;
     if (int rc = reset_counters(c, false)) return rc;
     WState init;

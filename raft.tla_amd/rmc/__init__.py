@@ -45,7 +45,7 @@ class Config(C.Structure):
                 ("max_log_len", C.c_int32), ("max_msgs", C.c_int32), ("max_dup", C.c_int32),
                 ("flags", C.c_uint32), ("invariants", C.c_uint32), ("device", C.c_int32),
                 ("max_depth", C.c_int32), ("state_capacity", C.c_uint64), ("seed", C.c_uint64),
-                ("device_window", C.c_uint64)]
+                ("device_window", C.c_uint64), ("set_bytes", C.c_uint64)]
 
 
 class Result(C.Structure):
@@ -60,7 +60,7 @@ class Result(C.Structure):
                 ("spilled", C.c_uint64), ("spills", C.c_uint64), ("spill_seconds", C.c_double),
                 ("parked", C.c_uint64), ("exchange_wait_seconds", C.c_double),
                 ("spill_links_on_device", C.c_int32), ("pad2", C.c_int32),
-                ("verified_spilled", C.c_uint64)]
+                ("verified_spilled", C.c_uint64), ("set_slots", C.c_uint64)]
 
 
 class LevelStats(C.Structure):
@@ -207,12 +207,13 @@ class RmcError(RuntimeError):
 
 def make_config(n_servers=3, n_values=2, max_term=2, max_log_len=1, max_msgs=2, max_dup=1,
                 symmetry=False, bug_quorum=False, invariants=INV_TYPEOK, check_deadlock=True,
-                device=0, max_depth=0, state_capacity=0, verify_states=False, spill=False, device_window=0):
+                device=0, max_depth=0, state_capacity=0, verify_states=False, spill=False, device_window=0,
+                set_bytes=0):
     flags = (FLAG_SYMMETRY if symmetry else 0) | (FLAG_BUG_QUORUM if bug_quorum else 0) | \
         (FLAG_CHECK_DEADLOCK if check_deadlock else 0) | (FLAG_VERIFY_STATES if verify_states else 0) | \
         (FLAG_SPILL if spill else 0)
     return Config(n_servers, n_values, max_term, max_log_len, max_msgs, max_dup, flags,
-                  invariants, device, max_depth, state_capacity, 0, device_window)
+                  invariants, device, max_depth, state_capacity, 0, device_window, set_bytes)
 
 
 def model_from_files(cfg_path, tla_path=None, raft_path=None, builtin_raft=False, simulate=False,

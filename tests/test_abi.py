@@ -31,6 +31,26 @@ def test_library_exports_every_declared_symbol():
         assert re.search(rf"\bT {name}\b", out), name
 
 
+def header_struct_fields(name):
+    text = open(os.path.join(ROOT, "include", "rmc.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), text, flags=re.S).group(1)
+    names = []
+    for _, decl in re.findall(r"\b(u?int\d+_t|double|float)\s+([\w\s,\[\]]+);", body):
+        names += [re.sub(r"\[.*", "", d).strip() for d in decl.split(",")]
+    return names
+
+
+@pytest.mark.parametrize("cname,pyname", [("rmc_config", "Config"), ("rmc_result", "Result"),
+                                          ("rmc_sim_config", "SimConfig"), ("rmc_sim_result", "SimResult")])
+def test_ctypes_structs_mirror_the_header(cname, pyname):
+    """The Python binding's structs list the header's fields in order (a field
+    added to one and not the other shifts every later field)."""
+    want = header_struct_fields(cname)
+    got = [f[0] for f in getattr(rmc, pyname)._fields_]
+    assert got == want, (cname, got, want)
+
+
 def test_library_is_gfx950_code():
     blob = open(rmc.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob

@@ -68,6 +68,33 @@ def test_bfs_matches_oracle(name):
     assert res.violated_inv == 0 and res.deadlock == 0
 
 
+def test_set_bytes_sizes_the_fingerprint_set():
+    """rmc_config.set_bytes (TLC -fpmem) sizes the fingerprint set apart from the
+    store: a set just large enough for the run (load <= 0.5) gives the oracle's
+    counts, resident and spilling; a set too small for the run stops with a
+    capacity error at the level that passes it, not a wrong count; a
+    state_capacity the set cannot hold is refused at create."""
+    g = GOLDEN["bounded_full"]  # 78.1 M states
+    slots = 1 << (2 * g["distinct"] - 1).bit_length()  # 2^28
+    for spill in (False, True):
+        cfg = cfg_from(g["params"], capacity=0)
+        cfg.set_bytes = slots * 8 + 4095  # rounded down to a power of two of slots
+        if spill:
+            cfg.flags |= rmc.FLAG_SPILL
+        res, levels, _ = run(cfg)
+        assert levels == g["level_new"] and res.distinct == g["distinct"] and res.generated == g["generated"]
+    cfg = cfg_from(g["params"], capacity=0)
+    cfg.set_bytes = slots * 4  # holds 67.1 M states
+    with pytest.raises(rmc.RmcError) as e:
+        run(cfg)
+    assert e.value.code == -28
+    cfg = cfg_from(g["params"], capacity=slots)
+    cfg.set_bytes = slots * 8
+    with pytest.raises(rmc.RmcError) as e:
+        rmc.Checker(cfg)
+    assert e.value.code == -22
+
+
 SMALL_LAUNCHES = r"""
 import json, os, sys
 sys.path.insert(0, os.path.join(sys.argv[1], 'raft.tla_amd'))
