@@ -737,6 +737,25 @@ void rmc_destroy(rmc_ctx* c) {
     delete c;
 }
 
+// The most new states one state's expansion can yield: every lane yields at most
+// one, and the guards of raft.tla's Next (raft.tla:421-430) enable per server i at
+// most Restart + Timeout (a Follower, :136,146), Restart + Timeout + S x RequestVote +
+// BecomeLeader (a Candidate, :157-158,195-196) or Restart + V x ClientRequest +
+// AdvanceCommitIndex + (S - 1) x AppendEntries (a Leader, :171-173,206-207,219-220),
+// plus Receive, Duplicate and Drop per bag slot.  The spill window sizes its
+// launches by this bound (RMC_LANE_BOUND=0: every lane, the round-5 bound).
+static u64 max_new_per_state(const rmc_ctx* c) {
+    const u64 lanes = (u64)c->P.off[10];
+    static const bool all_lanes = [] {
+        const char* e = getenv("RMC_LANE_BOUND");
+        return e && atoi(e) == 0;
+    }();
+    if (all_lanes) return lanes;
+    const u64 S = (u64)c->sh.S, V = (u64)c->P.V, K = (u64)(c->P.off[8] - c->P.off[7]);
+    const u64 per_server = std::max<u64>(std::max<u64>(2, S + 3), S + V + 1);
+    return std::min<u64>(lanes, S * per_server + 3 * K);
+}
+
 int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (!c) return RMC_E_INVAL;
     HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -835,10 +854,10 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             b = std::min(hi, a + even);
             if (c->spill.on && c->spill.dev_links) {
                 // the ring window: [a, count) is live (the rest of the frontier and
-                // the level being built); every lane yields at most one new state, so
-                // a launch of n states cannot overwrite a live state when
-                // count + n * lanes <= a + win — nothing is ever moved
-                const u64 lanes = (u64)c->P.off[10], count = c->h_ctr->count, win = c->spill.win;
+                // the level being built); a state yields at most max_new_per_state
+                // new states, so a launch of n states cannot overwrite a live state
+                // when count + n * that <= a + win — nothing is ever moved
+                const u64 lanes = max_new_per_state(c), count = c->h_ctr->count, win = c->spill.win;
                 const u64 room = count - a < win ? a + win - count : 0;
                 u64 want = std::min(b - a, room / lanes);
                 if (c->sh.verify) want = std::min(want, c->B.hcap / lanes);  // hbuf holds every hit of a launch
@@ -858,12 +877,12 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                     c->B.vlo = vlo;
                 }
             } else if (c->spill.on) {
-                // every lane yields at most one new state: a launch of n states
-                // stays inside the window when n * lanes <= room.  Launches
+                // a state yields at most max_new_per_state new states: a launch of
+                // n states stays inside the window when n * that <= room.  Launches
                 // shrink as the window fills; below 2^20 states the expanded
                 // states [base, a) move to the host first — once they are at
                 // least 1/8 of what the move shifts down (or nothing fits)
-                const u64 lanes = (u64)c->P.off[10];
+                const u64 lanes = max_new_per_state(c);
                 const u64 count = c->h_ctr->count, fit = (c->B.cap - count) / lanes;
                 u64 want = b - a;
                 const u64 old = a - c->spill.base;
