@@ -424,12 +424,13 @@ int main(int argc, char** argv) {
                "  because two distinct states had the same fingerprint:\n"
                "  calculated (optimistic):  val = %.1E\n", r.collision_probability);
     }
-    if (verify)
+    if (verify) {
         printf("Full-state verification: %llu fingerprint hits compared state by state, %llu collisions.\n",
                (unsigned long long)r.verified, (unsigned long long)r.collisions);
         if (r.verified_spilled)
             printf("  (%llu of the hits were on states that had left the device window: compared with "
                    "their host copies)\n", (unsigned long long)r.verified_spilled);
+    }
     printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
            (unsigned long long)r.generated, (unsigned long long)r.distinct, (unsigned long long)r.left_on_queue);
     printf("The depth of the complete state graph search is %d.\n", r.depth);

@@ -14,6 +14,6 @@ fi
 timeout -k 10 300 python -u bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
 if [ -n "$DIST_BENCH" ]; then
-  timeout -k 10 300 python -u bench.py --force-dist --no-cpu --no-probe-ceiling --steps 5 > $O/bench_dist1.json 2> $O/bench_dist1.err || { tail -20 $O/bench_dist1.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --force-dist --config specs/MCraftBench.cfg --no-cpu --no-probe-ceiling --v2-config= --steps 5 > $O/bench_dist1.json 2> $O/bench_dist1.err || { tail -20 $O/bench_dist1.err; exit 1; }
   cat $O/bench_dist1.json
 fi

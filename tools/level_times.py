@@ -2,10 +2,11 @@
 one JSON line per level — level, frontier expanded, new states, generated,
 seconds since the start — for a TLC model file.  Measurement tool.
 
-    python tools/level_times.py specs/MCraftBench.cfg [capacity [max_depth [spill]]] > levels.jsonl
+    python tools/level_times.py specs/MCraftBench.cfg [capacity [max_depth [spill [set_bytes]]]] > levels.jsonl
 
-capacity 0: librmc's own sizing; `spill`: RMC_FLAG_SPILL (how bench.py runs
-specs/MCraftBenchXL.cfg on one GPU).
+capacity 0: librmc's own sizing; max_depth 0: to the fixpoint; `spill`:
+RMC_FLAG_SPILL (how bench.py runs specs/MCraftBenchXL.cfg on one GPU);
+set_bytes: rmc_config.set_bytes (bench.py's sparse set: 137438953472 for XL).
 """
 import json
 import os
@@ -21,6 +22,8 @@ if len(sys.argv) > 3:
     cfg.max_depth = int(sys.argv[3])  # a prefix of a model larger than one GPU
 if len(sys.argv) > 4 and sys.argv[4] == "spill":
     cfg.flags |= rmc.FLAG_SPILL
+if len(sys.argv) > 5:
+    cfg.set_bytes = int(sys.argv[5])
 with rmc.Checker(cfg) as ck:
     ck.run()  # warm
     r = ck.run()
