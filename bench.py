@@ -422,8 +422,11 @@ def main(argv=None):
             info = rdist.shard(ck, transport=transport, keys_per_dest=a.keys_per_dest,
                                sent_cache_slots=a.sent_cache)
             transport = info.transport
+        cold = []  # the ctx's first run clears the whole fingerprint set (librmc's set epochs: DESIGN.md §d)
         for _ in range(a.warmup):
+            tw = time.perf_counter()
             one_run(ck)
+            cold.append(time.perf_counter() - tw)
         barrier()
         if dist is not None:
             import torch
@@ -497,6 +500,12 @@ def main(argv=None):
             "distinct": D, "generated": G, "depth": depth,
             "time_to_fixpoint_s": per_step, "state_bytes": W,
             "fingerprint_set": {"slots": last[0].set_slots, "bytes": last[0].set_slots * 8,
+                                "epochs": ("tagged: each timed run takes the next set epoch instead of clearing "
+                                           "the set; the ctx's first run (the warmup) cleared it, and every 255th "
+                                           "run clears it (RMC_SET_EPOCH)")
+                                          if not sharded and os.environ.get("RMC_SET_EPOCH", "1") != "0"
+                                          else "cleared before every run",
+                                "first_run_ms_with_clear": cold[0] * 1e3 if cold else None,
                                 "load": (last[0].distinct / last[0].set_slots) if last[0].set_slots else None,
                                 "set_bytes": cfg.set_bytes, "capacity": cfg.state_capacity,
                                 "rule": "sparse_set_bytes: load <= 1/4 of the capacity (TLC -fpmem)"

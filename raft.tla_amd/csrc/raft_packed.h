@@ -106,6 +106,21 @@ static __constant__ u64 c_fp_salt;  // visible to both passes (HIP_SYMBOL needs 
 #else
 #define RMC_FP_SALT 0ull
 #endif
+// Set epoch (round 6): the tag of the current run's fingerprint-set entries in
+// their top 8 bits, epoch << 56, set per run with the salt (set_fp_salt); 0 =
+// untagged (the set cleared to 0 before the run: sharded, verification and
+// resumed runs).  A slot whose tag is not the run's epoch is empty — the
+// entries of earlier runs on the same ctx included — so a run on a ctx whose
+// set already holds tagged entries starts without clearing it (rmc_run_bfs:
+// every 255th run, and the first, clear it whole).
+#if defined(__HIPCC__)
+static __constant__ u64 c_set_ep;
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RMC_SET_EP c_set_ep
+#else
+#define RMC_SET_EP 0ull
+#endif
 RMC_HD u64 hS(u64 w, u32 i) { return mix64(w ^ ((u64)(i + 1) << 59) ^ RMC_FP_SALT); }
 RMC_HD u64 hM(u32 slot) { return slot ? mix64((u64)slot ^ (0x1Full << 59) ^ RMC_FP_SALT) : 0ull; }
 
@@ -129,12 +144,19 @@ RMC_HD Fp fp_of(u64 a) { return Fp{a, smix(a)}; }
 RMC_HD void fp_add(Fp& h, u64 a) { h.k += a; h.s += smix(a); }
 RMC_HD void fp_sub(Fp& h, u64 a) { h.k -= a; h.s -= smix(a); }
 // A fingerprint's place in a table of mask + 1 slots: the value stored /
-// compared, v = k ^ (s & mask) (never 0, the empty slot), and the first slot
+// compared, v = k ^ (s & mask) (never 0, the empty slot; a tagged set replaces
+// its top 8 bits by the run's epoch: 56 + min(32, log2 slots) bits), and the first slot
 // of its probe sequence, k & mask.  The one fingerprint whose value would be 0
 // flips bit 0 of s (fp_norm, in every caller alike), so the slot is always
 // (v ^ s) & mask and callers may keep (v, s) only (fp_slot).
 RMC_HD u32 fp_norm(u64 k, u32 s32, u64 mask) { return (k ^ ((u64)s32 & mask)) == 0 ? (s32 ^ 1u) : s32; }
-RMC_HD u64 fp_v(u64 k, u32 s32n, u64 mask) { return k ^ ((u64)s32n & mask); }
+RMC_HD u64 fp_v(u64 k, u32 s32n, u64 mask) {
+    const u64 v = k ^ ((u64)s32n & mask);
+    // a tagged set keeps the low 56 bits (mask < 2^56) under the run's epoch
+    return RMC_SET_EP ? (v & ((1ull << 56) - 1)) | RMC_SET_EP : v;
+}
+// An empty slot: 0, or (tagged set) an entry of another run's epoch.
+RMC_HD bool fp_empty(u64 cur) { return RMC_SET_EP ? ((cur ^ RMC_SET_EP) >> 56) != 0 : cur == 0; }
 RMC_HD u64 fp_slot(u64 v, u32 s32n, u64 mask) { return (v ^ (u64)s32n) & mask; }
 struct TKey {
     u64 v, s0;

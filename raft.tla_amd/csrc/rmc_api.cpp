@@ -770,7 +770,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (resume) {
         c->res.left_on_queue = 0;
         c->res.seconds = 0;
-        HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
+        HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->set_epoch, c->st));
         c->h_ctr->count = c->level_start.back();
         if (int rc = reset_counters(c, true)) return rc;
         depth = c->resume_depth;
@@ -793,9 +793,22 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
             });
         }
     }
-    HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+    // The set epoch (raft_packed.h c_set_ep): a run on a ctx whose set holds the
+    // tagged entries of an earlier run takes the next epoch and clears nothing —
+    // their slots read as empty.  The first run of a ctx, every 255th and runs
+    // with verification (whose slot -> state map is cleared anyway) clear the set
+    // (RMC_SET_EPOCH=0: every run clears; =N: at most N epochs between clears).
+    const char* epe = getenv("RMC_SET_EPOCH");  // (read per run: tests vary it)
+    const u32 ep_max = epe ? (u32)std::min(255, std::max(0, atoi(epe))) : 255u;
+    const bool tagged = ep_max > 0 && !c->sh.verify;
+    if (tagged && c->set_epoch >= 1 && c->set_epoch < ep_max) {
+        c->set_epoch += 1;
+    } else {
+        HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+        c->set_epoch = tagged ? 1 : 0;
+    }
     if (c->sh.verify) HIPCHK(c, launch_fill(c->B.sidx, c->table_slots * 8, 0xFF, c->st));
-    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->set_epoch, c->st));
     if (int rc = reset_counters(c, false)) return rc;
     c->B.vlo = 0;
     c->spill.hcopied = 0;
@@ -989,7 +1002,7 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.verified_spilled = c->spill.host_hits;
     const double D = (double)c->res.distinct, G = (double)c->res.generated;
     // TLC's "calculated (optimistic)" fingerprint-collision estimate
-    c->res.collision_probability = fp_collision_estimate(D, G, c->table_slots);
+    c->res.collision_probability = fp_collision_estimate(D, G, c->table_slots, c->set_epoch != 0);
     c->res.seconds = secs();
     // lane efficiency of the walk: enabled lanes / visited slots (the kernels count
     // the slots only when built with -DRMC_WALK_STATS_BUILD: a register in the hot loop)
@@ -1105,6 +1118,7 @@ int rmc_checkpoint(rmc_ctx* c, const char* path) {
     const u64 base = c->spill.on ? c->spill.base : 0;
     h.first = base ? c->level_start[h.nlevels - 2] : 0;  // >= base at a level boundary
     h.slots = base ? c->table_slots : 0;
+    h.pad_ = h.slots ? c->set_epoch : 0;  // the dumped set's epoch tag (0: untagged)
     int rc = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(c->level_start.data(), 8, h.nlevels, f) == h.nlevels
                  ? 0 : fail(c, RMC_E_IO, "checkpoint write failed");
     auto put = [&](const void* p, u64 n) {
@@ -1197,7 +1211,10 @@ int rmc_recover(rmc_ctx* c, const char* path) {
     // diamond skipping (FOOT_VALID clear), the levels after it with
     HIPCHK(c, hipMemsetAsync(c->spill.on ? c->spill.foot : c->B.foot, 0,
                              (c->spill.on ? c->spill.win : c->B.cap) * 8, c->st));
-    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
+    // a dumped set keeps its entries' epoch tag (header pad_); states rehashed
+    // below go into an untagged set
+    c->set_epoch = h.slots ? std::min<u32>(h.pad_, 255u) : 0u;
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->set_epoch, c->st));
     if (int r2 = reset_counters(c, false)) return r2;
     const u64 ls0 = c->spill.dev_links ? 0 : s;  // links below ls0 go to the host
     if (ls0) get(c->spill.h_parent, ls0 * 8);

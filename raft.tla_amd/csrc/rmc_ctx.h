@@ -140,6 +140,10 @@ struct rmc_ctx {
     rmc::Counters* h_ctr = nullptr;  // pinned
     rmc::u32* d_staged = nullptr;
     rmc::u64 table_slots = 0;
+    // the epoch the set's current entries carry (raft_packed.h c_set_ep): 0 = untagged
+    // (cleared to 0 by the last run, or unknown), 1..255 = tagged; the next plain
+    // single-GPU run takes the next epoch without clearing the set (rmc_run_bfs)
+    rmc::u32 set_epoch = 0;
     rmc::u64 walked = 0;  // (state, lane) slots of the lane walk in the last run (RMC_WALK_STATS)
     rmc_result res{};
     std::string err;
@@ -170,10 +174,11 @@ namespace rmc_host {
 // TLC's "calculated (optimistic)" collision estimate D * (G - D) / 2^b for the
 // fingerprint bits b the set compares: 64 of k plus the bits of the second sum
 // folded in under the slot mask, min(32, log2 slots) (raft_packed.h Fp).
-inline double fp_collision_estimate(double D, double G, rmc::u64 slots) {
+inline double fp_collision_estimate(double D, double G, rmc::u64 slots, bool tagged = false) {
     int lb = 0;
     while (lb < 32 && (2ull << lb) <= slots) ++lb;
-    return D * (G - D) / 18446744073709551616.0 / (double)(1ull << lb);
+    // a tagged set compares 56 + lb bits (the top 8 hold the run's epoch)
+    return D * (G - D) / 18446744073709551616.0 / (double)(1ull << lb) * (tagged ? 256.0 : 1.0);
 }
 int fail(rmc_ctx* c, int code, const std::string& msg);
 int kcap_for(int max_msgs);

@@ -427,7 +427,8 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     if (c->B.sent) HIPCHK(c, launch_fill(c->B.sent, D.sent_slots * 8, 0, c->st));
     const bool verify = c->sh.verify;
     if (verify && !resume) HIPCHK(c, launch_fill(c->B.sidx, c->table_slots * 8, 0xFF, c->st));
-    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->st));
+    c->set_epoch = 0;  // sharded: an untagged set, cleared before the run (raft_packed.h c_set_ep)
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, 0, c->st));
     if (resume) c->h_ctr->count = c->level_start.back();
     if (int rc = reset_counters(c, resume)) return rc;
     // ---- Init (raft.tla:125-129): stored by its owner only

@@ -164,7 +164,9 @@ constexpr u64 POOL_TICK = 1ull << 48;
 
 // Fingerprint salt for the kernels of shape sh on this device (0 = default
 // hash); returns after the copy (the staging value lives on the caller's stack).
-hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st);
+// the fingerprint salt of rmc_config.seed and the set epoch of the run (raft_packed.h
+// c_set_ep: 0 = an untagged set, cleared before the run)
+hipError_t set_fp_salt(const Shape& sh, u64 seed, u32 set_epoch, hipStream_t st);
 
 // Sets bytes [p, p + bytes) to `byte` (the fingerprint set's clear; RMC_FILL=0: hipMemsetAsync).
 hipError_t launch_fill(void* p, u64 bytes, uint8_t byte, hipStream_t st);

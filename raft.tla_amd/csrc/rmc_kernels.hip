@@ -38,9 +38,9 @@ __device__ __forceinline__ int fp_insert(u64* __restrict__ table, u64 mask, u64 
     for (u64 n = 0; n <= mask; ++n) {
         const u64 cur = table[s];
         if (cur == key) return 0;
-        if (cur == 0) {
-            const u64 prev = atomicCAS((unsigned long long*)&table[s], 0ull, (unsigned long long)key);
-            if (prev == 0) return 1;
+        if (fp_empty(cur)) {  // 0, or another epoch's entry (a tagged set)
+            const u64 prev = atomicCAS((unsigned long long*)&table[s], (unsigned long long)cur, (unsigned long long)key);
+            if (prev == cur) return 1;
             if (prev == key) return 0;
         }
         s = (s + 1) & mask;
@@ -55,9 +55,9 @@ __device__ __forceinline__ int fp_insert_at(u64* __restrict__ table, u64 mask, u
     for (u64 n = 0; n <= mask; ++n) {
         const u64 cur = table[s];
         if (cur == key) { *at = s; return 0; }
-        if (cur == 0) {
-            const u64 prev = atomicCAS((unsigned long long*)&table[s], 0ull, (unsigned long long)key);
-            if (prev == 0) { *at = s; return 1; }
+        if (fp_empty(cur)) {
+            const u64 prev = atomicCAS((unsigned long long*)&table[s], (unsigned long long)cur, (unsigned long long)key);
+            if (prev == cur) { *at = s; return 1; }
             if (prev == key) { *at = s; return 0; }
         }
         s = (s + 1) & mask;
@@ -70,9 +70,9 @@ __device__ __forceinline__ int fp_insert_at(u64* __restrict__ table, u64 mask, u
 // Same protocol, given the already-loaded content `cur` of the first slot s0.
 __device__ __forceinline__ int fp_resolve(u64* __restrict__ table, u64 mask, u64 s0, u64 key, u64 cur, u32* full) {
     if (cur == key) return 0;
-    if (cur == 0) {
-        const u64 prev = atomicCAS((unsigned long long*)&table[s0], 0ull, (unsigned long long)key);
-        if (prev == 0) return 1;
+    if (fp_empty(cur)) {
+        const u64 prev = atomicCAS((unsigned long long*)&table[s0], (unsigned long long)cur, (unsigned long long)key);
+        if (prev == cur) return 1;
         if (prev == key) return 0;
     }
     return fp_insert(table, mask, s0, key, full);  // rare: continue linear probing
@@ -1160,10 +1160,11 @@ __device__ __forceinline__ void expand_body(const Params& P, const PermTable& PT
                         continue;
                     }
                 }
-                if (cur[b] == 0) {
+                if (fp_empty(cur[b])) {  // 0, or another epoch's entry: CAS it away
                     const u64 sl0 = fp_slot(key[b], s_ks[b][threadIdx.x], B.tmask);
-                    const u64 prev = atomicCAS((unsigned long long*)&B.table[sl0], 0ull, (unsigned long long)key[b]);
-                    if (prev == 0) newbits |= 1u << b;
+                    const u64 prev = atomicCAS((unsigned long long*)&B.table[sl0], (unsigned long long)cur[b],
+                                               (unsigned long long)key[b]);
+                    if (prev == cur[b]) newbits |= 1u << b;
                     else if (prev != key[b]) slowbits |= 1u << b;
                     else if constexpr (VERIFY) {
                         hitbits |= 1u << b;
@@ -2331,7 +2332,7 @@ static hipError_t launch_sk(bool sym, bool verify, int which, const Params& P, c
     hipError_t launch_sim_shape_##SS##_##KK(const Params& P, const u32* inits, u64 n_init, u64 n_beh, int depth, \
                                             u64 seed, int mode, SimCounters* out, i64 rec_beh, u32* rec,        \
                                             hipStream_t st);                                                    \
-    hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, hipStream_t st);
+    hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, u64 ep, hipStream_t st);
 RMC_SHAPES(RMC_SHAPE_DECLS)
 
 #ifdef RMC_SHAPE_S
@@ -2346,12 +2347,14 @@ RMC_SHAPES(RMC_SHAPE_DECLS)
                                             hipStream_t st) {                                                   \
         return launch_sim_t<SS, KK>(P, inits, n_init, n_beh, depth, seed, mode, out, rec_beh, rec, st);        \
     }                                                                                                           \
-    hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, hipStream_t st) {                                        \
+    hipError_t set_fp_salt_shape_##SS##_##KK(u64 salt, u64 ep, hipStream_t st) {                                \
         /* staged on this call's stack and waited for: concurrent callers (one host */                          \
         /* thread per GPU in rmc-tlc -gpus N) share no staging buffer */                                        \
-        const u64 h_salt = salt;                                                                                \
-        const hipError_t e =                                                                                    \
+        const u64 h_salt = salt, h_ep = ep;                                                                     \
+        hipError_t e =                                                                                          \
             hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fp_salt), &h_salt, sizeof h_salt, 0, hipMemcpyHostToDevice, st); \
+        if (e == hipSuccess)                                                                                    \
+            e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_set_ep), &h_ep, sizeof h_ep, 0, hipMemcpyHostToDevice, st); \
         return e != hipSuccess ? e : hipStreamSynchronize(st);                                                  \
     }
 #define RMC_DEFINE_SHAPE_(SS, KK) RMC_DEFINE_SHAPE(SS, KK)
@@ -2359,11 +2362,13 @@ RMC_DEFINE_SHAPE_(RMC_SHAPE_S, RMC_SHAPE_K)
 #else
 
 
-hipError_t set_fp_salt(const Shape& sh, u64 seed, hipStream_t st) {
+hipError_t set_fp_salt(const Shape& sh, u64 seed, u32 set_epoch, hipStream_t st) {
     const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
+    if (set_epoch > 255) return hipErrorInvalidValue;
+    const u64 ep = (u64)set_epoch << 56;
     // only the ctx's shape object runs its kernels
 #define RMC_SET_SALT(SS, KK) \
-    if (sh.S == SS && sh.K == KK) return set_fp_salt_shape_##SS##_##KK(salt, st);
+    if (sh.S == SS && sh.K == KK) return set_fp_salt_shape_##SS##_##KK(salt, ep, st);
     RMC_SHAPES(RMC_SET_SALT)
 #undef RMC_SET_SALT
     return hipErrorInvalidValue;

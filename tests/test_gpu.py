@@ -183,6 +183,59 @@ def test_fingerprint_salt_does_not_change_counts():
     assert levels == g["level_new"]
 
 
+@pytest.mark.parametrize("name,spill,ep_max", [("bounded_full", False, None), ("small_sym", False, None),
+                                               ("small", False, "2"), ("bounded_full", True, None),
+                                               ("small_sym", True, "3"), ("s5_prefix9", False, None)])
+def test_set_epochs_repeated_runs_equal_the_oracle(name, spill, ep_max, monkeypatch):
+    """Set epochs (raft_packed.h c_set_ep): runs after a ctx's first take the next
+    epoch instead of clearing the fingerprint set, and the earlier runs' entries
+    read as empty.  Six runs on one ctx, alternating two fingerprint salts (the
+    same states land in other slots under other keys), each equal to the oracle
+    level by level; RMC_SET_EPOCH=N wraps the epoch (a full clear) every N runs,
+    and a run with RMC_SET_EPOCH=0 in between clears the set and leaves it untagged."""
+    if ep_max is not None:
+        monkeypatch.setenv("RMC_SET_EPOCH", ep_max)
+    if spill:
+        g, cfg = spill_cfg(name, 1 << 16)
+    else:
+        g = GOLDEN[name]
+        cfg = cfg_from(g["params"], capacity=max(1 << 20, int(g["distinct"] * 1.25)))
+    with rmc.Checker(cfg) as ck:
+        for i in range(6):
+            ck.set_seed(0 if i % 2 == 0 else 0x5A17ED + i)
+            if i == 4:
+                monkeypatch.setenv("RMC_SET_EPOCH", "0")
+            elif i == 5:
+                monkeypatch.setenv("RMC_SET_EPOCH", ep_max or "255")
+            res = ck.run()
+            levels = [1] + [lv[3] for lv in ck.levels if lv[3]]
+            assert (res.distinct, res.generated, res.depth, res.left_on_queue) == \
+                (g["distinct"], g["generated"], g["depth"], g["left_on_queue"]), i
+            assert levels == g["level_new"], i
+            assert (res.spills > 0) == spill
+
+
+def test_set_epochs_checkpoint_of_a_later_run_recovers(tmp_path):
+    """A spilled checkpoint dumps the fingerprint set with its entries' epoch
+    tag (header pad_); recovering it into a fresh ctx adopts that epoch, so the
+    set of a ctx's third run (epoch 3) recovers like a first run's."""
+    g, cfg = spill_cfg("tiny2_v2", 4096, max_depth=30)
+    with rmc.Checker(cfg) as ck:
+        for _ in range(3):
+            r1 = ck.run()
+        assert r1.depth == 30 and r1.spills > 0
+        ck.checkpoint(str(tmp_path / "ck"))
+    _, cfg2 = spill_cfg("tiny2_v2", 4096)
+    with rmc.Checker(cfg2) as ck:
+        ck.recover(str(tmp_path / "ck"))
+        r2 = ck.run()
+        levels = [lv[3] for lv in ck.levels if lv[3]]
+        assert (r2.distinct, r2.generated, r2.depth) == (g["distinct"], g["generated"], g["depth"])
+        assert levels == g["level_new"][30:]
+        r3 = ck.run()  # a fresh run on the recovered ctx: the next epoch over the recovered set
+        assert (r3.distinct, r3.generated, r3.depth) == (g["distinct"], g["generated"], g["depth"])
+
+
 @pytest.mark.parametrize("name", ["small", "s5_prefix9", "bug_log_matching", "bounded_full", "small_sym",
                                   "s4_sym_prefix16", "sym_bug_one_leader"])
 def test_full_state_verification_is_exact(name):
