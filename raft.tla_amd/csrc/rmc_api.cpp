@@ -878,7 +878,11 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                     return fail(c, RMC_E_CAPACITY,
                                 "spill: the device window (" + std::to_string(win) +
                                     " states) cannot hold the frontier and the level being built; raise "
-                                    "rmc_config.device_window");
+                                    "rmc_config.device_window, or give the fingerprint set less HBM "
+                                    "(rmc_config.set_bytes, rmc-tlc -fpmem: its " +
+                                    std::to_string(c->table_slots) + " slots take " +
+                                    std::to_string((c->table_slots * (c->sh.verify ? 16 : 8)) >> 30) +
+                                    " GiB) so the window gets more");
                 b = a + want;
                 if (c->sh.verify) {
                     // the launch may overwrite the ring slots of states below
@@ -911,7 +915,11 @@ int rmc_run_bfs(rmc_ctx* c, rmc_progress_fn cb, void* user) {
                     return fail(c, RMC_E_CAPACITY,
                                 "spill: the device window (" + std::to_string(c->spill.win) +
                                     " states) cannot hold the frontier and the level being built; raise "
-                                    "rmc_config.device_window");
+                                    "rmc_config.device_window, or give the fingerprint set less HBM "
+                                    "(rmc_config.set_bytes, rmc-tlc -fpmem: its " +
+                                    std::to_string(c->table_slots) + " slots take " +
+                                    std::to_string((c->table_slots * (c->sh.verify ? 16 : 8)) >> 30) +
+                                    " GiB) so the window gets more");
                 b = a + want;
             }
             HIPCHK(c, launch(c->sh, 0, c->P, c->PT, c->B, a, b, nullptr, nullptr, 0, nullptr, c->st));

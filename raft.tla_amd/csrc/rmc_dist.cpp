@@ -1013,7 +1013,11 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
     // send markers share the fingerprint set with this rank's states: twice the
     // slots keeps the load of linear probing near the single-GPU one (when
     // HBM allows; otherwise the set stays as rmc_create sized it)
-    if (world > 1 && !c->sh.verify && !c->sh.sym && !D.table_grown) {
+    // (only with 8 GiB to spare after the larger set is allocated: the kernels'
+    // scratch, RCCL and other ranks sharing the device allocate after this)
+    size_t mfree = 0, mtot = 0;
+    (void)hipMemGetInfo(&mfree, &mtot);
+    if (world > 1 && !c->sh.verify && !c->sh.sym && !D.table_grown && mfree >= c->table_slots * 16 + (8ull << 30)) {
         u64* t2 = nullptr;
         if (hipMalloc(&t2, c->table_slots * 16) == hipSuccess) {
             (void)hipFree(c->B.table);
