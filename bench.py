@@ -46,7 +46,7 @@ def parse(argv=None):
                          "round measured; any other model: librmc's own sizing, 80%% of free HBM)")
     ap.add_argument("--set-bytes", type=int, default=-1,
                     help="fingerprint-set bytes per GPU (rmc_config.set_bytes, TLC -fpmem; 0: librmc's sizing, "
-                         "load <= 1/2; -1: the bench default, load <= 1/4 of the capacity: sparse_set_bytes)")
+                         "load <= 1/2; -1: the bench default, sparse_set_bytes: 8 slots per state of capacity, 4 sharded)")
     ap.add_argument("--spill", default="auto", choices=("auto", "on", "off"),
                     help="RMC_FLAG_SPILL (expanded levels leave the device window; their trace links stay in "
                          "HBM): auto = on for a single GPU unless the model is MCraftBench.cfg")
@@ -245,15 +245,19 @@ def pmc_traffic(config_path):
     return None, None
 
 
-def sparse_set_bytes(capacity):
+def sparse_set_bytes(capacity, per_state=4):
     """The bench's fingerprint-set size (rmc_config.set_bytes, TLC -fpmem): 8-B
-    slots for four times the states the GPU may store, rounded up to a power of
-    two — load <= 1/4 instead of librmc's default 1/2.  A probe for a new state
-    ends at the first empty slot, one dependent load per occupied slot before
-    it: doubling the set took XL 731 -> 704 ms and MCraftBench 210 -> 198 ms on
-    one box, its larger clear included (profiles/r06/ab/set_size.txt)."""
+    slots for `per_state` times the states the GPU may store, rounded up to a
+    power of two (librmc halves it until the store fits beside it) — load <= 1/4
+    instead of librmc's default 1/2.  A probe for a new state ends at the first
+    empty slot, one dependent load per occupied slot before it: doubling the set
+    took XL 731 -> 704 ms and MCraftBench 210 -> 198 ms on one box, its larger
+    clear included (profiles/r06/ab/set_size.txt).  One GPU takes 8 slots per
+    state: with set epochs its runs no longer clear the set, and MCraftBench's
+    2^34 slots measured 184.8-186.1 against 188.6-191.2 ms for 2^33
+    (profiles/r06/ab/set_size_mcraftbench.txt); XL stays at 2^34, what fits."""
     slots = 1
-    while slots < 4 * capacity:
+    while slots < per_state * capacity:
         slots <<= 1
     return slots * 8
 
@@ -281,7 +285,7 @@ def v2_fixpoint(path, dev, runs=3):
     c = rmc.config_from_files(path, builtin_raft=True)
     c.device = dev
     c.state_capacity = int(1.5e9)  # resident, no spill (the size every round measured)
-    c.set_bytes = sparse_set_bytes(c.state_capacity)
+    c.set_bytes = sparse_set_bytes(c.state_capacity, 8)
     ts = []
     with rmc.Checker(c) as ck:
         ck.run(record_levels=False)
@@ -392,8 +396,8 @@ def main(argv=None):
         cfg.state_capacity = 0
     if a.set_bytes >= 0:
         cfg.set_bytes = a.set_bytes
-    elif cfg.state_capacity:
-        cfg.set_bytes = sparse_set_bytes(cfg.state_capacity)
+    elif cfg.state_capacity:  # sharded runs clear their set every run (no set epochs): 4 slots per state
+        cfg.set_bytes = sparse_set_bytes(cfg.state_capacity, 4 if sharded else 8)
     spill = (a.spill == "on" or (a.spill == "auto" and not small)) and not sharded
     if spill:
         cfg.flags |= rmc.FLAG_SPILL
@@ -508,7 +512,7 @@ def main(argv=None):
                                 "first_run_ms_with_clear": cold[0] * 1e3 if cold else None,
                                 "load": (last[0].distinct / last[0].set_slots) if last[0].set_slots else None,
                                 "set_bytes": cfg.set_bytes, "capacity": cfg.state_capacity,
-                                "rule": "sparse_set_bytes: load <= 1/4 of the capacity (TLC -fpmem)"
+                                "rule": "sparse_set_bytes: 8 (sharded: 4) slots per state of capacity, halved by librmc until the store fits (TLC -fpmem)"
                                         if a.set_bytes < 0 and cfg.set_bytes else "set_bytes given / librmc's"},
             "spill": ({"flag": "RMC_FLAG_SPILL", "trace_links": "device" if last[0].spill_links_on_device else "host",
                        "window": ("ring (slot reuse, nothing copied)" if last[0].spill_links_on_device
