@@ -46,7 +46,7 @@ def parse(argv=None):
                          "round measured; any other model: librmc's own sizing, 80%% of free HBM)")
     ap.add_argument("--set-bytes", type=int, default=-1,
                     help="fingerprint-set bytes per GPU (rmc_config.set_bytes, TLC -fpmem; 0: librmc's sizing, "
-                         "load <= 1/2; -1: the bench default, sparse_set_bytes: 8 slots per state of capacity, 4 sharded)")
+                         "load <= 1/2; -1: the bench default, sparse_set_bytes: 8 slots per state of capacity)")
     ap.add_argument("--spill", default="auto", choices=("auto", "on", "off"),
                     help="RMC_FLAG_SPILL (expanded levels leave the device window; their trace links stay in "
                          "HBM): auto = on for a single GPU unless the model is MCraftBench.cfg")
@@ -252,7 +252,7 @@ def sparse_set_bytes(capacity, per_state=4):
     instead of librmc's default 1/2.  A probe for a new state ends at the first
     empty slot, one dependent load per occupied slot before it: doubling the set
     took XL 731 -> 704 ms and MCraftBench 210 -> 198 ms on one box, its larger
-    clear included (profiles/r06/ab/set_size.txt).  One GPU takes 8 slots per
+    clear included (profiles/r06/ab/set_size.txt).  The bench takes 8 slots per
     state: with set epochs its runs no longer clear the set, and MCraftBench's
     2^34 slots measured 184.8-186.1 against 188.6-191.2 ms for 2^33
     (profiles/r06/ab/set_size_mcraftbench.txt); XL stays at 2^34, what fits."""
@@ -396,8 +396,8 @@ def main(argv=None):
         cfg.state_capacity = 0
     if a.set_bytes >= 0:
         cfg.set_bytes = a.set_bytes
-    elif cfg.state_capacity:  # sharded runs clear their set every run (no set epochs): 4 slots per state
-        cfg.set_bytes = sparse_set_bytes(cfg.state_capacity, 4 if sharded else 8)
+    elif cfg.state_capacity:  # 8 slots per state (set epochs: a larger set costs no clear per run)
+        cfg.set_bytes = sparse_set_bytes(cfg.state_capacity, 8)
     spill = (a.spill == "on" or (a.spill == "auto" and not small)) and not sharded
     if spill:
         cfg.flags |= rmc.FLAG_SPILL
@@ -507,12 +507,12 @@ def main(argv=None):
                                 "epochs": ("tagged: each timed run takes the next set epoch instead of clearing "
                                            "the set; the ctx's first run (the warmup) cleared it, and every 255th "
                                            "run clears it (RMC_SET_EPOCH)")
-                                          if not sharded and os.environ.get("RMC_SET_EPOCH", "1") != "0"
+                                          if os.environ.get("RMC_SET_EPOCH", "1") != "0"
                                           else "cleared before every run",
                                 "first_run_ms_with_clear": cold[0] * 1e3 if cold else None,
                                 "load": (last[0].distinct / last[0].set_slots) if last[0].set_slots else None,
                                 "set_bytes": cfg.set_bytes, "capacity": cfg.state_capacity,
-                                "rule": "sparse_set_bytes: 8 (sharded: 4) slots per state of capacity, halved by librmc until the store fits (TLC -fpmem)"
+                                "rule": "sparse_set_bytes: 8 slots per state of capacity, halved by librmc until the store fits (TLC -fpmem)"
                                         if a.set_bytes < 0 and cfg.set_bytes else "set_bytes given / librmc's"},
             "spill": ({"flag": "RMC_FLAG_SPILL", "trace_links": "device" if last[0].spill_links_on_device else "host",
                        "window": ("ring (slot reuse, nothing copied)" if last[0].spill_links_on_device

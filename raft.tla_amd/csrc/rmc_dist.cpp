@@ -423,12 +423,26 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     D.keys_sent = D.states_sent = D.chunks = D.parked = 0;
     D.xfer_seconds = D.wait_seconds = 0;
     D.rep_levels = 0;
-    if (!resume) HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+    // Set epochs as on one GPU (rmc_run_bfs, raft_packed.h c_set_ep): a run after
+    // the ctx's first takes the next epoch instead of clearing the set.  The
+    // send-marker kernels re-derive every remote key from its materialised
+    // successor, never from a set value; SYMMETRY and verification (the lossy
+    // sent-cache kernel recovers raw keys from set values) keep an untagged set.
+    const char* epe = getenv("RMC_SET_EPOCH");
+    const u32 ep_max = epe ? (u32)std::min(255, std::max(0, atoi(epe))) : 255u;
+    const bool tagged = ep_max > 0 && !c->sh.verify && !c->sh.sym;
+    if (!resume) {
+        if (tagged && c->set_epoch >= 1 && c->set_epoch < ep_max) {
+            c->set_epoch += 1;
+        } else {
+            HIPCHK(c, launch_fill(c->B.table, c->table_slots * 8, 0, c->st));
+            c->set_epoch = tagged ? 1 : 0;
+        }
+    }
     if (c->B.sent) HIPCHK(c, launch_fill(c->B.sent, D.sent_slots * 8, 0, c->st));
     const bool verify = c->sh.verify;
     if (verify && !resume) HIPCHK(c, launch_fill(c->B.sidx, c->table_slots * 8, 0xFF, c->st));
-    c->set_epoch = 0;  // sharded: an untagged set, cleared before the run (raft_packed.h c_set_ep)
-    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, 0, c->st));
+    HIPCHK(c, set_fp_salt(c->sh, c->cfg.seed, c->set_epoch, c->st));
     if (resume) c->h_ctr->count = c->level_start.back();
     if (int rc = reset_counters(c, resume)) return rc;
     // ---- Init (raft.tla:125-129): stored by its owner only
@@ -876,7 +890,7 @@ int run_bfs_sharded(rmc_ctx* c, rmc_progress_fn cb, void* user) {
     c->res.exchange_wait_seconds = D.wait_seconds;
     c->res.parked = D.parked;
     const double Dd = (double)total_prev, G = (double)generated;
-    c->res.collision_probability = fp_collision_estimate(Dd, G, c->table_slots);
+    c->res.collision_probability = fp_collision_estimate(Dd, G, c->table_slots, c->set_epoch != 0);
     c->res.seconds = now_s() - t0;
     D.phase = "done";
     return 0;
@@ -1024,6 +1038,7 @@ int rmc_shard(rmc_ctx* c, int32_t rank, int32_t world, const uint8_t* rccl_id, c
             c->B.table = t2;
             c->table_slots *= 2;
             c->B.tmask = c->table_slots - 1;
+            c->set_epoch = 0;  // a new, uncleared set: the next run clears it
             D.table_grown = 1;
         }
     }

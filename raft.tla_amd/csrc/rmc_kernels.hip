@@ -2366,7 +2366,13 @@ hipError_t set_fp_salt(const Shape& sh, u64 seed, u32 set_epoch, hipStream_t st)
     const u64 salt = seed ? (mix64(seed) & ((1ull << 59) - 1)) : 0ull;
     if (set_epoch > 255) return hipErrorInvalidValue;
     const u64 ep = (u64)set_epoch << 56;
-    // only the ctx's shape object runs its kernels
+    // the common object's kernels insert too (k_owner_insert: sharded keys received)
+    {
+        const u64 h_ep = ep;
+        const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_set_ep), &h_ep, sizeof h_ep, 0, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    // only the ctx's shape object runs its kernels (the call waits for both copies)
 #define RMC_SET_SALT(SS, KK) \
     if (sh.S == SS && sh.K == KK) return set_fp_salt_shape_##SS##_##KK(salt, ep, st);
     RMC_SHAPES(RMC_SET_SALT)

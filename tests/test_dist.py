@@ -106,6 +106,34 @@ def test_sharded_bfs_matches_oracle(case, nproc, backend, rep, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case,nproc,backend,ep_max", [("small", 2, "gloo", None), ("s4_prefix10", 3, "gloo", "2"),
+                                                      ("tiny2_log3", 3, "gloo", None), ("small", 1, "nccl", None)])
+def test_sharded_set_epochs_reruns_equal_the_oracle(case, nproc, backend, ep_max, tmp_path):
+    """Set epochs on the sharded send-marker path: after a ctx's first run each
+    rank's set is not cleared but takes the next epoch (RMC_SET_EPOCH=2: a full
+    clear every second run); four more runs on the same sharded ctxs equal the
+    oracle."""
+    g = GOLDEN[case]
+    out = tmp_path / "r.json"
+    env_keep = os.environ.get("RMC_SET_EPOCH")
+    if ep_max is not None:
+        os.environ["RMC_SET_EPOCH"] = ep_max
+    try:
+        r = _torchrun(nproc, [os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case, "--out",
+                              str(out), "--device", "0", "--backend", backend, "--rerun", "4"], 29660 + nproc)
+    finally:
+        if ep_max is not None:
+            if env_keep is None:
+                os.environ.pop("RMC_SET_EPOCH", None)
+            else:
+                os.environ["RMC_SET_EPOCH"] = env_keep
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert (res["distinct"], res["generated"], res["depth"]) == (g["distinct"], g["generated"], g["depth"])
+    assert res["rerun"] == [[g["distinct"], g["generated"], g["depth"]]] * 4
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case,nproc", [("bug_one_leader", 2), ("bug_log_matching", 3), ("bug_both", 2),
                                         ("messages_small", 2), ("bug_cand_term", 3)])
 def test_sharded_violation_and_trace(case, nproc, tmp_path):
