@@ -11,6 +11,6 @@ timeout -k 10 180 python tools/level_times.py $CFG ${CAP1:-1500000000} ${DEPTH:-
 RMC_DIST_REP=${REP:-1048576} RMC_DIST_DEBUG=1 OMP_NUM_THREADS=1 timeout -k 10 900 python -m torch.distributed.run \
   --nnodes=1 --nproc-per-node=8 --master-addr 127.0.0.1 --master-port 29808 tests/dist_worker.py \
   --cfg $CFG --out $O/dist8.json --device 0 --backend gloo --capacity ${CAP:-180000000} \
-  --keys-per-dest $((1 << 22)) --rerun 0 --max-depth ${DEPTH:-0} > $O/dist8.out 2> $O/dist8.err || exit 1
+  --keys-per-dest $((1 << 22)) --rerun ${RERUN:-0} --max-depth ${DEPTH:-0} > $O/dist8.out 2> $O/dist8.err || exit 1
 grep -h "\[rmc rank" $O/dist8.err > $O/rounds.txt
-python3 -c "import json; d=json.load(open('$O/dist8.json')); print(d['distinct'], d['generated'], d['depth'], d['keys_sent'], d['states_sent'])"
+python3 -c "import json; d=json.load(open('$O/dist8.json')); print(d['distinct'], d['generated'], d['depth'], d['keys_sent'], d['states_sent'], d['rerun'])"
